@@ -1,0 +1,136 @@
+// PyTorch custom-op bindings (TORCH_LIBRARY "dlion") for the gfx950 kernels.
+// Every op launches on the caller's current HIP stream, takes pre-built device
+// metadata (no host sync, no allocation: safe to capture in a hipGraph) and
+// refuses CPU tensors loudly -- there is deliberately no silent fallback here;
+// the pure-PyTorch oracle lives in ops/reference.py and is chosen explicitly.
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace {
+
+using at::Tensor;
+
+void check_dev(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "dlion: ", name, " must be a GPU (HIP) tensor");
+  TORCH_CHECK(t.is_contiguous(), "dlion: ", name, " must be contiguous");
+}
+
+void check_hip(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "dlion: ", what, " failed: ", hipGetErrorString(e));
+}
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void lion_local(const Tensor& meta, int64_t seg_off, int64_t chunk_off, int64_t n_chunks, int64_t dtype,
+                double decay, double neg_lr, double b1, double omb1, double b2, double omb2) {
+  check_dev(meta, "meta");
+  TORCH_CHECK(meta.scalar_type() == at::kLong, "dlion: meta must be int64");
+  const c10::DeviceGuard g(meta.device());
+  const int64_t* base = meta.data_ptr<int64_t>();
+  check_hip(dlion::launch_lion_local(static_cast<int>(dtype), base + seg_off, base + chunk_off, n_chunks,
+                                     static_cast<float>(decay), static_cast<float>(neg_lr), static_cast<float>(b1),
+                                     static_cast<float>(omb1), static_cast<float>(b2), static_cast<float>(omb2),
+                                     cur_stream()),
+            "lion_local");
+}
+
+void lion_encode(const Tensor& meta, int64_t seg_off, int64_t chunk_off, int64_t n_chunks, int64_t dtype,
+                 const Tensor& bits, double b1, double omb1, double b2, double omb2, bool update_m,
+                 bool stochastic, double rr, int64_t seed, int64_t step) {
+  check_dev(meta, "meta");
+  check_dev(bits, "bits");
+  TORCH_CHECK(bits.scalar_type() == at::kByte, "dlion: bits must be uint8");
+  const c10::DeviceGuard g(meta.device());
+  const int64_t* base = meta.data_ptr<int64_t>();
+  check_hip(dlion::launch_lion_encode(static_cast<int>(dtype), base + seg_off, base + chunk_off, n_chunks,
+                                      bits.data_ptr<uint8_t>(), static_cast<float>(b1), static_cast<float>(omb1),
+                                      static_cast<float>(b2), static_cast<float>(omb2), update_m ? 1 : 0,
+                                      stochastic ? 1 : 0, static_cast<float>(rr), static_cast<uint64_t>(seed),
+                                      static_cast<uint32_t>(step), cur_stream()),
+            "lion_encode");
+}
+
+void lion_vote_apply(const Tensor& meta, int64_t seg_off, int64_t chunk_off, int64_t n_chunks, int64_t dtype,
+                     const Tensor& planes, int64_t plane_stride, const Tensor& alive, int64_t mode, int64_t tie,
+                     const std::optional<Tensor>& neg, double decay, double neg_lr,
+                     const std::optional<Tensor>& own, const std::optional<Tensor>& agree) {
+  check_dev(meta, "meta");
+  check_dev(planes, "planes");
+  check_dev(alive, "alive");
+  TORCH_CHECK(planes.scalar_type() == at::kByte, "dlion: planes must be uint8");
+  TORCH_CHECK(alive.scalar_type() == at::kByte, "dlion: alive must be uint8");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "dlion: bad vote mode ", mode);
+  const uint8_t* negp = nullptr;
+  if (neg.has_value()) {
+    check_dev(*neg, "neg");
+    negp = neg->data_ptr<uint8_t>();
+  }
+  unsigned long long* agp = nullptr;
+  const uint8_t* ownp = nullptr;
+  if (agree.has_value()) {
+    TORCH_CHECK(own.has_value(), "dlion: vote agreement needs this rank's own bits");
+    check_dev(*own, "own");
+    ownp = own->data_ptr<uint8_t>();
+    check_dev(*agree, "agree");
+    TORCH_CHECK(agree->scalar_type() == at::kLong, "dlion: agree must be int64");
+    agp = reinterpret_cast<unsigned long long*>(agree->data_ptr<int64_t>());
+  }
+  const c10::DeviceGuard g(meta.device());
+  const int64_t* base = meta.data_ptr<int64_t>();
+  check_hip(dlion::launch_lion_vote_apply(static_cast<int>(dtype), base + seg_off, base + chunk_off, n_chunks,
+                                          planes.data_ptr<uint8_t>(), plane_stride, alive.data_ptr<uint8_t>(),
+                                          static_cast<int>(alive.numel()), static_cast<int>(mode),
+                                          static_cast<int>(tie), negp, static_cast<float>(decay),
+                                          static_cast<float>(neg_lr), ownp, agp,
+                                          cur_stream()),
+            "lion_vote_apply");
+}
+
+void vote_reduce(const Tensor& recv, int64_t nbytes, const Tensor& alive, int64_t tie, const Tensor& out,
+                 const std::optional<Tensor>& neg_out) {
+  check_dev(recv, "recv");
+  check_dev(alive, "alive");
+  check_dev(out, "out");
+  TORCH_CHECK(nbytes % 4 == 0, "dlion: vote_reduce shard bytes must be a multiple of 4");
+  TORCH_CHECK(out.numel() >= nbytes, "dlion: vote_reduce out too small");
+  TORCH_CHECK(recv.numel() >= nbytes * alive.numel(), "dlion: vote_reduce recv too small");
+  uint8_t* negp = nullptr;
+  if (neg_out.has_value()) {
+    check_dev(*neg_out, "neg_out");
+    negp = neg_out->data_ptr<uint8_t>();
+  }
+  const c10::DeviceGuard g(recv.device());
+  check_hip(dlion::launch_vote_reduce(recv.data_ptr<uint8_t>(), nbytes, alive.data_ptr<uint8_t>(),
+                                      static_cast<int>(alive.numel()), static_cast<int>(tie),
+                                      out.data_ptr<uint8_t>(), negp, cur_stream()),
+            "vote_reduce");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(dlion, m) {
+  m.def(
+      "lion_local(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, float decay, float neg_lr,"
+      " float b1, float omb1, float b2, float omb2) -> ()");
+  m.def(
+      "lion_encode(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, Tensor(a!) bits, float b1,"
+      " float omb1, float b2, float omb2, bool update_m, bool stochastic, float rr, int seed, int step) -> ()");
+  m.def(
+      "lion_vote_apply(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, Tensor planes,"
+      " int plane_stride, Tensor alive, int mode, int tie, Tensor? neg, float decay, float neg_lr,"
+      " Tensor? own, Tensor(b!)? agree) -> ()");
+  m.def("vote_reduce(Tensor recv, int nbytes, Tensor alive, int tie, Tensor(a!) out, Tensor(b!)? neg_out) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
+  m.impl("lion_local", &lion_local);
+  m.impl("lion_encode", &lion_encode);
+  m.impl("lion_vote_apply", &lion_vote_apply);
+  m.impl("vote_reduce", &vote_reduce);
+}

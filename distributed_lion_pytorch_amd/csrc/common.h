@@ -1,0 +1,145 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of distributed_lion_pytorch_amd.
+//
+// Everything here is written for a 64-lane wavefront and 16-byte-per-lane
+// vector memory access (cdna_hip_programming.md Guideline 13): bf16/fp16 are
+// moved as uint4 (8 elements), fp32 as two float4.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dlion {
+
+// dtype codes shared with the Python side (ops/hip.py::DTYPE_CODE)
+enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
+
+// ---------------------------------------------------------------- conversions
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(static_cast<uint32_t>(h) << 16);
+}
+
+// round-to-nearest-even, NaN preserved (quietened) -- identical to ATen's
+// c10::BFloat16 round_to_nearest_even so that bf16 results are bit-exact with
+// the PyTorch reference path.
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0u;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+
+__device__ __forceinline__ float f16_to_f32(uint16_t h) {
+  return static_cast<float>(__builtin_bit_cast(_Float16, h));
+}
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {
+  return __builtin_bit_cast(uint16_t, static_cast<_Float16>(f));  // RNE
+}
+
+// Element traits: storage type, load/store of 8 consecutive elements.
+template <int DT> struct Elem;
+
+template <> struct Elem<kF32> {
+  using S = float;
+  __device__ __forceinline__ static float to_f(S v) { return v; }
+  __device__ __forceinline__ static S from_f(float v) { return v; }
+  __device__ __forceinline__ static void load8(const S* p, float (&o)[8]) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0];
+    const float4 b = reinterpret_cast<const float4*>(p)[1];
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+    o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  }
+  __device__ __forceinline__ static void store8(S* p, const float (&o)[8]) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(o[0], o[1], o[2], o[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(o[4], o[5], o[6], o[7]);
+  }
+  // round-trip through storage precision (identity for f32)
+  __device__ __forceinline__ static float rnd(float v) { return v; }
+};
+
+template <int DT> struct Elem16 {
+  using S = uint16_t;
+  __device__ __forceinline__ static float to_f(S v) {
+    return DT == kBF16 ? bf16_to_f32(v) : f16_to_f32(v);
+  }
+  __device__ __forceinline__ static S from_f(float v) {
+    return DT == kBF16 ? f32_to_bf16(v) : f32_to_f16(v);
+  }
+  __device__ __forceinline__ static void load8(const S* p, float (&o)[8]) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[2 * i] = to_f(static_cast<S>(w[i] & 0xffffu));
+      o[2 * i + 1] = to_f(static_cast<S>(w[i] >> 16));
+    }
+  }
+  __device__ __forceinline__ static void store8(S* p, const float (&o)[8]) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      w[i] = static_cast<uint32_t>(from_f(o[2 * i])) |
+             (static_cast<uint32_t>(from_f(o[2 * i + 1])) << 16);
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  __device__ __forceinline__ static float rnd(float v) { return to_f(from_f(v)); }
+};
+template <> struct Elem<kBF16> : Elem16<kBF16> {};
+template <> struct Elem<kF16> : Elem16<kF16> {};
+
+// Load / store 8 elements starting at element e of a tensor with n elements.
+// `vec` says the tensor base is 16-B aligned and n % 8 == 0, so the fast path
+// is one (bf16) or two (f32) dwordx4 per lane; otherwise a guarded scalar path.
+template <int DT>
+__device__ __forceinline__ void load8g(const typename Elem<DT>::S* base, int64_t e, int64_t n,
+                                       bool vec, float (&o)[8]) {
+  if (vec) {
+    Elem<DT>::load8(base + e, o);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (e + j < n) ? Elem<DT>::to_f(base[e + j]) : 0.f;
+  }
+}
+template <int DT>
+__device__ __forceinline__ void store8g(typename Elem<DT>::S* base, int64_t e, int64_t n, bool vec,
+                                        const float (&o)[8]) {
+  if (vec) {
+    Elem<DT>::store8(base + e, o);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (e + j < n) base[e + j] = Elem<DT>::from_f(o[j]);
+  }
+}
+
+// ------------------------------------------------------------ vote counting
+// Spread the 8 bits of a byte into the 8 bytes of a u64 (bit j -> bit 8j), so
+// that summing spread bytes over W <= 255 ranks counts 8 votes in parallel.
+__device__ __forceinline__ uint64_t spread8(uint32_t b) {
+  uint64_t x = b & 0xffu;
+  x = (x | (x << 28)) & 0x0000000F0000000FULL;
+  x = (x | (x << 14)) & 0x0003000300030003ULL;
+  x = (x | (x << 7)) & 0x0101010101010101ULL;
+  return x;
+}
+
+// ------------------------------------------------------------- Philox4x32-10
+// Counter-based RNG for the stochastic-binarization encoder: every
+// (seed, element, step) triple gets an independent, reproducible draw.
+__device__ __forceinline__ uint4 philox4x32_10(uint4 ctr, uint2 key) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t hi0 = __umulhi(M0, ctr.x), lo0 = M0 * ctr.x;
+    const uint32_t hi1 = __umulhi(M1, ctr.z), lo1 = M1 * ctr.z;
+    ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+    key.x += W0;
+    key.y += W1;
+  }
+  return ctr;
+}
+__device__ __forceinline__ float u32_to_unit(uint32_t x) {
+  return static_cast<float>(x >> 8) * (1.0f / 16777216.0f);  // [0, 1)
+}
+
+}  // namespace dlion

@@ -1,0 +1,21 @@
+// Host-side launch entry points of the gfx950 kernels (implemented in *.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dlion {
+
+// ---- optimizer (lion_kernels.hip)
+hipError_t launch_lion_local(int dt, const int64_t* seg, const int64_t* chunks, int64_t n_chunks, float decay,
+                             float neg_lr, float b1, float omb1, float b2, float omb2, hipStream_t st);
+hipError_t launch_lion_encode(int dt, const int64_t* seg, const int64_t* chunks, int64_t n_chunks, uint8_t* bits,
+                              float b1, float omb1, float b2, float omb2, int update_m, int stochastic, float rr,
+                              uint64_t seed, uint32_t step, hipStream_t st);
+hipError_t launch_lion_vote_apply(int dt, const int64_t* seg, const int64_t* chunks, int64_t n_chunks,
+                                  const uint8_t* planes, int64_t plane_stride, const uint8_t* alive, int world,
+                                  int mode, int tie, const uint8_t* neg, float decay, float neg_lr, const uint8_t* own,
+                                  unsigned long long* agree, hipStream_t st);
+hipError_t launch_vote_reduce(const uint8_t* recv, int64_t nbytes, const uint8_t* alive, int world, int tie,
+                              uint8_t* out, uint8_t* neg_out, hipStream_t st);
+
+}  // namespace dlion

@@ -1,0 +1,327 @@
+// Distributed Lion optimizer kernels for gfx950 (MI355X / CDNA4).
+//
+// Replaces the per-parameter ATen chains of the reference optimizer
+// (/root/reference/distributed_lion.py:47-96, ~20 + 6*W launches and one
+// collective PER TENSOR) with multi-tensor kernels that touch every byte once:
+//
+//   K0 lion_local      p,g,m -> p,m           local Lion          (ref :47-59)
+//   K1 lion_encode     g,m   -> m, sign bits  WD-free interp+sign+1-bit pack
+//                                             + momentum EMA       (ref :64-77, :96)
+//   K3 (K1 with stochastic=1)                 stochastic binarization, Philox
+//                                                                  (ref :98-108)
+//   K2 lion_vote_apply p, W bit planes -> p   popcount majority / average vote
+//                                             + decoupled WD + step (ref :84-92)
+//   K4 vote_reduce     W shards -> voted bits  (all-to-all "vote-RS" scheme)
+//
+// Multi-tensor layout (built once per parameter set by parallel/plan.py):
+//   seg   [T][8] int64 : p_ptr, g_ptr, m_ptr, numel, bit_off, flags, 0, 0
+//   chunk [C][2] int64 : segment index, first element
+// A chunk is CHUNK=8192 elements (one 256-thread block, 4 iterations of 2048);
+// each tensor owns ceil(numel/2048)*2048 bits of the bucket's bit space, so the
+// packed bits of tensor t start at byte bit_off/8 and never straddle tensors.
+// Bit layout is little-endian "packbits": element e <-> byte e/8, bit e%8, i.e.
+// exactly the reference's wire encoding (ref :75-77) but 1 bit/param (the
+// reference promotes to int64, 8 bytes per 8 params).
+#include "common.h"
+
+namespace dlion {
+
+constexpr int kThreads = 256;
+constexpr int kIters = 4;
+constexpr int kSpan = kThreads * 8;        // 2048 elements per block iteration
+constexpr int64_t kChunk = kSpan * kIters;  // 8192 elements per block
+
+struct SegRow {
+  const void* p;
+  const void* g;
+  const void* m;
+  int64_t n;
+  int64_t bit_off;
+  bool vec;
+};
+
+__device__ __forceinline__ SegRow load_seg(const int64_t* __restrict__ seg, int64_t s) {
+  const int64_t* r = seg + 8 * s;
+  SegRow o;
+  o.p = reinterpret_cast<const void*>(r[0]);
+  o.g = reinterpret_cast<const void*>(r[1]);
+  o.m = reinterpret_cast<const void*>(r[2]);
+  o.n = r[3];
+  o.bit_off = r[4];
+  o.vec = (r[5] & 1) != 0;
+  return o;
+}
+
+__device__ __forceinline__ float sgn(float x) {  // ATen sign: NaN -> 0, +-0 -> 0
+  return static_cast<float>((x > 0.f) - (x < 0.f));
+}
+
+// ----------------------------------------------------------------------- K0
+template <int DT>
+__global__ void __launch_bounds__(kThreads)
+lion_local_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ chunks,
+                  float decay, float neg_lr, float b1, float omb1, float b2, float omb2) {
+  using E = Elem<DT>;
+  using S = typename E::S;
+  const int64_t s = chunks[2 * blockIdx.x], start = chunks[2 * blockIdx.x + 1];
+  const SegRow r = load_seg(seg, s);
+  S* p = const_cast<S*>(static_cast<const S*>(r.p));
+  const S* g = static_cast<const S*>(r.g);
+  S* m = const_cast<S*>(static_cast<const S*>(r.m));
+#pragma unroll
+  for (int it = 0; it < kIters; ++it) {
+    const int64_t e = start + it * kSpan + threadIdx.x * 8;
+    if (e >= r.n) break;
+    float pv[8], gv[8], mv[8];
+    load8g<DT>(p, e, r.n, r.vec, pv);
+    load8g<DT>(g, e, r.n, r.vec, gv);
+    load8g<DT>(m, e, r.n, r.vec, mv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float pw = E::rnd(pv[j] * decay);                       // p *= 1 - lr*wd
+      const float u = E::rnd(__fmaf_rn(gv[j], omb1, E::rnd(mv[j] * b1)));  // b1*m + (1-b1)*g
+      pv[j] = __fmaf_rn(neg_lr, sgn(u), pw);                         // p -= lr*sign(u)
+      mv[j] = __fmaf_rn(gv[j], omb2, E::rnd(mv[j] * b2));            // m = b2*m + (1-b2)*g
+    }
+    store8g<DT>(p, e, r.n, r.vec, pv);
+    store8g<DT>(m, e, r.n, r.vec, mv);
+  }
+}
+
+// ----------------------------------------------------------------- K1 / K3
+// bits: this rank's packed sign plane for the bucket (bucket-relative bit_off).
+// stochastic: bit = Bernoulli(clamp((u + rr) / (2 rr), 0, 1)) with
+//   rr = (1 + 1/b1) * max_grad_norm  (ref :106-108, clamped: SURVEY D4).
+template <int DT, bool STOC>
+__global__ void __launch_bounds__(kThreads)
+lion_encode_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ chunks,
+                   uint8_t* __restrict__ bits, float b1, float omb1, float b2, float omb2,
+                   int update_m, float rr, uint32_t seed_lo, uint32_t seed_hi, uint32_t step) {
+  using E = Elem<DT>;
+  using S = typename E::S;
+  const int64_t s = chunks[2 * blockIdx.x], start = chunks[2 * blockIdx.x + 1];
+  const SegRow r = load_seg(seg, s);
+  const S* g = static_cast<const S*>(r.g);
+  S* m = const_cast<S*>(static_cast<const S*>(r.m));
+  const int64_t region = (r.n + kSpan - 1) / kSpan * kSpan;
+#pragma unroll
+  for (int it = 0; it < kIters; ++it) {
+    const int64_t e = start + it * kSpan + threadIdx.x * 8;
+    if (e >= region) break;  // uniform per block iteration (region % 2048 == 0)
+    uint32_t byte = 0;
+    if (e < r.n) {
+      float gv[8], mv[8];
+      load8g<DT>(g, e, r.n, r.vec, gv);
+      load8g<DT>(m, e, r.n, r.vec, mv);
+      float u[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[j] = E::rnd(__fmaf_rn(gv[j], omb1, E::rnd(mv[j] * b1)));
+      if constexpr (STOC) {
+        const uint64_t gi = static_cast<uint64_t>(r.bit_off + e);  // unique per element
+        const uint4 c0 = philox4x32_10(
+            make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32), step, 0u),
+            make_uint2(seed_lo, seed_hi));
+        const uint4 c1 = philox4x32_10(
+            make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32), step, 1u),
+            make_uint2(seed_lo, seed_hi));
+        const uint32_t rnd[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float inv = 0.5f / rr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (e + j < r.n) {
+            const float pr = fminf(fmaxf((u[j] + rr) * inv, 0.f), 1.f);
+            byte |= static_cast<uint32_t>(u32_to_unit(rnd[j]) < pr) << j;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (e + j < r.n) byte |= static_cast<uint32_t>(u[j] > 0.f) << j;  // sign 0/NaN -> 0
+      }
+      if (update_m) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mv[j] = __fmaf_rn(gv[j], omb2, E::rnd(mv[j] * b2));
+        store8g<DT>(m, e, r.n, r.vec, mv);
+      }
+    }
+    bits[(r.bit_off + e) >> 3] = static_cast<uint8_t>(byte);
+  }
+}
+
+// ----------------------------------------------------------------------- K2
+// mode 0: majority vote over the alive planes  delta = +1 / -1 / tie rule
+// mode 1: average (paper's server "Averaging")  delta = (2c - n) / n
+// mode 2: pre-voted bitmap (vote-RS/AG path)    delta = pos ? +1 : (neg ? -1 : 0)
+//         planes = pos bitmap, neg = optional neg bitmap (nullptr -> ~pos)
+// tie: 0 -> -1 (reference parity: torch.mode tie -> False), 1 -> 0, 2 -> +1
+// p <- round(round(p * decay) - lr * delta)   (ref :64 then :92)
+// agree (optional): count of coordinates where this rank's own bits (`own`,
+// its send plane) agree with the voted direction (vote-agreement telemetry).
+template <int DT>
+__global__ void __launch_bounds__(kThreads)
+lion_vote_apply_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ chunks,
+                       const uint8_t* __restrict__ planes, int64_t plane_stride,
+                       const uint8_t* __restrict__ alive, int world, int mode, int tie,
+                       const uint8_t* __restrict__ neg, float decay, float neg_lr,
+                       const uint8_t* __restrict__ own, unsigned long long* __restrict__ agree) {
+  using E = Elem<DT>;
+  using S = typename E::S;
+  const int64_t s = chunks[2 * blockIdx.x], start = chunks[2 * blockIdx.x + 1];
+  const SegRow r = load_seg(seg, s);
+  S* p = const_cast<S*>(static_cast<const S*>(r.p));
+  const float tie_delta = tie == 0 ? -1.f : (tie == 1 ? 0.f : 1.f);
+  int n_live = 0;  // liveness is a device vector: no host sync to learn who voted
+  for (int k = 0; k < world; ++k) n_live += alive[k] != 0;
+  const float inv_n = n_live > 0 ? 1.f / static_cast<float>(n_live) : 0.f;
+  uint32_t n_agree = 0;
+#pragma unroll
+  for (int it = 0; it < kIters; ++it) {
+    const int64_t e = start + it * kSpan + threadIdx.x * 8;
+    if (e >= r.n) break;
+    const int64_t byte_idx = (r.bit_off + e) >> 3;
+    float delta[8];
+    if (mode == 2) {
+      const uint32_t pos = planes[byte_idx];
+      const uint32_t ng = neg ? neg[byte_idx] : (~pos & 0xffu);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        delta[j] = ((pos >> j) & 1) ? 1.f : (((ng >> j) & 1) ? -1.f : 0.f);
+    } else {
+      uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int r0 = 0; r0 < world; r0 += 255) {
+        const int r1 = min(world, r0 + 255);
+        uint64_t acc = 0;
+        for (int k = r0; k < r1; ++k)
+          if (alive[k]) acc += spread8(planes[k * plane_stride + byte_idx]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cnt[j] += static_cast<uint32_t>((acc >> (8 * j)) & 0xffu);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int twice = 2 * static_cast<int>(cnt[j]);
+        if (n_live == 0)
+          delta[j] = 0.f;  // nobody voted: weight decay only
+        else if (mode == 1)
+          delta[j] = static_cast<float>(twice - n_live) * inv_n;
+        else
+          delta[j] = twice > n_live ? 1.f : (twice < n_live ? -1.f : tie_delta);
+      }
+    }
+    if (agree != nullptr) {
+      const uint32_t mine = own[byte_idx];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (e + j < r.n) n_agree += (((mine >> j) & 1) ? 1.f : -1.f) * delta[j] > 0.f;
+    }
+    float pv[8];
+    load8g<DT>(p, e, r.n, r.vec, pv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pv[j] = __fmaf_rn(neg_lr, delta[j], E::rnd(pv[j] * decay));
+    store8g<DT>(p, e, r.n, r.vec, pv);
+  }
+  if (agree != nullptr) {
+    // wave reduce then one atomic per wave (Guideline 12)
+    for (int off = 32; off > 0; off >>= 1) n_agree += __shfl_xor(n_agree, off);
+    if ((threadIdx.x & 63) == 0) atomicAdd(agree, static_cast<unsigned long long>(n_agree));
+  }
+}
+
+// ----------------------------------------------------------------------- K4
+// recv: [W][nbytes] shards gathered by all_to_all; out: voted positive bits;
+// neg_out (optional): voted negative bits (only needed when ties map to 0).
+// 4 bytes (32 coordinates) per thread, grid-stride.
+__global__ void __launch_bounds__(kThreads)
+vote_reduce_kernel(const uint8_t* __restrict__ recv, int64_t nbytes, const uint8_t* __restrict__ alive,
+                   int world, int tie, uint8_t* __restrict__ out, uint8_t* __restrict__ neg_out) {
+  const int64_t nwords = nbytes >> 2;  // nbytes % 4 == 0 guaranteed by the planner
+  int n_live = 0;
+  for (int k = 0; k < world; ++k) n_live += alive[k] != 0;
+  for (int64_t w = blockIdx.x * (int64_t)kThreads + threadIdx.x; w < nwords;
+       w += (int64_t)gridDim.x * kThreads) {
+    uint32_t cnt[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) cnt[j] = 0;
+    for (int r0 = 0; r0 < world; r0 += 255) {
+      const int r1 = min(world, r0 + 255);
+      uint64_t acc[4] = {0, 0, 0, 0};
+      for (int k = r0; k < r1; ++k) {
+        if (!alive[k]) continue;
+        const uint32_t v = reinterpret_cast<const uint32_t*>(recv + k * nbytes)[w];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[b] += spread8(v >> (8 * b));
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cnt[8 * b + j] += static_cast<uint32_t>((acc[b] >> (8 * j)) & 0xffu);
+    }
+    uint32_t pos = 0, ng = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const int twice = 2 * static_cast<int>(cnt[j]);
+      const bool is_pos = n_live > 0 && (twice > n_live || (twice == n_live && tie == 2));
+      const bool is_neg = n_live > 0 && (twice < n_live || (twice == n_live && tie == 0));
+      pos |= static_cast<uint32_t>(is_pos) << j;
+      ng |= static_cast<uint32_t>(is_neg) << j;
+    }
+    reinterpret_cast<uint32_t*>(out)[w] = pos;
+    if (neg_out != nullptr) reinterpret_cast<uint32_t*>(neg_out)[w] = ng;
+  }
+}
+
+// ------------------------------------------------------------ host launchers
+#define DLION_DISPATCH(dt, ...)                         \
+  switch (dt) {                                         \
+    case kF32: { constexpr int DT = kF32; __VA_ARGS__; break; } \
+    case kBF16: { constexpr int DT = kBF16; __VA_ARGS__; break; } \
+    case kF16: { constexpr int DT = kF16; __VA_ARGS__; break; } \
+    default: return hipErrorInvalidValue;               \
+  }
+
+hipError_t launch_lion_local(int dt, const int64_t* seg, const int64_t* chunks, int64_t n_chunks,
+                             float decay, float neg_lr, float b1, float omb1, float b2, float omb2,
+                             hipStream_t st) {
+  if (n_chunks == 0) return hipSuccess;
+  DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_local_kernel<DT>), dim3(n_chunks), dim3(kThreads), 0, st,
+                                        seg, chunks, decay, neg_lr, b1, omb1, b2, omb2));
+  return hipGetLastError();
+}
+
+hipError_t launch_lion_encode(int dt, const int64_t* seg, const int64_t* chunks, int64_t n_chunks,
+                              uint8_t* bits, float b1, float omb1, float b2, float omb2, int update_m,
+                              int stochastic, float rr, uint64_t seed, uint32_t step, hipStream_t st) {
+  if (n_chunks == 0) return hipSuccess;
+  const uint32_t lo = static_cast<uint32_t>(seed), hi = static_cast<uint32_t>(seed >> 32);
+  if (stochastic) {
+    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_encode_kernel<DT, true>), dim3(n_chunks), dim3(kThreads), 0,
+                                          st, seg, chunks, bits, b1, omb1, b2, omb2, update_m, rr, lo, hi, step));
+  } else {
+    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_encode_kernel<DT, false>), dim3(n_chunks), dim3(kThreads), 0,
+                                          st, seg, chunks, bits, b1, omb1, b2, omb2, update_m, rr, lo, hi, step));
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_lion_vote_apply(int dt, const int64_t* seg, const int64_t* chunks, int64_t n_chunks,
+                                  const uint8_t* planes, int64_t plane_stride, const uint8_t* alive, int world,
+                                  int mode, int tie, const uint8_t* neg, float decay, float neg_lr,
+                                  const uint8_t* own, unsigned long long* agree, hipStream_t st) {
+  if (n_chunks == 0) return hipSuccess;
+  DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_vote_apply_kernel<DT>), dim3(n_chunks), dim3(kThreads), 0, st,
+                                        seg, chunks, planes, plane_stride, alive, world, mode, tie, neg, decay,
+                                        neg_lr, own, agree));
+  return hipGetLastError();
+}
+
+hipError_t launch_vote_reduce(const uint8_t* recv, int64_t nbytes, const uint8_t* alive, int world, int tie,
+                              uint8_t* out, uint8_t* neg_out, hipStream_t st) {
+  const int64_t nwords = nbytes >> 2;
+  if (nwords == 0) return hipSuccess;
+  int64_t blocks = (nwords + kThreads - 1) / kThreads;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(vote_reduce_kernel, dim3(blocks), dim3(kThreads), 0, st, recv, nbytes, alive, world, tie,
+                     out, neg_out);
+  return hipGetLastError();
+}
+
+}  // namespace dlion
