@@ -1,0 +1,212 @@
+#!/usr/bin/env python
+"""Headline benchmark: GPT-2 small CLM training with Distributed Lion.
+
+Metric (BASELINE.json): tokens/sec (whole job) + vote wire bytes per step,
+GPT-2 CLM at 1/2/4/8 MI355X.  Config = the reference's README run
+(/root/reference/README.md:20-37): GPT-2 small (124M, `--config_name gpt2`,
+random init), bf16 weights (`--torch_dtype bfloat16`), per-device batch 20,
+block size 1024, gradient accumulation 8, Lion lr 1e-4 / wd 0.1, async grads
+(no gradient all-reduce), HF-default local grad clipping at 1.0, dropout 0.1.
+Data is synthetic (random token ids of that shape; no network).
+
+  python bench.py --gpus N --steps K --warmup W
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Every step is a full training step (8 micro-batches fwd+bwd, clip, vote
+exchange over RCCL, Lion update).  Rank 0 prints one JSON line.
+`--impl reference` runs the reference algorithm on the same hardware (HF
+GPT2LMHeadModel + per-tensor int64 all_gather Lion) for an A/B comparison.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from distributed_lion_pytorch_amd import Lion  # noqa: E402
+from distributed_lion_pytorch_amd.models.gpt2 import GPT2Config, GPT2LMHeadModel  # noqa: E402
+from distributed_lion_pytorch_amd.parallel.exchange import wire_bytes_per_step  # noqa: E402
+from distributed_lion_pytorch_amd.trainer.engine import StepTimer, TrainStep, broadcast_parameters  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="gpt2")
+    ap.add_argument("--micro_batch", type=int, default=20)
+    ap.add_argument("--seq_len", type=int, default=1024)
+    ap.add_argument("--grad_accum", type=int, default=8)
+    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--weight_decay", type=float, default=0.1)
+    ap.add_argument("--max_grad_norm", type=float, default=1.0)
+    ap.add_argument("--exchange", default="a2a", help="allgather | a2a | ref_int64")
+    ap.add_argument("--bucket_mb", type=float, default=32.0)
+    ap.add_argument("--impl", default="native", choices=["native", "reference"])
+    ap.add_argument("--fused", default="auto", choices=["auto", "torch", "hip"])
+    ap.add_argument("--dropout", type=float, default=None, help="override GPT-2 dropout (default 0.1)")
+    ap.add_argument("--profile_dir", default=None)
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    return world, rank, dev
+
+
+def build_native(args, dev):
+    from distributed_lion_pytorch_amd.ops import fused
+
+    fused.set_impl(args.fused)
+    cfg = GPT2Config.from_name(args.model)
+    if args.dropout is not None:
+        cfg.resid_pdrop = cfg.embd_pdrop = cfg.attn_pdrop = args.dropout
+    torch.manual_seed(0)
+    model = GPT2LMHeadModel(cfg).to(device=dev, dtype=torch.bfloat16)
+    broadcast_parameters(model)
+    opt = Lion(model.parameters(), lr=args.lr, weight_decay=args.weight_decay, exchange=args.exchange,
+               bucket_mb=args.bucket_mb)
+    return model, opt, cfg
+
+
+def build_reference(args, dev):
+    """HF GPT2LMHeadModel + the reference optimizer algorithm (per-tensor
+    int64 all_gather, ATen ops) -- the reference's behaviour on MI355X."""
+    import transformers
+
+    from distributed_lion_pytorch_amd.ops import reference as ref
+
+    cfg = GPT2Config.from_name(args.model)
+    hf_cfg = transformers.GPT2Config(**{k: v for k, v in cfg.to_hf_dict().items() if k != "architectures"})
+    torch.manual_seed(0)
+    model = transformers.GPT2LMHeadModel(hf_cfg).to(device=dev, dtype=torch.bfloat16)
+    broadcast_parameters(model)
+
+    class RefLion(torch.optim.Optimizer):
+        def __init__(self, params, lr, weight_decay):
+            super().__init__(params, dict(lr=lr, betas=(0.9, 0.99), weight_decay=weight_decay))
+
+        @torch.no_grad()
+        def step(self):
+            distributed = dist.is_initialized() and dist.get_world_size() > 1
+            for g in self.param_groups:
+                for p in g["params"]:
+                    if p.grad is None:
+                        continue
+                    st = self.state[p]
+                    if not st:
+                        st["exp_avg"] = torch.zeros_like(p)
+                    args_ = (p, p.grad, st["exp_avg"], g["lr"], g["weight_decay"], *g["betas"])
+                    if distributed:
+                        ref.update_fn_distributed(*args_, wire_dtype=torch.int64)
+                    else:
+                        ref.update_fn(*args_)
+
+    opt = RefLion(model.parameters(), args.lr, args.weight_decay)
+    return model, opt, cfg
+
+
+def main():
+    args = parse()
+    world, rank, dev = setup_dist(args)
+    build = build_native if args.impl == "native" else build_reference
+    model, opt, cfg = build(args, dev)
+    n_params = sum({p.data_ptr(): p.numel() for p in model.parameters()}.values())
+
+    if args.impl == "native":
+        loss_fn = None
+    else:
+        def loss_fn(m, b):
+            return m(input_ids=b["input_ids"], labels=b["labels"]).loss
+
+    step = TrainStep(model, opt, grad_accum=args.grad_accum, max_grad_norm=args.max_grad_norm, loss_fn=loss_fn)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+
+    def batches():
+        for _ in range(args.grad_accum):
+            ids = torch.randint(0, cfg.vocab_size, (args.micro_batch, args.seq_len), device=dev, generator=gen)
+            yield {"input_ids": ids, "labels": ids}
+
+    for _ in range(args.warmup):
+        step(batches())
+    timer = StepTimer(dev)
+    prof = None
+    if args.profile_dir and rank == 0:
+        prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
+                                                  torch.profiler.ProfilerActivity.CUDA])
+        prof.__enter__()
+    with timer:
+        for _ in range(args.steps):
+            loss = step(batches())
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        os.makedirs(args.profile_dir, exist_ok=True)
+        prof.export_chrome_trace(os.path.join(args.profile_dir, "trace.json"))
+        with open(os.path.join(args.profile_dir, "top_kernels.txt"), "w") as f:
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40))
+    elapsed = torch.tensor([timer.elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    tokens = world * args.grad_accum * args.micro_batch * args.seq_len * args.steps
+    tps = tokens / elapsed
+    ms = 1000.0 * elapsed / args.steps
+    stats = opt.stats() if hasattr(opt, "stats") else {}
+    exchange = args.exchange if args.impl == "native" else "ref_int64"
+    wire = wire_bytes_per_step(n_params, world, exchange)
+    if rank == 0:
+        out = {
+            "metric": "tokens/sec + all-reduce bytes/step, GPT-2 CLM at 1/2/4/8 MI355X",
+            "value": round(tps, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random token ids, GPT-2 vocab), random-init weights",
+            "config": {
+                "model": f"{args.model} ({n_params / 1e6:.1f}M params)",
+                "global_batch": world * args.grad_accum * args.micro_batch,
+                "micro_batch": args.micro_batch,
+                "grad_accum": args.grad_accum,
+                "seq_len": args.seq_len,
+                "parallelism": f"dp{world}",
+                "optimizer": "distributed Lion (majority vote), lr 1e-4, wd 0.1",
+                "exchange": exchange,
+                "impl": args.impl,
+            },
+            "wire_bytes_per_step_per_rank": wire,
+            "bf16_allreduce_bytes_per_step_per_rank": 0 if world == 1 else int(2 * (world - 1) / world * 2 * n_params),
+            "loss": round(float(loss.item()), 4),
+            "optimizer_stats": stats,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

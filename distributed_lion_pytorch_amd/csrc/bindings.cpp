@@ -112,9 +112,35 @@ void vote_reduce(const Tensor& recv, int64_t nbytes, const Tensor& alive, int64_
             "vote_reduce");
 }
 
+int dtype_code(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kHalf: return 2;
+    default: TORCH_CHECK(false, "dlion: unsupported dtype ", t);
+  }
+  return -1;
+}
+
+Tensor softmax_xent_(const Tensor& logits, const Tensor& labels, int64_t v) {
+  check_dev(logits, "logits");
+  check_dev(labels, "labels");
+  TORCH_CHECK(logits.dim() == 2, "dlion: logits must be [N, Vpad]");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == logits.size(0), "dlion: labels must be int64[N]");
+  TORCH_CHECK(logits.size(1) % 8 == 0 && v <= logits.size(1), "dlion: padded vocab must be a multiple of 8");
+  const c10::DeviceGuard g(logits.device());
+  auto loss = at::empty({logits.size(0)}, logits.options().dtype(at::kFloat));
+  check_hip(dlion::launch_softmax_xent(dtype_code(logits.scalar_type()), logits.data_ptr(), labels.data_ptr<int64_t>(),
+                                       logits.size(0), logits.size(1), static_cast<int>(v), loss.data_ptr<float>(),
+                                       cur_stream()),
+            "softmax_xent");
+  return loss;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dlion, m) {
+  m.def("softmax_xent_(Tensor(a!) logits, Tensor labels, int v) -> Tensor");
   m.def(
       "lion_local(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, float decay, float neg_lr,"
       " float b1, float omb1, float b2, float omb2) -> ()");
@@ -133,4 +159,5 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("lion_encode", &lion_encode);
   m.impl("lion_vote_apply", &lion_vote_apply);
   m.impl("vote_reduce", &vote_reduce);
+  m.impl("softmax_xent_", &softmax_xent_);
 }

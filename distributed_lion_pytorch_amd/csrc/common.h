@@ -31,8 +31,32 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
 __device__ __forceinline__ float f16_to_f32(uint16_t h) {
   return static_cast<float>(__builtin_bit_cast(_Float16, h));
 }
+// Integer round-to-nearest-even f32 -> f16.  Deliberately not
+// static_cast<_Float16>: hipcc is free to fold a (float)(half)x round trip
+// into mixed-precision FMAs, which broke bit-parity with ATen (measured:
+// tools/probe_fp16.py, 476 / 300k momentum mismatches).
 __device__ __forceinline__ uint16_t f32_to_f16(float f) {
-  return __builtin_bit_cast(uint16_t, static_cast<_Float16>(f));  // RNE
+  const uint32_t x = __float_as_uint(f);
+  const uint32_t sign = (x >> 16) & 0x8000u;
+  const uint32_t ax = x & 0x7fffffffu;
+  if (ax > 0x7f800000u) return static_cast<uint16_t>(sign | 0x7e00u);  // NaN
+  if (ax >= 0x47800000u) return static_cast<uint16_t>(sign | 0x7c00u);  // >= 2^16 (and inf) -> inf
+  if (ax < 0x33000000u) return static_cast<uint16_t>(sign);             // < 2^-25 -> 0
+  const uint32_t e = ax >> 23;
+  uint32_t h, rem, halfway;
+  if (e >= 113) {  // normal half
+    h = ((e - 112) << 10) | ((ax & 0x7fffffu) >> 13);
+    rem = ax & 0x1fffu;
+    halfway = 0x1000u;
+  } else {  // subnormal half: round(mant24 * 2^(e - 126))
+    const uint32_t mant = (ax & 0x7fffffu) | 0x800000u;
+    const uint32_t shift = 126 - e;  // 14..24
+    h = mant >> shift;
+    rem = mant & ((1u << shift) - 1u);
+    halfway = 1u << (shift - 1u);
+  }
+  if (rem > halfway || (rem == halfway && (h & 1u))) ++h;  // carry into the exponent is correct
+  return static_cast<uint16_t>(sign | h);
 }
 
 // Element traits: storage type, load/store of 8 consecutive elements.

@@ -18,4 +18,8 @@ hipError_t launch_lion_vote_apply(int dt, const int64_t* seg, const int64_t* chu
 hipError_t launch_vote_reduce(const uint8_t* recv, int64_t nbytes, const uint8_t* alive, int world, int tie,
                               uint8_t* out, uint8_t* neg_out, hipStream_t st);
 
+// ---- LM head cross-entropy (xent_kernels.hip)
+hipError_t launch_softmax_xent(int dt, void* logits, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,
+                               hipStream_t st);
+
 }  // namespace dlion

@@ -1,0 +1,149 @@
+"""Fused model ops with a gfx950 fast path and a PyTorch fallback.
+
+Every function here is the single entry point the native models use; the
+implementation is chosen per call:
+
+* on a GPU tensor the hand-written HIP kernels from ``_dlion_C.so`` run (the
+  extension is *required* on a GPU box -- see ops/hip.py);
+* on CPU tensors (unit tests, gloo runs) a plain PyTorch composition with the
+  same semantics runs.
+
+``set_impl("torch")`` forces the PyTorch path everywhere (A/B benchmarks).
+"""
+from __future__ import annotations
+
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import hip
+
+_IMPL = {"mode": os.environ.get("DLION_FUSED_IMPL", "auto")}  # auto | torch | hip
+
+
+def set_impl(mode: str) -> None:
+    if mode not in ("auto", "torch", "hip"):
+        raise ValueError(mode)
+    _IMPL["mode"] = mode
+
+
+def get_impl() -> str:
+    return _IMPL["mode"]
+
+
+def _use_hip(t: torch.Tensor) -> bool:
+    mode = _IMPL["mode"]
+    if mode == "torch" or not t.is_cuda:
+        return False
+    if mode == "hip" or not hip.fallback_allowed():
+        hip.require()
+        return True
+    return hip.available()
+
+
+# ---------------------------------------------------------------- layer norm
+def layer_norm(x: torch.Tensor, ln: torch.nn.LayerNorm) -> torch.Tensor:
+    return F.layer_norm(x, ln.normalized_shape, ln.weight, ln.bias, ln.eps)
+
+
+# ------------------------------------------------------------- dropout + add
+def dropout_add(y: torch.Tensor, residual: torch.Tensor, p: float) -> torch.Tensor:
+    if p > 0.0:
+        y = F.dropout(y, p, True)
+    return residual + y
+
+
+# --------------------------------------------------------------- bias + GELU
+def linear_gelu(x2d: torch.Tensor, w_in_out: torch.Tensor, bias: torch.Tensor, exact: bool = False):
+    """gelu(x @ W + b) with HF Conv1D's [in, out] weight layout."""
+    h = torch.addmm(bias, x2d, w_in_out)
+    return F.gelu(h, approximate="none" if exact else "tanh")
+
+
+# ------------------------------------------------------------------ attention
+def causal_attention(qkv: torch.Tensor, dropout_p: float) -> torch.Tensor:
+    """qkv: [B, T, 3, H, D] -> causal softmax attention output [B, T, H*D]."""
+    B, T, _, H, D = qkv.shape
+    q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)  # [B, H, T, D] views
+    y = F.scaled_dot_product_attention(q, k, v, dropout_p=dropout_p, is_causal=True)
+    return y.transpose(1, 2).reshape(B, T, H * D)
+
+
+# ------------------------------------------------- LM head + cross-entropy
+def _pad_rows(w: torch.Tensor, mult: int = 64) -> torch.Tensor:
+    v = w.shape[0]
+    vp = (v + mult - 1) // mult * mult
+    if vp == v:
+        return w
+    return torch.cat([w, w.new_zeros(vp - v, w.shape[1])], 0)
+
+
+class _LMHeadCE(torch.autograd.Function):
+    """loss = mean_{labels != -100} CE(h @ W^T, labels), gradients computed in
+    the forward pass (the loss gradient is a scalar multiple of
+    softmax - onehot), so the [N, V] logits never persist and never exist in
+    fp32.  The vocabulary is padded to a multiple of 64 for aligned rows and
+    well-shaped GEMMs; padded columns are masked out of the softmax."""
+
+    @staticmethod
+    def forward(ctx, h2d, weight, labels1d):
+        v = weight.shape[0]
+        need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        wp = _pad_rows(weight)
+        logits = h2d @ wp.t()  # [N, Vp] in the compute dtype (hipBLASLt)
+        valid = labels1d != -100
+        n_valid = valid.sum().clamp_min(1).to(torch.float32)
+        if _use_hip(logits):
+            row_loss = hip.ops().softmax_xent_(logits, labels1d, v)  # logits <- softmax - onehot (in place)
+        else:
+            row_loss = _softmax_xent_torch_(logits, labels1d, v)
+        loss = row_loss.sum() / n_valid
+        if need_grad:
+            dh = logits @ wp  # [N, C]
+            dw = (logits.t() @ h2d)[:v] if ctx.needs_input_grad[1] else None
+            ctx.save_for_backward(dh, dw if dw is not None else dh.new_empty(0), n_valid)
+            ctx.has_dw = dw is not None
+        del logits
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        dh, dw, n_valid = ctx.saved_tensors
+        scale = (g / n_valid).to(dh.dtype)
+        gh = dh * scale if ctx.needs_input_grad[0] else None
+        gw = dw * scale if ctx.has_dw and ctx.needs_input_grad[1] else None
+        return gh, gw, None
+
+
+def _softmax_xent_torch_(logits: torch.Tensor, labels: torch.Tensor, v: int) -> torch.Tensor:
+    """In-place reference of the HIP kernel: logits[:, :v] <- softmax - onehot
+    (zero rows for ignored labels, zero padded columns); returns fp32 row loss."""
+    x = logits[:, :v].float()
+    lse = torch.logsumexp(x, dim=1)
+    valid = labels != -100
+    safe = labels.clamp_min(0)
+    tgt = x.gather(1, safe[:, None]).squeeze(1)
+    row_loss = torch.where(valid, lse - tgt, torch.zeros_like(lse))
+    prob = torch.exp(x - lse[:, None])
+    prob.scatter_add_(1, safe[:, None], -torch.ones_like(tgt)[:, None])
+    prob[~valid] = 0.0
+    logits[:, :v] = prob.to(logits.dtype)
+    if logits.shape[1] > v:
+        logits[:, v:] = 0
+    return row_loss
+
+
+def lm_head_cross_entropy(h: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """Mean token cross-entropy of ``h @ weight.T`` against ``labels`` (-100 ignored)."""
+    h2d = h.reshape(-1, h.shape[-1])
+    return _LMHeadCE.apply(h2d, weight, labels.reshape(-1))
+
+
+def reference_lm_loss(h, weight, labels):
+    """Unfused reference (HF semantics) used by tests."""
+    logits = (h.reshape(-1, h.shape[-1]) @ weight.t()).float()
+    return F.cross_entropy(logits, labels.reshape(-1), ignore_index=-100)
+
+

@@ -35,9 +35,15 @@ def _clone(ts):
     return [t.clone() for t in ts]
 
 
-def _assert_close(a, b, dtype):
+def _assert_close(a, b, dtype, exact=True):
+    """bf16: bit-exact with ATen-HIP (fma with fp32 alpha, RNE after every op;
+    tools/probe_aten_numerics.py).  fp32: fp32 fma ordering may differ by an
+    ulp.  fp16 and the fractional `average` deltas: within one ulp."""
     if dtype == torch.float32:
         torch.testing.assert_close(a, b, rtol=2e-7, atol=1e-7)
+    elif dtype == torch.float16 or not exact:
+        torch.testing.assert_close(a.float(), b.float(), rtol=1e-3 if dtype == torch.float16 else 8e-3, atol=1e-5)
+        assert (a != b).float().mean().item() < 1e-3
     else:
         assert torch.equal(a, b), (a - b).abs().max()
 
@@ -115,7 +121,7 @@ def test_vote_apply_kernel_fake_voters(dtype, world, mode, tie, cuda):
         tx.apply(None, b2, pl, b.nbytes, alive, mode, tie, None, hp, own=own, agree=agree_t)
     torch.cuda.synchronize()
     for a, b in zip(ps, p2):
-        _assert_close(a, b, dtype)
+        _assert_close(a, b, dtype, exact=mode != ref.VOTE_AVERAGE)
     assert agree.item() == agree_t.item()
 
 
