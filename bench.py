@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--fused", default="auto", choices=["auto", "torch", "hip"])
     ap.add_argument("--dropout", type=float, default=None, help="override GPT-2 dropout (default 0.1)")
     ap.add_argument("--profile_dir", default=None)
+    ap.add_argument("--rocm_fa", default=None, help="PyTorch SDPA flash library on ROCm: ck | aotriton")
     return ap.parse_args()
 
 
@@ -126,6 +127,8 @@ def build_reference(args, dev):
 def main():
     args = parse()
     world, rank, dev = setup_dist(args)
+    if args.rocm_fa:
+        torch.backends.cuda.preferred_rocm_fa_library(args.rocm_fa)
     build = build_native if args.impl == "native" else build_reference
     model, opt, cfg = build(args, dev)
     n_params = sum({p.data_ptr(): p.numel() for p in model.parameters()}.values())

@@ -1,0 +1,38 @@
+// Argument block of the gfx950 flash-attention kernels (attention.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dlion {
+
+struct AttnArgs {
+  const __bf16* q;
+  const __bf16* k;
+  const __bf16* v;
+  const __bf16* o;
+  const __bf16* dout;
+  const __bf16* qt;   // [B][H][D][T]   (bwd dKV)
+  const __bf16* kt;   // [B][Hkv][D][T] (bwd dQ)
+  const __bf16* vt;   // [B][Hkv][D][T] (fwd)
+  const __bf16* dot;  // [B][H][D][T]   (bwd dKV)
+  __bf16* out;        // fwd O
+  __bf16* dq;
+  __bf16* dk;
+  __bf16* dv;
+  float* lse;          // [B][H][T] base-2 log-sum-exp of scaled scores
+  const float* delta;  // [B][H][T] rowsum(dO * O)
+  int64_t q_sb, q_st, q_sh;
+  int64_t k_sb, k_st, k_sh;
+  int64_t v_sb, v_st, v_sh;
+  int64_t o_sb, o_st, o_sh;    // O and dO share this layout
+  int64_t dq_sb, dq_st, dq_sh;
+  int64_t dk_sb, dk_st, dk_sh;  // dK and dV share this layout
+  int B, T, H, Hkv;
+  float scale;       // softmax scale (1/sqrt(D))
+  float scale_log2;  // scale * log2(e)
+  uint32_t thresh16; // dropout threshold (keep if u16 >= thresh16), 0 = no dropout
+  float inv_keep;
+  uint32_t seed;
+};
+
+}  // namespace dlion

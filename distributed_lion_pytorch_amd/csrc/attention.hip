@@ -1,0 +1,439 @@
+// Causal flash attention (forward + backward, optional dropout) for gfx950.
+//
+// Replaces PyTorch SDPA (aotriton on ROCm) plus the layout copies around it
+// (q/k/v unbind + stack in backward, output transpose) in the GPT-2/Llama
+// blocks.  Inputs are read in their native strided layout ([B,T,3,H,D] packed
+// qkv for GPT-2, separate [B,T,H,D] / [B,T,Hkv,D] for Llama GQA) and the
+// gradients are written straight into the packed dqkv layout.
+//
+// Design (cdna_hip_programming.md §3 "accumulator tile as the next MFMA's
+// operand"): every wave owns one 32x32 tile pair and uses
+// v_mfma_f32_32x32x16_bf16 only.  Scores are computed TRANSPOSED,
+// S^T = K Q^T, so the accumulator has the query on the lane and 16 keys in
+// registers: the softmax row-reduction is 15 in-register ops + one
+// cross-half shuffle, and P^T feeds O^T += V^T P^T with no lane movement.
+// The permuted-k operand (V^T rows) comes from a V^T copy in HBM (two 8-byte
+// loads per fragment).  Backward uses two kernels without atomics:
+//   dKV: per 32-key tile, S = Q K^T orientation (key on the lane), loops over
+//        query tiles accumulating dV += Pd^T dO and dK += dS^T Q in registers;
+//   dQ : per 32-query tile, forward orientation, dQ += dS K.
+// Dropout: keep(q, key) is a stateless hash of (seed, b*H+h, q, key) with
+// 16-bit resolution, so forward and both backward kernels regenerate the
+// identical mask in any register layout.
+#include "common.h"
+#include "attention.h"
+
+namespace dlion {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+
+
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// 32 random bits shared by keys (2i, 2i+1) of query q; key & 1 picks the half
+__device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint32_t bh, uint32_t q, uint32_t key) {
+  return lowbias32(seed ^ (bh * 0x9E3779B9u) ^ (q * 0x85EBCA6Bu) ^ ((key >> 1) * 0xC2B2AE35u));
+}
+__device__ __forceinline__ bool drop_keep(uint32_t hash, uint32_t key, uint32_t thresh16) {
+  return ((hash >> ((key & 1u) * 16u)) & 0xffffu) >= thresh16;
+}
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8 ld8(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+// permuted-k fragment: elements 0..3 from p[0..3], 4..7 from p[8..11]
+__device__ __forceinline__ bf16x8 ld4x2(const __bf16* p) {
+  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(p);
+  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(p + 8);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+// accumulator registers 8s..8s+7 as a bf16 operand fragment (k-step s)
+__device__ __forceinline__ bf16x8 acc_frag(const f32x16& x, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = static_cast<__bf16>(x[8 * s + j]);
+  return r;
+}
+__device__ __forceinline__ int acc_row(int reg, int hf) { return (reg & 3) + 8 * (reg >> 2) + 4 * hf; }
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// ------------------------------------------------------------------ forward
+template <int D, bool DROP>
+__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
+  const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
+  const int nqt = a.T >> 5;
+  const int64_t nbh = static_cast<int64_t>(a.B) * a.H;
+  const int64_t gw = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (gw >= nbh * nqt) return;
+  const int qtile = nqt - 1 - static_cast<int>(gw / nbh);  // heaviest (longest causal range) first
+  const int bh = static_cast<int>(gw % nbh);
+  const int b = bh / a.H, h = bh % a.H, hk = h / (a.H / a.Hkv);
+  const int q = qtile * 32 + r;
+
+  bf16x8 qf[D / 16];
+  const __bf16* qp = a.q + b * a.q_sb + static_cast<int64_t>(q) * a.q_st + h * a.q_sh + 8 * hf;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) qf[s] = ld8(qp + 16 * s);
+
+  f32x16 oacc[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) oacc[t] = zero16();
+  float m = -INFINITY, l = 0.f;
+  const __bf16* kbase = a.k + b * a.k_sb + hk * a.k_sh + 8 * hf;
+  const __bf16* vtb = a.vt + static_cast<int64_t>(b * a.Hkv + hk) * D * a.T + 4 * hf;
+
+  for (int kt = 0; kt <= qtile; ++kt) {
+    const int kb = kt * 32;
+    f32x16 s = zero16();
+    const __bf16* kp = kbase + static_cast<int64_t>(kb + r) * a.k_st;
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) s = mfma32(ld8(kp + 16 * ks), qf[ks], s);
+    float mx = m;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      float x = s[reg] * a.scale_log2;
+      if (kt == qtile && kb + acc_row(reg, hf) > q) x = -INFINITY;
+      s[reg] = x;
+      mx = fmaxf(mx, x);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float alpha = exp2f(m - mx);
+    float rs = 0.f;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const float p = exp2f(s[reg] - mx);
+      rs += p;
+      s[reg] = p;
+    }
+    rs += __shfl_xor(rs, 32);
+    l = l * alpha + rs;
+    m = mx;
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[t][i] *= alpha;
+    if constexpr (DROP) {
+#pragma unroll
+      for (int reg = 0; reg < 16; reg += 2) {  // regs (2i, 2i+1) hold keys (2j, 2j+1)
+        const uint32_t key = kb + acc_row(reg, hf);
+        const uint32_t hsh = drop_hash(a.seed, bh, q, key);
+        s[reg] = drop_keep(hsh, key, a.thresh16) ? s[reg] * a.inv_keep : 0.f;
+        s[reg + 1] = drop_keep(hsh, key + 1, a.thresh16) ? s[reg + 1] * a.inv_keep : 0.f;
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pf = acc_frag(s, s2);
+#pragma unroll
+      for (int t = 0; t < D / 32; ++t) {
+        const __bf16* vp = vtb + static_cast<int64_t>(32 * t + r) * a.T + kb + 16 * s2;
+        oacc[t] = mfma32(ld4x2(vp), pf, oacc[t]);
+      }
+    }
+  }
+  const float inv_l = 1.f / l;
+  __bf16* op = a.out + b * a.o_sb + static_cast<int64_t>(q) * a.o_st + h * a.o_sh;
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 w;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] = static_cast<__bf16>(oacc[t][4 * g + i] * inv_l);
+      *reinterpret_cast<bf16x4*>(op + 32 * t + 8 * g + 4 * hf) = w;
+    }
+  if (hf == 0) a.lse[static_cast<int64_t>(bh) * a.T + q] = m + log2f(l);
+}
+
+// --------------------------------------------------------------- backward dQ
+template <int D, bool DROP>
+__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
+  const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
+  const int nqt = a.T >> 5;
+  const int64_t nbh = static_cast<int64_t>(a.B) * a.H;
+  const int64_t gw = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (gw >= nbh * nqt) return;
+  const int qtile = nqt - 1 - static_cast<int>(gw / nbh);
+  const int bh = static_cast<int>(gw % nbh);
+  const int b = bh / a.H, h = bh % a.H, hk = h / (a.H / a.Hkv);
+  const int q = qtile * 32 + r;
+
+  bf16x8 qf[D / 16], dof[D / 16];
+  const __bf16* qp = a.q + b * a.q_sb + static_cast<int64_t>(q) * a.q_st + h * a.q_sh + 8 * hf;
+  const __bf16* dop = a.dout + b * a.o_sb + static_cast<int64_t>(q) * a.o_st + h * a.o_sh + 8 * hf;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    qf[s] = ld8(qp + 16 * s);
+    dof[s] = ld8(dop + 16 * s);
+  }
+  const float lse2 = a.lse[static_cast<int64_t>(bh) * a.T + q];
+  const float dlt = a.delta[static_cast<int64_t>(bh) * a.T + q];
+  f32x16 dq[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) dq[t] = zero16();
+  const __bf16* kbase = a.k + b * a.k_sb + hk * a.k_sh + 8 * hf;
+  const __bf16* vbase = a.v + b * a.v_sb + hk * a.v_sh + 8 * hf;
+  const __bf16* ktb = a.kt + static_cast<int64_t>(b * a.Hkv + hk) * D * a.T + 4 * hf;
+
+  for (int kt = 0; kt <= qtile; ++kt) {
+    const int kb = kt * 32;
+    f32x16 s = zero16(), dp = zero16();
+    const __bf16* kp = kbase + static_cast<int64_t>(kb + r) * a.k_st;
+    const __bf16* vp = vbase + static_cast<int64_t>(kb + r) * a.v_st;
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      s = mfma32(ld8(kp + 16 * ks), qf[ks], s);
+      dp = mfma32(ld8(vp + 16 * ks), dof[ks], dp);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 16; reg += 2) {
+      const int key = kb + acc_row(reg, hf);
+      uint32_t hsh = 0;
+      if constexpr (DROP) hsh = drop_hash(a.seed, bh, q, key);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int kk = key + e;
+        float p = (kt == qtile && kk > q) ? 0.f : exp2f(s[reg + e] * a.scale_log2 - lse2);
+        float dpv = dp[reg + e];
+        if constexpr (DROP) dpv = drop_keep(hsh, kk, a.thresh16) ? dpv * a.inv_keep : 0.f;
+        s[reg + e] = p * (dpv - dlt);  // dS^T
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 dsf = acc_frag(s, s2);
+#pragma unroll
+      for (int t = 0; t < D / 32; ++t) {
+        const __bf16* kq = ktb + static_cast<int64_t>(32 * t + r) * a.T + kb + 16 * s2;
+        dq[t] = mfma32(dsf, ld4x2(kq), dq[t]);
+      }
+    }
+  }
+  // dq[t]: rows = q (registers), cols = d (lane)
+  __bf16* base = a.dq + b * a.dq_sb + h * a.dq_sh;
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int qq = qtile * 32 + acc_row(reg, hf);
+      base[static_cast<int64_t>(qq) * a.dq_st + 32 * t + r] = static_cast<__bf16>(dq[t][reg] * a.scale);
+    }
+}
+
+// -------------------------------------------------------------- backward dKV
+template <int D, bool DROP>
+__global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
+  const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
+  const int nkt = a.T >> 5;
+  const int64_t nbh = static_cast<int64_t>(a.B) * a.Hkv;
+  const int64_t gw = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (gw >= nbh * nkt) return;
+  const int ktile = static_cast<int>(gw / nbh);  // low key tiles see the most queries: first
+  const int bhk = static_cast<int>(gw % nbh);
+  const int b = bhk / a.Hkv, hk = bhk % a.Hkv;
+  const int group = a.H / a.Hkv;
+  const int kb = ktile * 32;
+  const int key = kb + r;
+
+  bf16x8 kf[D / 16], vf[D / 16];
+  const __bf16* kp = a.k + b * a.k_sb + static_cast<int64_t>(key) * a.k_st + hk * a.k_sh + 8 * hf;
+  const __bf16* vp = a.v + b * a.v_sb + static_cast<int64_t>(key) * a.v_st + hk * a.v_sh + 8 * hf;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    kf[s] = ld8(kp + 16 * s);
+    vf[s] = ld8(vp + 16 * s);
+  }
+  f32x16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) {
+    dk[t] = zero16();
+    dv[t] = zero16();
+  }
+  for (int gh = 0; gh < group; ++gh) {
+    const int h = hk * group + gh;
+    const int bh = b * a.H + h;
+    const __bf16* qbase = a.q + b * a.q_sb + h * a.q_sh + 8 * hf;
+    const __bf16* dobase = a.dout + b * a.o_sb + h * a.o_sh + 8 * hf;
+    const __bf16* qtb = a.qt + static_cast<int64_t>(bh) * D * a.T + 4 * hf;
+    const __bf16* dotb = a.dot + static_cast<int64_t>(bh) * D * a.T + 4 * hf;
+    const float* lseb = a.lse + static_cast<int64_t>(bh) * a.T;
+    const float* dlb = a.delta + static_cast<int64_t>(bh) * a.T;
+    for (int qt = ktile; qt < (a.T >> 5); ++qt) {
+      const int qb = qt * 32;
+      f32x16 s = zero16(), dp = zero16();
+      const __bf16* qp = qbase + static_cast<int64_t>(qb + r) * a.q_st;
+      const __bf16* dop = dobase + static_cast<int64_t>(qb + r) * a.o_st;
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        s = mfma32(ld8(qp + 16 * ks), kf[ks], s);     // S  = Q K^T : rows q, cols key
+        dp = mfma32(ld8(dop + 16 * ks), vf[ks], dp);  // dP = dO V^T
+      }
+      float lse4[16], dl4[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 lv = *reinterpret_cast<const float4*>(lseb + qb + 8 * g + 4 * hf);
+        const float4 dv4 = *reinterpret_cast<const float4*>(dlb + qb + 8 * g + 4 * hf);
+        lse4[4 * g] = lv.x; lse4[4 * g + 1] = lv.y; lse4[4 * g + 2] = lv.z; lse4[4 * g + 3] = lv.w;
+        dl4[4 * g] = dv4.x; dl4[4 * g + 1] = dv4.y; dl4[4 * g + 2] = dv4.z; dl4[4 * g + 3] = dv4.w;
+      }
+      f32x16 pd;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int qq = qb + acc_row(reg, hf);
+        const float p = (qt == ktile && key > qq) ? 0.f : exp2f(s[reg] * a.scale_log2 - lse4[reg]);
+        float dpv = dp[reg];
+        float pdv = p;
+        if constexpr (DROP) {
+          const bool kp_ = drop_keep(drop_hash(a.seed, bh, qq, key), key, a.thresh16);
+          dpv = kp_ ? dpv * a.inv_keep : 0.f;
+          pdv = kp_ ? p * a.inv_keep : 0.f;
+        }
+        pd[reg] = pdv;
+        s[reg] = p * (dpv - dl4[reg]);  // dS
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pf = acc_frag(pd, s2);
+        const bf16x8 dsf = acc_frag(s, s2);
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) {
+          const int64_t row = static_cast<int64_t>(32 * t + r) * a.T + qb + 16 * s2;
+          dv[t] = mfma32(pf, ld4x2(dotb + row), dv[t]);  // dV += Pd^T dO
+          dk[t] = mfma32(dsf, ld4x2(qtb + row), dk[t]);  // dK += dS^T Q
+        }
+      }
+    }
+  }
+  // dk/dv[t]: rows = key (registers), cols = d (lane)
+  __bf16* dkb = a.dk + b * a.dk_sb + hk * a.dk_sh;
+  __bf16* dvb = a.dv + b * a.dk_sb + hk * a.dk_sh;
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int64_t off = static_cast<int64_t>(kb + acc_row(reg, hf)) * a.dk_st + 32 * t + r;
+      dkb[off] = static_cast<__bf16>(dk[t][reg] * a.scale);
+      dvb[off] = static_cast<__bf16>(dv[t][reg]);
+    }
+}
+
+// ------------------------------------------------- transpose [B,T,X,D] -> [B,X,D,T]
+// 64 tokens x D tile per 256-thread block through LDS (padded rows).
+template <int D>
+__global__ void __launch_bounds__(256) transpose_btxd_kernel(const __bf16* __restrict__ in, int64_t sb, int64_t st,
+                                                            int64_t sx, __bf16* __restrict__ out, int T, int X) {
+  __shared__ __bf16 tile[D][64 + 2];
+  const int tt = blockIdx.x, bx = blockIdx.y;
+  const int b = bx / X, x = bx % X;
+  const __bf16* src = in + b * sb + x * sx + static_cast<int64_t>(tt * 64) * st;
+  // load: 64 tokens x D, 8 elements per thread per step
+  for (int i = threadIdx.x; i < 64 * (D / 8); i += 256) {
+    const int tok = i / (D / 8), c8 = (i % (D / 8)) * 8;
+    const bf16x8 v = ld8(src + static_cast<int64_t>(tok) * st + c8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[c8 + j][tok] = v[j];
+  }
+  __syncthreads();
+  __bf16* dst = out + (static_cast<int64_t>(bx) * D) * T + tt * 64;
+  for (int i = threadIdx.x; i < D * 32; i += 256) {  // 2 tokens per thread
+    const int d = i / 32, t2 = (i % 32) * 2;
+    const uint32_t lo = __builtin_bit_cast(uint16_t, tile[d][t2]);
+    const uint32_t hi = __builtin_bit_cast(uint16_t, tile[d][t2 + 1]);
+    *reinterpret_cast<uint32_t*>(dst + static_cast<int64_t>(d) * T + t2) = lo | (hi << 16);
+  }
+}
+
+// ------------------------------------------------------------- delta = rowsum(dO*O)
+template <int D>
+__global__ void __launch_bounds__(256) attn_delta_kernel(AttnArgs a) {
+  // one wave-quarter (16 lanes) per row: D/16 elements per lane
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 16 + (threadIdx.x >> 4);
+  const int64_t nrows = static_cast<int64_t>(a.B) * a.H * a.T;
+  if (row >= nrows) return;
+  const int sub = threadIdx.x & 15;
+  const int bh = static_cast<int>(row / a.T), q = static_cast<int>(row % a.T);
+  const int b = bh / a.H, h = bh % a.H;
+  const int64_t off = b * a.o_sb + static_cast<int64_t>(q) * a.o_st + h * a.o_sh;
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < D / 16; ++j) {
+    const int d = sub * (D / 16) + j;
+    acc += static_cast<float>(a.o[off + d]) * static_cast<float>(a.dout[off + d]);
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 16);
+  if (sub == 0) const_cast<float*>(a.delta)[row] = acc;
+}
+
+// ------------------------------------------------------------------ launchers
+static inline int64_t waves_blocks(int64_t waves) { return (waves + 3) / 4; }
+
+hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) {
+  const int64_t blocks = waves_blocks(static_cast<int64_t>(a.B) * a.H * (a.T / 32));
+  if (D == 64) {
+    if (drop) hipLaunchKernelGGL((attn_fwd_kernel<64, true>), dim3(blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<64, false>), dim3(blocks), dim3(256), 0, st, a);
+  } else if (D == 128) {
+    if (drop) hipLaunchKernelGGL((attn_fwd_kernel<128, true>), dim3(blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<128, false>), dim3(blocks), dim3(256), 0, st, a);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) {
+  const int64_t rows = static_cast<int64_t>(a.B) * a.H * a.T;
+  const int64_t bq = waves_blocks(static_cast<int64_t>(a.B) * a.H * (a.T / 32));
+  const int64_t bkv = waves_blocks(static_cast<int64_t>(a.B) * a.Hkv * (a.T / 32));
+#define BWD(DD)                                                                                         \
+  hipLaunchKernelGGL((attn_delta_kernel<DD>), dim3((rows + 15) / 16), dim3(256), 0, st, a);             \
+  if (drop) {                                                                                           \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), dim3(bkv), dim3(256), 0, st, a);               \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, true>), dim3(bq), dim3(256), 0, st, a);                 \
+  } else {                                                                                              \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), dim3(bkv), dim3(256), 0, st, a);              \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, false>), dim3(bq), dim3(256), 0, st, a);                \
+  }
+  if (D == 64) {
+    BWD(64)
+  } else if (D == 128) {
+    BWD(128)
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef BWD
+  return hipGetLastError();
+}
+
+hipError_t launch_transpose_btxd(const void* in, int64_t sb, int64_t st, int64_t sx, void* out, int B, int T, int X,
+                                 int D, hipStream_t stream) {
+  const dim3 grid(T / 64, B * X);
+  const __bf16* i = static_cast<const __bf16*>(in);
+  __bf16* o = static_cast<__bf16*>(out);
+  if (D == 64) hipLaunchKernelGGL((transpose_btxd_kernel<64>), grid, dim3(256), 0, stream, i, sb, st, sx, o, T, X);
+  else if (D == 128) hipLaunchKernelGGL((transpose_btxd_kernel<128>), grid, dim3(256), 0, stream, i, sb, st, sx, o, T, X);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace dlion

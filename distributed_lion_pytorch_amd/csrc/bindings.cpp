@@ -137,9 +137,107 @@ Tensor softmax_xent_(const Tensor& logits, const Tensor& labels, int64_t v) {
   return loss;
 }
 
+// ------------------------------------------------------------ flash attention
+void check_bthd(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, "dlion attn: ", name, " must be a bf16 GPU tensor");
+  TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1, "dlion attn: ", name, " must be [B,T,H,D] with contiguous D");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0 &&
+                  t.stride(0) % 8 == 0,
+              "dlion attn: ", name, " must be 16-byte aligned");
+}
+
+Tensor transpose_btxd(const Tensor& x) {
+  check_bthd(x, "x");
+  const int64_t B = x.size(0), T = x.size(1), X = x.size(2), D = x.size(3);
+  TORCH_CHECK(T % 64 == 0 && (D == 64 || D == 128), "dlion attn: need T % 64 == 0 and D in {64, 128}");
+  auto out = at::empty({B, X, D, T}, x.options());
+  const c10::DeviceGuard g(x.device());
+  check_hip(dlion::launch_transpose_btxd(x.data_ptr(), x.stride(0), x.stride(1), x.stride(2), out.data_ptr(),
+                                         static_cast<int>(B), static_cast<int>(T), static_cast<int>(X),
+                                         static_cast<int>(D), cur_stream()),
+            "transpose_btxd");
+  return out;
+}
+
+dlion::AttnArgs attn_args(const Tensor& q, const Tensor& k, const Tensor& v, double p, int64_t seed) {
+  check_bthd(q, "q");
+  check_bthd(k, "k");
+  check_bthd(v, "v");
+  const int64_t B = q.size(0), T = q.size(1), H = q.size(2), D = q.size(3), Hkv = k.size(2);
+  TORCH_CHECK(k.size(0) == B && k.size(1) == T && k.size(3) == D && v.sizes() == k.sizes(), "dlion attn: shape mismatch");
+  TORCH_CHECK(H % Hkv == 0, "dlion attn: H must be a multiple of Hkv");
+  TORCH_CHECK(T % 64 == 0 && (D == 64 || D == 128), "dlion attn: need T % 64 == 0 and D in {64, 128}");
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dlion attn: dropout must be in [0, 1)");
+  dlion::AttnArgs a{};
+  a.q = static_cast<const __bf16*>(q.data_ptr());
+  a.k = static_cast<const __bf16*>(k.data_ptr());
+  a.v = static_cast<const __bf16*>(v.data_ptr());
+  a.q_sb = q.stride(0); a.q_st = q.stride(1); a.q_sh = q.stride(2);
+  a.k_sb = k.stride(0); a.k_st = k.stride(1); a.k_sh = k.stride(2);
+  a.v_sb = v.stride(0); a.v_st = v.stride(1); a.v_sh = v.stride(2);
+  a.B = static_cast<int>(B); a.T = static_cast<int>(T); a.H = static_cast<int>(H); a.Hkv = static_cast<int>(Hkv);
+  a.scale = static_cast<float>(1.0 / std::sqrt(static_cast<double>(D)));
+  a.scale_log2 = static_cast<float>(1.4426950408889634 / std::sqrt(static_cast<double>(D)));
+  uint32_t th = static_cast<uint32_t>(std::llround(p * 65536.0));
+  if (th > 65535u) th = 65535u;
+  a.thresh16 = th;
+  a.inv_keep = static_cast<float>(65536.0 / (65536.0 - th));
+  a.seed = static_cast<uint32_t>(seed);
+  return a;
+}
+
+std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, double p, int64_t seed) {
+  auto a = attn_args(q, k, v, p, seed);
+  const c10::DeviceGuard g(q.device());
+  const Tensor vt = transpose_btxd(v);
+  auto out = at::empty({q.size(0), q.size(1), q.size(2), q.size(3)}, q.options());
+  auto lse = at::empty({q.size(0), q.size(2), q.size(1)}, q.options().dtype(at::kFloat));
+  a.vt = static_cast<const __bf16*>(vt.data_ptr());
+  a.out = static_cast<__bf16*>(out.data_ptr());
+  a.o_sb = out.stride(0); a.o_st = out.stride(1); a.o_sh = out.stride(2);
+  a.lse = lse.data_ptr<float>();
+  check_hip(dlion::launch_attn_fwd(a, static_cast<int>(q.size(3)), a.thresh16 > 0, cur_stream()), "attn_fwd");
+  return {out, lse};
+}
+
+void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& out, const Tensor& dout,
+              const Tensor& lse, double p, int64_t seed, const Tensor& dq, const Tensor& dk, const Tensor& dv) {
+  auto a = attn_args(q, k, v, p, seed);
+  check_bthd(out, "out");
+  check_bthd(dout, "dout");
+  check_bthd(dq, "dq");
+  check_bthd(dk, "dk");
+  check_bthd(dv, "dv");
+  TORCH_CHECK(out.strides() == dout.strides(), "dlion attn: out and dout must share strides");
+  TORCH_CHECK(dk.strides() == dv.strides(), "dlion attn: dk and dv must share strides");
+  TORCH_CHECK(lse.is_contiguous() && lse.scalar_type() == at::kFloat, "dlion attn: lse must be contiguous fp32");
+  const c10::DeviceGuard g(q.device());
+  const Tensor qt = transpose_btxd(q), kt = transpose_btxd(k), dot = transpose_btxd(dout);
+  auto delta = at::empty_like(lse);
+  a.o = static_cast<const __bf16*>(out.data_ptr());
+  a.dout = static_cast<const __bf16*>(dout.data_ptr());
+  a.o_sb = out.stride(0); a.o_st = out.stride(1); a.o_sh = out.stride(2);
+  a.qt = static_cast<const __bf16*>(qt.data_ptr());
+  a.kt = static_cast<const __bf16*>(kt.data_ptr());
+  a.dot = static_cast<const __bf16*>(dot.data_ptr());
+  a.lse = lse.data_ptr<float>();
+  a.delta = delta.data_ptr<float>();
+  a.dq = static_cast<__bf16*>(dq.data_ptr());
+  a.dk = static_cast<__bf16*>(dk.data_ptr());
+  a.dv = static_cast<__bf16*>(dv.data_ptr());
+  a.dq_sb = dq.stride(0); a.dq_st = dq.stride(1); a.dq_sh = dq.stride(2);
+  a.dk_sb = dk.stride(0); a.dk_st = dk.stride(1); a.dk_sh = dk.stride(2);
+  check_hip(dlion::launch_attn_bwd(a, static_cast<int>(q.size(3)), a.thresh16 > 0, cur_stream()), "attn_bwd");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dlion, m) {
+  m.def("transpose_btxd(Tensor x) -> Tensor");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float p, int seed) -> (Tensor, Tensor)");
+  m.def(
+      "attn_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout, Tensor lse, float p, int seed,"
+      " Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
   m.def("softmax_xent_(Tensor(a!) logits, Tensor labels, int v) -> Tensor");
   m.def(
       "lion_local(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, float decay, float neg_lr,"
@@ -160,4 +258,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("lion_vote_apply", &lion_vote_apply);
   m.impl("vote_reduce", &vote_reduce);
   m.impl("softmax_xent_", &softmax_xent_);
+  m.impl("transpose_btxd", &transpose_btxd);
+  m.impl("attn_fwd", &attn_fwd);
+  m.impl("attn_bwd", &attn_bwd);
 }

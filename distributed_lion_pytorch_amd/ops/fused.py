@@ -63,12 +63,118 @@ def linear_gelu(x2d: torch.Tensor, w_in_out: torch.Tensor, bias: torch.Tensor, e
 
 
 # ------------------------------------------------------------------ attention
+def _attn_ok(x: torch.Tensor, T: int, D: int) -> bool:
+    return x.dtype == torch.bfloat16 and D in (64, 128) and T % 64 == 0 and _use_hip(x)
+
+
+def _new_seed() -> int:
+    return int(torch.randint(0, 2**31 - 1, (1,)).item())
+
+
+class _FlashAttnPacked(torch.autograd.Function):
+    """Causal attention on packed qkv [B,T,3,H,D]; dqkv is written in place of
+    the q/k/v gradients (no stack/cat) by the gfx950 kernels."""
+
+    @staticmethod
+    def forward(ctx, qkv, p, seed):
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        out, lse = hip.ops().attn_fwd(q, k, v, p, seed)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.p, ctx.seed = p, seed
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        dout = dout.contiguous()
+        dqkv = torch.empty_like(qkv)
+        hip.ops().attn_bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], out, dout, lse, ctx.p, ctx.seed,
+                           dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2])
+        return dqkv, None, None
+
+
+class _FlashAttn(torch.autograd.Function):
+    """Causal (GQA) attention on separate q [B,T,H,D], k/v [B,T,Hkv,D]."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, p, seed):
+        out, lse = hip.ops().attn_fwd(q, k, v, p, seed)
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.p, ctx.seed = p, seed
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, lse = ctx.saved_tensors
+        dout = dout.contiguous()
+        dq = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+        dkv = torch.empty((2,) + tuple(k.shape), dtype=k.dtype, device=k.device)
+        hip.ops().attn_bwd(q, k, v, out, dout, lse, ctx.p, ctx.seed, dq, dkv[0], dkv[1])
+        return dq, dkv[0], dkv[1], None, None
+
+
 def causal_attention(qkv: torch.Tensor, dropout_p: float) -> torch.Tensor:
     """qkv: [B, T, 3, H, D] -> causal softmax attention output [B, T, H*D]."""
     B, T, _, H, D = qkv.shape
+    if _attn_ok(qkv, T, D):
+        return _FlashAttnPacked.apply(qkv, float(dropout_p), _new_seed()).view(B, T, H * D)
     q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)  # [B, H, T, D] views
     y = F.scaled_dot_product_attention(q, k, v, dropout_p=dropout_p, is_causal=True)
     return y.transpose(1, 2).reshape(B, T, H * D)
+
+
+def causal_attention_gqa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, dropout_p: float = 0.0) -> torch.Tensor:
+    """q [B,T,H,D], k/v [B,T,Hkv,D] -> [B,T,H*D] (grouped-query causal attention)."""
+    B, T, H, D = q.shape
+    if _attn_ok(q, T, D):
+        return _FlashAttn.apply(q, k, v, float(dropout_p), _new_seed()).view(B, T, H * D)
+    rep = H // k.shape[2]
+    qh, kh, vh = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+    if rep > 1:
+        kh = kh.repeat_interleave(rep, dim=1)
+        vh = vh.repeat_interleave(rep, dim=1)
+    y = F.scaled_dot_product_attention(qh, kh, vh, dropout_p=dropout_p, is_causal=True)
+    return y.transpose(1, 2).reshape(B, T, H * D)
+
+
+_M32 = 0xFFFFFFFF
+
+
+def _lowbias32(x: torch.Tensor) -> torch.Tensor:
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def attention_dropout_keep(B: int, H: int, T: int, p: float, seed: int, device=None) -> torch.Tensor:
+    """bool keep-mask [B, H, T(q), T(key)] exactly as the HIP kernels draw it."""
+    th = min(65535, int(round(p * 65536)))
+    bh = torch.arange(B * H, device=device, dtype=torch.int64).view(B * H, 1, 1)
+    q = torch.arange(T, device=device, dtype=torch.int64).view(1, T, 1)
+    key = torch.arange(T, device=device, dtype=torch.int64).view(1, 1, T)
+    x = ((bh * 0x9E3779B9) & _M32) ^ ((q * 0x85EBCA6B) & _M32) ^ (((key >> 1) * 0xC2B2AE35) & _M32) ^ (seed & _M32)
+    u16 = (_lowbias32(x) >> ((key & 1) * 16)) & 0xFFFF
+    return (u16 >= th).view(B, H, T, T)
+
+
+def reference_attention(q, k, v, dropout_p: float = 0.0, seed: int = 0) -> torch.Tensor:
+    """fp32 math reference with the kernels' dropout mask: q [B,T,H,D], k/v [B,T,Hkv,D]."""
+    B, T, H, D = q.shape
+    rep = H // k.shape[2]
+    qh = q.float().transpose(1, 2)
+    kh = k.float().transpose(1, 2).repeat_interleave(rep, dim=1)
+    vh = v.float().transpose(1, 2).repeat_interleave(rep, dim=1)
+    s = (qh @ kh.transpose(-1, -2)) / (D ** 0.5)
+    causal = torch.ones(T, T, dtype=torch.bool, device=q.device).tril()
+    s = s.masked_fill(~causal, float("-inf"))
+    pr = torch.softmax(s, dim=-1)
+    if dropout_p > 0:
+        th = min(65535, int(round(dropout_p * 65536)))
+        keep = attention_dropout_keep(B, H, T, dropout_p, seed, q.device)
+        pr = pr * keep * (65536.0 / (65536.0 - th))
+    return (pr @ vh).transpose(1, 2).reshape(B, T, H * D)
 
 
 # ------------------------------------------------- LM head + cross-entropy

@@ -1,0 +1,69 @@
+"""gfx950 flash attention (fwd + bwd, dropout, GQA) vs an fp32 PyTorch reference
+that uses the identical stateless dropout mask."""
+import pytest
+import torch
+
+from distributed_lion_pytorch_amd.ops import fused, hip
+
+
+def test_dropout_mask_statistics_cpu():
+    keep = fused.attention_dropout_keep(2, 3, 128, 0.1, seed=7)
+    frac = keep.float().mean().item()
+    assert abs(frac - 0.9) < 0.01
+    keep2 = fused.attention_dropout_keep(2, 3, 128, 0.1, seed=8)
+    assert (keep != keep2).float().mean().item() > 0.1
+
+
+def _close(a, b, tol):
+    err = (a.float() - b.float()).abs().max().item()
+    scale = b.float().abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err} vs scale {scale}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T,H,Hkv,D", [(2, 128, 4, 4, 64), (1, 256, 8, 2, 128), (3, 64, 2, 1, 64)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_flash_attention_fwd_bwd(B, T, H, Hkv, D, p, cuda):
+    hip.require()
+    torch.manual_seed(0)
+    q = torch.randn(B, T, H, D, device=cuda, dtype=torch.bfloat16)
+    k = torch.randn(B, T, Hkv, D, device=cuda, dtype=torch.bfloat16)
+    v = torch.randn(B, T, Hkv, D, device=cuda, dtype=torch.bfloat16)
+    dout = torch.randn(B, T, H * D, device=cuda, dtype=torch.bfloat16)
+    seed = 1234
+    qs, ks, vs = (t.clone().requires_grad_() for t in (q, k, v))
+    out = fused._FlashAttn.apply(qs, ks, vs, p, seed).view(B, T, H * D)
+    out.backward(dout)
+    qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
+    ref = fused.reference_attention(qr, kr, vr, p, seed)
+    ref.backward(dout.float())
+    _close(out, ref, 2e-2)
+    _close(qs.grad, qr.grad, 3e-2)
+    _close(ks.grad, kr.grad, 3e-2)
+    _close(vs.grad, vr.grad, 3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_packed_qkv_attention_matches_reference(p, cuda):
+    hip.require()
+    torch.manual_seed(1)
+    B, T, H, D = 2, 192, 3, 64
+    qkv = torch.randn(B, T, 3, H, D, device=cuda, dtype=torch.bfloat16)
+    dout = torch.randn(B, T, H * D, device=cuda, dtype=torch.bfloat16)
+    a = qkv.clone().requires_grad_()
+    out = fused._FlashAttnPacked.apply(a, p, 99).view(B, T, H * D)
+    out.backward(dout)
+    r = qkv.float().requires_grad_()
+    ref = fused.reference_attention(r[:, :, 0], r[:, :, 1], r[:, :, 2], p, 99)
+    ref.backward(dout.float())
+    _close(out, ref, 2e-2)
+    _close(a.grad, r.grad, 3e-2)
+
+
+@pytest.mark.gpu
+def test_transpose_kernel(cuda):
+    hip.require()
+    x = torch.randn(2, 128, 3, 5, 64, device=cuda, dtype=torch.bfloat16)[:, :, 1]
+    xt = hip.ops().transpose_btxd(x)
+    assert torch.equal(xt, x.permute(0, 2, 3, 1).contiguous())
