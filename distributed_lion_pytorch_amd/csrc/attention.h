@@ -33,6 +33,8 @@ struct AttnArgs {
   uint32_t thresh16; // dropout threshold (keep if u16 >= thresh16), 0 = no dropout
   float inv_keep;
   uint32_t seed;
+  int ldt;    // row stride (elements) of the [.., D, T] transposed operands (padded off a power of 2)
+  int order;  // tile_map() ordering (0: heads fastest, 1: head-grouped + XCD remap)
 };
 
 }  // namespace dlion

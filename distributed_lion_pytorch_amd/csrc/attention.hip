@@ -69,6 +69,32 @@ __device__ __forceinline__ bf16x8 acc_frag(const f32x16& x, int s) {
 }
 __device__ __forceinline__ int acc_row(int reg, int hf) { return (reg & 3) + 8 * (reg >> 2) + 4 * hf; }
 
+// (blockIdx, wave) -> (bh, tile): the 4 waves of a block take 4 consecutive
+// 32-row tiles of ONE head (their K/V or Q/dO fragment loads coincide and hit
+// the CU's L1), all blocks of a head share an XCD (bijective remap, guide §5)
+// so a head's K/V stay in that XCD's L2, heads are walked one after the other
+// (few heads in flight -> the working set fits L2), heavy tiles first.
+// Returns false for waves past the last tile.
+__device__ __forceinline__ bool tile_map(int order, int nbh, int ntiles, bool heavy_high, int& bh, int& tile) {
+  if (order == 0) {  // waves walk heads fastest; globally heaviest tiles first
+    const int64_t gw = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    if (gw >= static_cast<int64_t>(nbh) * ntiles) return false;
+    const int t = static_cast<int>(gw / nbh);
+    tile = heavy_high ? ntiles - 1 - t : t;
+    bh = static_cast<int>(gw % nbh);
+    return true;
+  }
+  const int bpb = (ntiles + 3) >> 2;  // blocks per head
+  const int nblocks = nbh * bpb;
+  const int i = blockIdx.x, xcd = i & 7, q = nblocks >> 3, rr = nblocks & 7;
+  const int L = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (i >> 3);
+  bh = L / bpb;
+  int blk = L - bh * bpb;
+  if (heavy_high) blk = bpb - 1 - blk;
+  tile = blk * 4 + (threadIdx.x >> 6);
+  return bh < nbh && tile < ntiles;
+}
+
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -80,12 +106,8 @@ __device__ __forceinline__ f32x16 zero16() {
 template <int D, bool DROP>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
-  const int nqt = a.T >> 5;
-  const int64_t nbh = static_cast<int64_t>(a.B) * a.H;
-  const int64_t gw = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (gw >= nbh * nqt) return;
-  const int qtile = nqt - 1 - static_cast<int>(gw / nbh);  // heaviest (longest causal range) first
-  const int bh = static_cast<int>(gw % nbh);
+  int bh, qtile;
+  if (!tile_map(a.order, a.B * a.H, a.T >> 5, true, bh, qtile)) return;
   const int b = bh / a.H, h = bh % a.H, hk = h / (a.H / a.Hkv);
   const int q = qtile * 32 + r;
 
@@ -99,28 +121,46 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   for (int t = 0; t < D / 32; ++t) oacc[t] = zero16();
   float m = -INFINITY, l = 0.f;
   const __bf16* kbase = a.k + b * a.k_sb + hk * a.k_sh + 8 * hf;
-  const __bf16* vtb = a.vt + static_cast<int64_t>(b * a.Hkv + hk) * D * a.T + 4 * hf;
+  const __bf16* vtb = a.vt + static_cast<int64_t>(b * a.Hkv + hk) * D * a.ldt + 4 * hf;
+
+  // register double-buffering: the K / V^T fragments of tile kt+1 are in
+  // flight while tile kt is computed (the loop is latency-bound otherwise)
+  bf16x8 kc[D / 16], vc[2][D / 32];
+  auto load_kv = [&](int kt, bf16x8(&kf)[D / 16], bf16x8(&vf)[2][D / 32]) {
+    const __bf16* kp = kbase + static_cast<int64_t>(kt * 32 + r) * a.k_st;
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) kf[ks] = ld8(kp + 16 * ks);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int t = 0; t < D / 32; ++t)
+        vf[s2][t] = ld4x2(vtb + static_cast<int64_t>(32 * t + r) * a.ldt + kt * 32 + 16 * s2);
+  };
+  load_kv(0, kc, vc);
 
   for (int kt = 0; kt <= qtile; ++kt) {
     const int kb = kt * 32;
+    bf16x8 kn[D / 16], vn[2][D / 32];
+    if (kt < qtile) load_kv(kt + 1, kn, vn);
     f32x16 s = zero16();
-    const __bf16* kp = kbase + static_cast<int64_t>(kb + r) * a.k_st;
 #pragma unroll
-    for (int ks = 0; ks < D / 16; ++ks) s = mfma32(ld8(kp + 16 * ks), qf[ks], s);
+    for (int ks = 0; ks < D / 16; ++ks) s = mfma32(kc[ks], qf[ks], s);
     float mx = m;
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      float x = s[reg] * a.scale_log2;
-      if (kt == qtile && kb + acc_row(reg, hf) > q) x = -INFINITY;
-      s[reg] = x;
-      mx = fmaxf(mx, x);
+    for (int reg = 0; reg < 16; ++reg) s[reg] *= a.scale_log2;
+    if (kt == qtile) {  // causal mask only on the diagonal tile (wave-uniform branch)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg)
+        if (kb + acc_row(reg, hf) > q) s[reg] = -INFINITY;
     }
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) mx = fmaxf(mx, s[reg]);
     mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float alpha = exp2f(m - mx);
+    const float alpha = __builtin_amdgcn_exp2f(m - mx);
     float rs = 0.f;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      const float p = exp2f(s[reg] - mx);
+      const float p = __builtin_amdgcn_exp2f(s[reg] - mx);
       rs += p;
       s[reg] = p;
     }
@@ -131,26 +171,32 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     for (int t = 0; t < D / 32; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) oacc[t][i] *= alpha;
-    if constexpr (DROP) {
+    if constexpr (DROP) {  // 1/(1-p) is applied once to O at the end
+      const uint32_t hbase = a.seed ^ (static_cast<uint32_t>(bh) * 0x9E3779B9u) ^ (static_cast<uint32_t>(q) * 0x85EBCA6Bu);
 #pragma unroll
       for (int reg = 0; reg < 16; reg += 2) {  // regs (2i, 2i+1) hold keys (2j, 2j+1)
         const uint32_t key = kb + acc_row(reg, hf);
-        const uint32_t hsh = drop_hash(a.seed, bh, q, key);
-        s[reg] = drop_keep(hsh, key, a.thresh16) ? s[reg] * a.inv_keep : 0.f;
-        s[reg + 1] = drop_keep(hsh, key + 1, a.thresh16) ? s[reg + 1] * a.inv_keep : 0.f;
+        const uint32_t hsh = lowbias32(hbase ^ ((key >> 1) * 0xC2B2AE35u));
+        if ((hsh & 0xffffu) < a.thresh16) s[reg] = 0.f;
+        if ((hsh >> 16) < a.thresh16) s[reg + 1] = 0.f;
       }
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pf = acc_frag(s, s2);
 #pragma unroll
-      for (int t = 0; t < D / 32; ++t) {
-        const __bf16* vp = vtb + static_cast<int64_t>(32 * t + r) * a.T + kb + 16 * s2;
-        oacc[t] = mfma32(ld4x2(vp), pf, oacc[t]);
-      }
+      for (int t = 0; t < D / 32; ++t) oacc[t] = mfma32(vc[s2][t], pf, oacc[t]);
+    }
+    if (kt < qtile) {
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) kc[ks] = kn[ks];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) vc[s2][t] = vn[s2][t];
     }
   }
-  const float inv_l = 1.f / l;
+  const float inv_l = (DROP ? a.inv_keep : 1.f) / l;
   __bf16* op = a.out + b * a.o_sb + static_cast<int64_t>(q) * a.o_st + h * a.o_sh;
 #pragma unroll
   for (int t = 0; t < D / 32; ++t)
@@ -168,12 +214,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 template <int D, bool DROP>
 __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
-  const int nqt = a.T >> 5;
-  const int64_t nbh = static_cast<int64_t>(a.B) * a.H;
-  const int64_t gw = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (gw >= nbh * nqt) return;
-  const int qtile = nqt - 1 - static_cast<int>(gw / nbh);
-  const int bh = static_cast<int>(gw % nbh);
+  int bh, qtile;
+  if (!tile_map(a.order, a.B * a.H, a.T >> 5, true, bh, qtile)) return;
   const int b = bh / a.H, h = bh % a.H, hk = h / (a.H / a.Hkv);
   const int q = qtile * 32 + r;
 
@@ -192,17 +234,34 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   for (int t = 0; t < D / 32; ++t) dq[t] = zero16();
   const __bf16* kbase = a.k + b * a.k_sb + hk * a.k_sh + 8 * hf;
   const __bf16* vbase = a.v + b * a.v_sb + hk * a.v_sh + 8 * hf;
-  const __bf16* ktb = a.kt + static_cast<int64_t>(b * a.Hkv + hk) * D * a.T + 4 * hf;
+  const __bf16* ktb = a.kt + static_cast<int64_t>(b * a.Hkv + hk) * D * a.ldt + 4 * hf;
 
-  for (int kt = 0; kt <= qtile; ++kt) {
-    const int kb = kt * 32;
-    f32x16 s = zero16(), dp = zero16();
-    const __bf16* kp = kbase + static_cast<int64_t>(kb + r) * a.k_st;
-    const __bf16* vp = vbase + static_cast<int64_t>(kb + r) * a.v_st;
+  // K / V rows and K^T fragments of tile kt+1 are prefetched during tile kt
+  bf16x8 kc[D / 16], vc[D / 16], tc[2][D / 32];
+  auto load_kv = [&](int kt, bf16x8(&kf)[D / 16], bf16x8(&vf)[D / 16], bf16x8(&tf)[2][D / 32]) {
+    const __bf16* kp = kbase + static_cast<int64_t>(kt * 32 + r) * a.k_st;
+    const __bf16* vp = vbase + static_cast<int64_t>(kt * 32 + r) * a.v_st;
 #pragma unroll
     for (int ks = 0; ks < D / 16; ++ks) {
-      s = mfma32(ld8(kp + 16 * ks), qf[ks], s);
-      dp = mfma32(ld8(vp + 16 * ks), dof[ks], dp);
+      kf[ks] = ld8(kp + 16 * ks);
+      vf[ks] = ld8(vp + 16 * ks);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int t = 0; t < D / 32; ++t)
+        tf[s2][t] = ld4x2(ktb + static_cast<int64_t>(32 * t + r) * a.ldt + kt * 32 + 16 * s2);
+  };
+  load_kv(0, kc, vc, tc);
+  for (int kt = 0; kt <= qtile; ++kt) {
+    const int kb = kt * 32;
+    bf16x8 kn[D / 16], vn[D / 16], tn[2][D / 32];
+    if (kt < qtile) load_kv(kt + 1, kn, vn, tn);
+    f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      s = mfma32(kc[ks], qf[ks], s);
+      dp = mfma32(vc[ks], dof[ks], dp);
     }
 #pragma unroll
     for (int reg = 0; reg < 16; reg += 2) {
@@ -212,7 +271,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int kk = key + e;
-        float p = (kt == qtile && kk > q) ? 0.f : exp2f(s[reg + e] * a.scale_log2 - lse2);
+        float p = (kt == qtile && kk > q) ? 0.f : __builtin_amdgcn_exp2f(s[reg + e] * a.scale_log2 - lse2);
         float dpv = dp[reg + e];
         if constexpr (DROP) dpv = drop_keep(hsh, kk, a.thresh16) ? dpv * a.inv_keep : 0.f;
         s[reg + e] = p * (dpv - dlt);  // dS^T
@@ -222,10 +281,18 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 dsf = acc_frag(s, s2);
 #pragma unroll
-      for (int t = 0; t < D / 32; ++t) {
-        const __bf16* kq = ktb + static_cast<int64_t>(32 * t + r) * a.T + kb + 16 * s2;
-        dq[t] = mfma32(dsf, ld4x2(kq), dq[t]);
+      for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tc[s2][t], dq[t]);
+    }
+    if (kt < qtile) {
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        kc[ks] = kn[ks];
+        vc[ks] = vn[ks];
       }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) tc[s2][t] = tn[s2][t];
     }
   }
   // dq[t]: rows = q (registers), cols = d (lane)
@@ -243,12 +310,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
 template <int D, bool DROP>
 __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
-  const int nkt = a.T >> 5;
-  const int64_t nbh = static_cast<int64_t>(a.B) * a.Hkv;
-  const int64_t gw = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (gw >= nbh * nkt) return;
-  const int ktile = static_cast<int>(gw / nbh);  // low key tiles see the most queries: first
-  const int bhk = static_cast<int>(gw % nbh);
+  int bhk, ktile;  // low key tiles see the most queries: first
+  if (!tile_map(a.order, a.B * a.Hkv, a.T >> 5, false, bhk, ktile)) return;
   const int b = bhk / a.Hkv, hk = bhk % a.Hkv;
   const int group = a.H / a.Hkv;
   const int kb = ktile * 32;
@@ -273,20 +336,26 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
     const int bh = b * a.H + h;
     const __bf16* qbase = a.q + b * a.q_sb + h * a.q_sh + 8 * hf;
     const __bf16* dobase = a.dout + b * a.o_sb + h * a.o_sh + 8 * hf;
-    const __bf16* qtb = a.qt + static_cast<int64_t>(bh) * D * a.T + 4 * hf;
-    const __bf16* dotb = a.dot + static_cast<int64_t>(bh) * D * a.T + 4 * hf;
+    const __bf16* qtb = a.qt + static_cast<int64_t>(bh) * D * a.ldt + 4 * hf;
+    const __bf16* dotb = a.dot + static_cast<int64_t>(bh) * D * a.ldt + 4 * hf;
     const float* lseb = a.lse + static_cast<int64_t>(bh) * a.T;
     const float* dlb = a.delta + static_cast<int64_t>(bh) * a.T;
-    for (int qt = ktile; qt < (a.T >> 5); ++qt) {
-      const int qb = qt * 32;
-      f32x16 s = zero16(), dp = zero16();
-      const __bf16* qp = qbase + static_cast<int64_t>(qb + r) * a.q_st;
-      const __bf16* dop = dobase + static_cast<int64_t>(qb + r) * a.o_st;
+    // Q / dO rows of tile qt+1 are prefetched while tile qt is computed; the
+    // transposed fragments and row statistics of tile qt are issued at the top
+    // of the iteration so their latency hides under the S / dP MFMAs.
+    bf16x8 qc[D / 16], dc[D / 16];
+    auto load_qd = [&](int qt, bf16x8(&qf)[D / 16], bf16x8(&df)[D / 16]) {
+      const __bf16* qp = qbase + static_cast<int64_t>(qt * 32 + r) * a.q_st;
+      const __bf16* dop = dobase + static_cast<int64_t>(qt * 32 + r) * a.o_st;
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
-        s = mfma32(ld8(qp + 16 * ks), kf[ks], s);     // S  = Q K^T : rows q, cols key
-        dp = mfma32(ld8(dop + 16 * ks), vf[ks], dp);  // dP = dO V^T
+        qf[ks] = ld8(qp + 16 * ks);
+        df[ks] = ld8(dop + 16 * ks);
       }
+    };
+    load_qd(ktile, qc, dc);
+    for (int qt = ktile; qt < (a.T >> 5); ++qt) {
+      const int qb = qt * 32;
       float lse4[16], dl4[16];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -295,11 +364,30 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
         lse4[4 * g] = lv.x; lse4[4 * g + 1] = lv.y; lse4[4 * g + 2] = lv.z; lse4[4 * g + 3] = lv.w;
         dl4[4 * g] = dv4.x; dl4[4 * g + 1] = dv4.y; dl4[4 * g + 2] = dv4.z; dl4[4 * g + 3] = dv4.w;
       }
+      bf16x8 qtf[2][D / 32], dtf[2][D / 32];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) {
+          const int64_t row = static_cast<int64_t>(32 * t + r) * a.ldt + qb + 16 * s2;
+          qtf[s2][t] = ld4x2(qtb + row);
+          dtf[s2][t] = ld4x2(dotb + row);
+        }
+      bf16x8 qn[D / 16], dn[D / 16];
+      const bool more = qt + 1 < (a.T >> 5);
+      if (more) load_qd(qt + 1, qn, dn);
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        s = mfma32(qc[ks], kf[ks], s);   // S  = Q K^T : rows q, cols key
+        dp = mfma32(dc[ks], vf[ks], dp);  // dP = dO V^T
+      }
       f32x16 pd;
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         const int qq = qb + acc_row(reg, hf);
-        const float p = (qt == ktile && key > qq) ? 0.f : exp2f(s[reg] * a.scale_log2 - lse4[reg]);
+        const float p =
+            (qt == ktile && key > qq) ? 0.f : __builtin_amdgcn_exp2f(s[reg] * a.scale_log2 - lse4[reg]);
         float dpv = dp[reg];
         float pdv = p;
         if constexpr (DROP) {
@@ -316,9 +404,15 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
         const bf16x8 dsf = acc_frag(s, s2);
 #pragma unroll
         for (int t = 0; t < D / 32; ++t) {
-          const int64_t row = static_cast<int64_t>(32 * t + r) * a.T + qb + 16 * s2;
-          dv[t] = mfma32(pf, ld4x2(dotb + row), dv[t]);  // dV += Pd^T dO
-          dk[t] = mfma32(dsf, ld4x2(qtb + row), dk[t]);  // dK += dS^T Q
+          dv[t] = mfma32(pf, dtf[s2][t], dv[t]);   // dV += Pd^T dO
+          dk[t] = mfma32(dsf, qtf[s2][t], dk[t]);  // dK += dS^T Q
+        }
+      }
+      if (more) {
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) {
+          qc[ks] = qn[ks];
+          dc[ks] = dn[ks];
         }
       }
     }
@@ -340,7 +434,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
 // 64 tokens x D tile per 256-thread block through LDS (padded rows).
 template <int D>
 __global__ void __launch_bounds__(256) transpose_btxd_kernel(const __bf16* __restrict__ in, int64_t sb, int64_t st,
-                                                            int64_t sx, __bf16* __restrict__ out, int T, int X) {
+                                                            int64_t sx, __bf16* __restrict__ out, int ldt, int X) {
   __shared__ __bf16 tile[D][64 + 2];
   const int tt = blockIdx.x, bx = blockIdx.y;
   const int b = bx / X, x = bx % X;
@@ -353,12 +447,12 @@ __global__ void __launch_bounds__(256) transpose_btxd_kernel(const __bf16* __res
     for (int j = 0; j < 8; ++j) tile[c8 + j][tok] = v[j];
   }
   __syncthreads();
-  __bf16* dst = out + (static_cast<int64_t>(bx) * D) * T + tt * 64;
+  __bf16* dst = out + (static_cast<int64_t>(bx) * D) * ldt + tt * 64;
   for (int i = threadIdx.x; i < D * 32; i += 256) {  // 2 tokens per thread
     const int d = i / 32, t2 = (i % 32) * 2;
     const uint32_t lo = __builtin_bit_cast(uint16_t, tile[d][t2]);
     const uint32_t hi = __builtin_bit_cast(uint16_t, tile[d][t2 + 1]);
-    *reinterpret_cast<uint32_t*>(dst + static_cast<int64_t>(d) * T + t2) = lo | (hi << 16);
+    *reinterpret_cast<uint32_t*>(dst + static_cast<int64_t>(d) * ldt + t2) = lo | (hi << 16);
   }
 }
 
@@ -385,10 +479,11 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------ launchers
-static inline int64_t waves_blocks(int64_t waves) { return (waves + 3) / 4; }
+// grid of tile_map(): ceil(tiles / 4) blocks of 4 waves per head
+static inline int64_t tile_blocks(int64_t nbh, int T) { return nbh * (((T >> 5) + 3) >> 2); }
 
 hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) {
-  const int64_t blocks = waves_blocks(static_cast<int64_t>(a.B) * a.H * (a.T / 32));
+  const int64_t blocks = tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T);
   if (D == 64) {
     if (drop) hipLaunchKernelGGL((attn_fwd_kernel<64, true>), dim3(blocks), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((attn_fwd_kernel<64, false>), dim3(blocks), dim3(256), 0, st, a);
@@ -403,8 +498,8 @@ hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
 
 hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) {
   const int64_t rows = static_cast<int64_t>(a.B) * a.H * a.T;
-  const int64_t bq = waves_blocks(static_cast<int64_t>(a.B) * a.H * (a.T / 32));
-  const int64_t bkv = waves_blocks(static_cast<int64_t>(a.B) * a.Hkv * (a.T / 32));
+  const int64_t bq = tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T);
+  const int64_t bkv = tile_blocks(static_cast<int64_t>(a.B) * a.Hkv, a.T);
 #define BWD(DD)                                                                                         \
   hipLaunchKernelGGL((attn_delta_kernel<DD>), dim3((rows + 15) / 16), dim3(256), 0, st, a);             \
   if (drop) {                                                                                           \
@@ -426,12 +521,12 @@ hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
 }
 
 hipError_t launch_transpose_btxd(const void* in, int64_t sb, int64_t st, int64_t sx, void* out, int B, int T, int X,
-                                 int D, hipStream_t stream) {
+                                 int D, int ldt, hipStream_t stream) {
   const dim3 grid(T / 64, B * X);
   const __bf16* i = static_cast<const __bf16*>(in);
   __bf16* o = static_cast<__bf16*>(out);
-  if (D == 64) hipLaunchKernelGGL((transpose_btxd_kernel<64>), grid, dim3(256), 0, stream, i, sb, st, sx, o, T, X);
-  else if (D == 128) hipLaunchKernelGGL((transpose_btxd_kernel<128>), grid, dim3(256), 0, stream, i, sb, st, sx, o, T, X);
+  if (D == 64) hipLaunchKernelGGL((transpose_btxd_kernel<64>), grid, dim3(256), 0, stream, i, sb, st, sx, o, ldt, X);
+  else if (D == 128) hipLaunchKernelGGL((transpose_btxd_kernel<128>), grid, dim3(256), 0, stream, i, sb, st, sx, o, ldt, X);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

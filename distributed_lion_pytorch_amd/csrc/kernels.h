@@ -24,7 +24,7 @@ hipError_t launch_vote_reduce(const uint8_t* recv, int64_t nbytes, const uint8_t
 hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st);
 hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st);
 hipError_t launch_transpose_btxd(const void* in, int64_t sb, int64_t st, int64_t sx, void* out, int B, int T, int X,
-                                 int D, hipStream_t stream);
+                                 int D, int ldt, hipStream_t stream);
 
 // ---- LM head cross-entropy (xent_kernels.hip)
 hipError_t launch_softmax_xent(int dt, void* logits, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,
