@@ -23,6 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import fused
+from ..ops.linear import linear_kn
 
 
 @dataclass
@@ -89,8 +90,7 @@ class Conv1D(nn.Module):
         self.bias = nn.Parameter(torch.zeros(nf))
 
     def forward(self, x):
-        shp = x.shape[:-1] + (self.weight.shape[1],)
-        return torch.addmm(self.bias, x.reshape(-1, x.shape[-1]), self.weight).view(shp)
+        return linear_kn(x, self.weight, self.bias)
 
 
 class Attention(nn.Module):

@@ -58,7 +58,9 @@ def dropout_add(y: torch.Tensor, residual: torch.Tensor, p: float) -> torch.Tens
 # --------------------------------------------------------------- bias + GELU
 def linear_gelu(x2d: torch.Tensor, w_in_out: torch.Tensor, bias: torch.Tensor, exact: bool = False):
     """gelu(x @ W + b) with HF Conv1D's [in, out] weight layout."""
-    h = torch.addmm(bias, x2d, w_in_out)
+    from .linear import linear_kn
+
+    h = linear_kn(x2d, w_in_out, bias)
     return F.gelu(h, approximate="none" if exact else "tanh")
 
 

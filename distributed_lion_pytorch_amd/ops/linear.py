@@ -1,0 +1,96 @@
+"""Linear layers whose weight gradient is a split-K GEMM.
+
+The training GEMMs of a transformer layer have two easy shapes (forward and
+input-gradient: M = tokens, large) and one hard shape: the weight gradient
+dW = X^T dY reduces over all M = B*T tokens (20480 in the GPT-2 bench) into a
+small [K, N] output -- 9-36 256x256 output tiles for GPT-2 -- so a plain GEMM
+fills 9-36 of the 256 CUs.  Measured on MI355X (tools/bench_gemm.py):
+182-490 TF/s for hipBLASLt's own choice vs 540-840 TF/s when the token axis
+is split S ways into a batched GEMM with fp32 output (``bmm(out_dtype=f32)``),
+summed in fp32 and rounded once.  S is picked so that S x tiles ~ 160.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def split_k_factor(M: int, K: int, N: int) -> int:
+    tiles = math.ceil(K / 256) * math.ceil(N / 256)
+    if tiles >= 160:
+        return 1
+    s = 2 ** int(round(math.log2(160.0 / tiles)))
+    s = max(1, min(16, s))
+    while s > 1 and M % s:
+        s //= 2
+    return s
+
+
+def wgrad(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a^T @ b for a [M, K], b [M, N] (-> [K, N]) with token-axis split-K."""
+    M, K = a.shape
+    N = b.shape[1]
+    s = split_k_factor(M, K, N) if a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) else 1
+    if s == 1:
+        return a.t() @ b
+    part = torch.bmm(a.view(s, M // s, K).transpose(1, 2), b.view(s, M // s, N), out_dtype=torch.float32)
+    return part.sum(0).to(a.dtype)
+
+
+class _LinearKN(torch.autograd.Function):
+    """y = x @ W + b with W stored [K, N] (HF Conv1D layout)."""
+
+    @staticmethod
+    def forward(ctx, x2d, w, b):
+        ctx.save_for_backward(x2d, w)
+        ctx.has_b = b is not None
+        return torch.addmm(b, x2d, w) if b is not None else x2d @ w
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2d, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = dy @ w.t() if ctx.needs_input_grad[0] else None
+        dw = wgrad(x2d, dy) if ctx.needs_input_grad[1] else None
+        db = dy.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+class _LinearNK(torch.autograd.Function):
+    """y = x @ W^T + b with W stored [N, K] (nn.Linear layout)."""
+
+    @staticmethod
+    def forward(ctx, x2d, w, b):
+        ctx.save_for_backward(x2d, w)
+        ctx.has_b = b is not None
+        return torch.nn.functional.linear(x2d, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2d, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = dy @ w if ctx.needs_input_grad[0] else None
+        dw = wgrad(dy, x2d) if ctx.needs_input_grad[1] else None
+        db = dy.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def linear_kn(x: torch.Tensor, w: torch.Tensor, b=None) -> torch.Tensor:
+    shp = x.shape[:-1] + (w.shape[1],)
+    x2d = x.reshape(-1, x.shape[-1])
+    if not x.is_cuda:
+        y = torch.addmm(b, x2d, w) if b is not None else x2d @ w
+    else:
+        y = _LinearKN.apply(x2d, w, b)
+    return y.view(shp)
+
+
+def linear_nk(x: torch.Tensor, w: torch.Tensor, b=None) -> torch.Tensor:
+    shp = x.shape[:-1] + (w.shape[0],)
+    x2d = x.reshape(-1, x.shape[-1])
+    if not x.is_cuda:
+        y = torch.nn.functional.linear(x2d, w, b)
+    else:
+        y = _LinearNK.apply(x2d, w, b)
+    return y.view(shp)
