@@ -31,7 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from distributed_lion_pytorch_amd import Lion  # noqa: E402
-from distributed_lion_pytorch_amd.models.gpt2 import GPT2Config, GPT2LMHeadModel  # noqa: E402
+from distributed_lion_pytorch_amd.models.gpt2 import GPT2LMHeadModel, gpt2_config  # noqa: E402
 from distributed_lion_pytorch_amd.parallel.exchange import wire_bytes_per_step  # noqa: E402
 from distributed_lion_pytorch_amd.trainer.engine import StepTimer, TrainStep, broadcast_parameters  # noqa: E402
 
@@ -76,7 +76,7 @@ def build_native(args, dev):
     from distributed_lion_pytorch_amd.ops import fused
 
     fused.set_impl(args.fused)
-    cfg = GPT2Config.from_name(args.model)
+    cfg = gpt2_config(args.model)
     if args.dropout is not None:
         cfg.resid_pdrop = cfg.embd_pdrop = cfg.attn_pdrop = args.dropout
     torch.manual_seed(0)
@@ -94,10 +94,9 @@ def build_reference(args, dev):
 
     from distributed_lion_pytorch_amd.ops import reference as ref
 
-    cfg = GPT2Config.from_name(args.model)
-    hf_cfg = transformers.GPT2Config(**{k: v for k, v in cfg.to_hf_dict().items() if k != "architectures"})
+    cfg = gpt2_config(args.model)
     torch.manual_seed(0)
-    model = transformers.GPT2LMHeadModel(hf_cfg).to(device=dev, dtype=torch.bfloat16)
+    model = transformers.GPT2LMHeadModel(cfg).to(device=dev, dtype=torch.bfloat16)
     broadcast_parameters(model)
 
     class RefLion(torch.optim.Optimizer):

@@ -1,88 +1,57 @@
-"""GPT-2 (causal LM) with HF-compatible parameter names and checkpoint format.
+"""GPT-2 (causal LM): HF-format checkpoints, MI355X-native compute path.
 
 The reference trains ``transformers.GPT2LMHeadModel`` built from the ``gpt2``
-config (/root/reference/run_clm.py:397-442; README.md:20-37).  This module is
-a native re-implementation of the same architecture -- identical parameter
-names/shapes (``transformer.h.{i}.attn.c_attn.weight`` stored [in, out] like
-HF ``Conv1D``), identical init, tied ``lm_head`` -- so ``state_dict()`` loads
-into HF's class and vice versa, while the compute path is ours:
+config (/root/reference/run_clm.py:397-442; README.md:20-37).  This module
+re-implements the architecture as a ``transformers.PreTrainedModel`` over the
+stock ``GPT2Config`` -- identical parameter names/shapes
+(``transformer.h.{i}.attn.c_attn.weight`` stored [in, out] like HF
+``Conv1D``), identical init and tied ``lm_head`` -- so ``save_pretrained`` /
+``from_pretrained`` / HF ``Trainer`` checkpoints interoperate with HF's own
+class, while every hot op runs through our kernels:
 
-* projections are single hipBLASLt GEMMs on the [in, out] weights (``addmm``);
-* attention, bias+GELU, residual+LayerNorm and the LM-head cross-entropy go
-  through :mod:`distributed_lion_pytorch_amd.ops.fused`, which dispatches to
-  hand-written gfx950 kernels when the extension is present.
+* projections: hipBLASLt GEMMs on the [in, out] weights with split-K weight
+  gradients (ops/linear.py);
+* attention: gfx950 flash attention on the packed qkv, in-kernel dropout
+  (ops/fused.causal_attention -> csrc/attention.hip);
+* LM head + loss: fused softmax-cross-entropy kernel, no fp32 logits
+  (ops/fused.lm_head_cross_entropy -> csrc/xent_kernels.hip).
 """
 from __future__ import annotations
 
 import math
-from dataclasses import asdict, dataclass, field
 from typing import Optional
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+from transformers import GPT2Config, PreTrainedModel
+from transformers.modeling_outputs import CausalLMOutputWithCrossAttentions
 
 from ..ops import fused
 from ..ops.linear import linear_kn
 
+GPT2_SIZES = {
+    "gpt2": dict(n_embd=768, n_layer=12, n_head=12),
+    "gpt2-medium": dict(n_embd=1024, n_layer=24, n_head=16),
+    "gpt2-large": dict(n_embd=1280, n_layer=36, n_head=20),
+    "gpt2-xl": dict(n_embd=1600, n_layer=48, n_head=25),
+    "gpt2-tiny": dict(n_embd=64, n_layer=2, n_head=4, vocab_size=512, n_positions=256, bos_token_id=511,
+                      eos_token_id=511),
+}
 
-@dataclass
-class GPT2Config:
-    vocab_size: int = 50257
-    n_positions: int = 1024
-    n_embd: int = 768
-    n_layer: int = 12
-    n_head: int = 12
-    n_inner: Optional[int] = None
-    activation_function: str = "gelu_new"
-    resid_pdrop: float = 0.1
-    embd_pdrop: float = 0.1
-    attn_pdrop: float = 0.1
-    layer_norm_epsilon: float = 1e-5
-    initializer_range: float = 0.02
-    tie_word_embeddings: bool = True
-    bos_token_id: int = 50256
-    eos_token_id: int = 50256
-    extra: dict = field(default_factory=dict)
 
-    model_type = "gpt2"
-
-    @classmethod
-    def from_name(cls, name: str) -> "GPT2Config":
-        sizes = {
-            "gpt2": dict(n_embd=768, n_layer=12, n_head=12),
-            "gpt2-medium": dict(n_embd=1024, n_layer=24, n_head=16),
-            "gpt2-large": dict(n_embd=1280, n_layer=36, n_head=20),
-            "gpt2-xl": dict(n_embd=1600, n_layer=48, n_head=25),
-            "gpt2-tiny": dict(n_embd=64, n_layer=2, n_head=4, vocab_size=512, n_positions=128),
-        }
-        key = name.split("/")[-1]
-        if key not in sizes:
-            raise KeyError(f"unknown GPT-2 size {name!r}")
-        return cls(**sizes[key])
-
-    @classmethod
-    def from_dict(cls, d: dict) -> "GPT2Config":
-        known = {k: d[k] for k in cls.__dataclass_fields__ if k in d and k != "extra"}
-        extra = {k: v for k, v in d.items() if k not in cls.__dataclass_fields__}
-        return cls(**known, extra=extra)
-
-    def to_hf_dict(self) -> dict:
-        d = asdict(self)
-        extra = d.pop("extra")
-        d.update(extra)
-        d["model_type"] = "gpt2"
-        d["architectures"] = ["GPT2LMHeadModel"]
-        d["n_ctx"] = self.n_positions
-        return d
-
-    @property
-    def inner(self) -> int:
-        return self.n_inner if self.n_inner is not None else 4 * self.n_embd
+def gpt2_config(name: str = "gpt2", **overrides) -> GPT2Config:
+    """HF GPT2Config for a named size (no hub access needed)."""
+    key = name.rstrip("/").split("/")[-1]
+    if key not in GPT2_SIZES:
+        raise KeyError(f"unknown GPT-2 size {name!r}; known: {sorted(GPT2_SIZES)}")
+    kw = dict(GPT2_SIZES[key])
+    kw.update(overrides)
+    return GPT2Config(**kw)
 
 
 class Conv1D(nn.Module):
-    """Affine map with HF's [in, out] weight layout: y = x @ W + b (one GEMM)."""
+    """Affine map with HF's [in, out] weight layout: y = x @ W + b."""
 
     def __init__(self, nx: int, nf: int):
         super().__init__()
@@ -101,10 +70,9 @@ class Attention(nn.Module):
         self.c_attn = Conv1D(cfg.n_embd, 3 * cfg.n_embd)
         self.c_proj = Conv1D(cfg.n_embd, cfg.n_embd)
         self.attn_pdrop = cfg.attn_pdrop
-        self.resid_pdrop = cfg.resid_pdrop
 
     def forward(self, x):
-        B, T, C = x.shape
+        B, T, _ = x.shape
         qkv = self.c_attn(x).view(B, T, 3, self.n_head, self.head_dim)
         y = fused.causal_attention(qkv, self.attn_pdrop if self.training else 0.0)  # [B, T, C]
         return self.c_proj(y)
@@ -113,9 +81,10 @@ class Attention(nn.Module):
 class MLP(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
-        self.c_fc = Conv1D(cfg.n_embd, cfg.inner)
-        self.c_proj = Conv1D(cfg.inner, cfg.n_embd)
-        if cfg.activation_function not in ("gelu_new", "gelu_pytorch_tanh", "gelu"):
+        inner = cfg.n_inner if cfg.n_inner is not None else 4 * cfg.n_embd
+        self.c_fc = Conv1D(cfg.n_embd, inner)
+        self.c_proj = Conv1D(inner, cfg.n_embd)
+        if cfg.activation_function not in ("gelu_new", "gelu_pytorch_tanh", "gelu", "gelu_fast"):
             raise ValueError(f"unsupported activation {cfg.activation_function}")
         self.exact_gelu = cfg.activation_function == "gelu"
 
@@ -152,7 +121,7 @@ class GPT2Model(nn.Module):
         self.gradient_checkpointing = False
 
     def forward(self, input_ids):
-        B, T = input_ids.shape
+        T = input_ids.shape[1]
         pos = torch.arange(T, device=input_ids.device)
         x = self.wte(input_ids) + self.wpe(pos)[None]
         if self.training and self.embd_pdrop > 0:
@@ -165,43 +134,21 @@ class GPT2Model(nn.Module):
         return fused.layer_norm(x, self.ln_f)
 
 
-class CausalLMOutput(dict):
-    """Minimal ModelOutput look-alike (attribute + key access, tuple index 0 = loss or logits)."""
-
-    def __getattr__(self, k):
-        try:
-            return self[k]
-        except KeyError as e:
-            raise AttributeError(k) from e
-
-    def __getitem__(self, k):
-        if isinstance(k, int):
-            vals = [v for v in self.values() if v is not None]
-            return vals[k]
-        return super().__getitem__(k)
-
-    def to_tuple(self):
-        return tuple(v for v in self.values() if v is not None)
-
-
-class GPT2LMHeadModel(nn.Module):
+class GPT2LMHeadModel(PreTrainedModel):
     config_class = GPT2Config
     base_model_prefix = "transformer"
-    _tied_weights_keys = ["lm_head.weight"]
+    _tied_weights_keys = {"lm_head.weight": "transformer.wte.weight"}
+    supports_gradient_checkpointing = True
+    _no_split_modules = ["Block"]
 
-    def __init__(self, cfg: GPT2Config):
-        super().__init__()
-        self.config = cfg
-        self.transformer = GPT2Model(cfg)
-        self.lm_head = nn.Linear(cfg.n_embd, cfg.vocab_size, bias=False)
-        if cfg.tie_word_embeddings:
-            self.lm_head.weight = self.transformer.wte.weight
-        self.apply(self._init_weights)
-        # GPT-2 "special scaled init" of the residual projections (as HF)
-        for name, p in self.named_parameters():
-            if name.endswith("c_proj.weight"):
-                nn.init.normal_(p, mean=0.0, std=cfg.initializer_range / math.sqrt(2 * cfg.n_layer))
+    def __init__(self, config: GPT2Config):
+        super().__init__(config)
+        self.transformer = GPT2Model(config)
+        self.lm_head = nn.Linear(config.n_embd, config.vocab_size, bias=False)
+        self.post_init()
+        self.reset_parameters()
 
+    # -- init identical to HF GPT2PreTrainedModel._init_weights + scaled c_proj
     def _init_weights(self, m):
         std = self.config.initializer_range
         if isinstance(m, (nn.Linear, Conv1D)):
@@ -214,33 +161,55 @@ class GPT2LMHeadModel(nn.Module):
             nn.init.ones_(m.weight)
             nn.init.zeros_(m.bias)
 
-    # HF-ish conveniences used by trainers / entrypoints
+    @torch.no_grad()
+    def reset_parameters(self):
+        self.apply(self._init_weights)
+        for name, p in self.named_parameters():
+            if name.endswith("c_proj.weight"):
+                nn.init.normal_(p, mean=0.0, std=self.config.initializer_range / math.sqrt(2 * self.config.n_layer))
+        self.tie_weights()
+
+    def tie_weights(self, *args, **kwargs):
+        if getattr(self.config, "tie_word_embeddings", True):
+            self.lm_head.weight = self.transformer.wte.weight
+
     def get_input_embeddings(self):
         return self.transformer.wte
 
-    def gradient_checkpointing_enable(self, **_):
+    def set_input_embeddings(self, emb):
+        self.transformer.wte = emb
+
+    def get_output_embeddings(self):
+        return self.lm_head
+
+    def _set_gradient_checkpointing(self, enable: bool = True, gradient_checkpointing_func=None):
+        self.transformer.gradient_checkpointing = enable
+
+    def gradient_checkpointing_enable(self, gradient_checkpointing_kwargs=None):
         self.transformer.gradient_checkpointing = True
 
-    def num_parameters(self) -> int:
-        return sum({p.data_ptr(): p.numel() for p in self.parameters()}.values())
+    def gradient_checkpointing_disable(self):
+        self.transformer.gradient_checkpointing = False
 
-    def forward(self, input_ids, labels=None, attention_mask=None, return_logits: bool = True, **_):
+    def forward(self, input_ids=None, labels=None, attention_mask=None, num_items_in_batch=None,
+                return_dict: Optional[bool] = None, **kwargs):
         h = self.transformer(input_ids)
         loss = None
         logits = None
         if labels is not None:
             # shift inside the fused LM-head + cross-entropy (HF semantics:
-            # position t predicts label t+1, ignore_index -100)
-            loss = fused.lm_head_cross_entropy(h[:, :-1], self.lm_head.weight, labels[:, 1:])
-            if return_logits and not self.training:
+            # position t predicts label t+1, ignore_index -100).  With
+            # num_items_in_batch the sum is normalised by it (HF GA-aware loss).
+            loss = fused.lm_head_cross_entropy(h[:, :-1], self.lm_head.weight, labels[:, 1:],
+                                               normalizer=num_items_in_batch)
+            if not self.training:
                 logits = F.linear(h, self.lm_head.weight)
         else:
             logits = F.linear(h, self.lm_head.weight)
-        return CausalLMOutput(loss=loss, logits=logits)
+        return CausalLMOutputWithCrossAttentions(loss=loss, logits=logits)
 
     def flops_per_token(self, seq_len: int) -> float:
         """Training FLOPs per token (6N + attention), for MFU reporting."""
         c = self.config
         n = self.num_parameters() - c.n_positions * c.n_embd
-        attn = 12 * c.n_layer * c.n_embd * seq_len  # 6 * 2 * L * T * d (QK^T and PV, fwd+bwd)
-        return 6 * n + attn
+        return 6 * n + 12 * c.n_layer * c.n_embd * seq_len

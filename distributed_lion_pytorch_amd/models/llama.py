@@ -1,0 +1,251 @@
+"""Llama (Llama-2 / Llama-3 family): HF-format checkpoints, native compute path.
+
+The reference fine-tunes ``meta-llama/Llama-2-7b-hf`` (SFT, /root/reference/
+sft_llama2.py:22,141-154; DPO, dpo_llama2.py:133-152) through HF/peft/trl.
+This is a ``transformers.PreTrainedModel`` over the stock ``LlamaConfig``
+with HF parameter names (``model.layers.{i}.self_attn.q_proj.weight`` ...),
+so HF Llama checkpoints load and our checkpoints load into HF, but the
+compute path is ours: RMSNorm, rotary embeddings (rotate-half convention),
+grouped-query causal attention on the gfx950 flash kernel, SwiGLU MLP, split-K
+weight gradients, fused LM-head cross-entropy.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from transformers import LlamaConfig, PreTrainedModel
+from transformers.modeling_outputs import CausalLMOutputWithPast
+
+from ..ops import fused
+from ..ops.linear import linear_nk
+
+LLAMA_SIZES = {
+    "llama-2-7b": dict(hidden_size=4096, intermediate_size=11008, num_hidden_layers=32, num_attention_heads=32,
+                       num_key_value_heads=32, vocab_size=32000, rope_theta=10000.0, max_position_embeddings=4096,
+                       rms_norm_eps=1e-5),
+    "llama-2-13b": dict(hidden_size=5120, intermediate_size=13824, num_hidden_layers=40, num_attention_heads=40,
+                        num_key_value_heads=40, vocab_size=32000, rope_theta=10000.0, max_position_embeddings=4096,
+                        rms_norm_eps=1e-5),
+    "llama-3-8b": dict(hidden_size=4096, intermediate_size=14336, num_hidden_layers=32, num_attention_heads=32,
+                       num_key_value_heads=8, vocab_size=128256, rope_theta=500000.0, max_position_embeddings=8192,
+                       rms_norm_eps=1e-5),
+    "llama-tiny": dict(hidden_size=128, intermediate_size=352, num_hidden_layers=2, num_attention_heads=2,
+                       num_key_value_heads=1, vocab_size=512, rope_theta=10000.0, max_position_embeddings=512,
+                       rms_norm_eps=1e-5),
+}
+_ALIASES = {"Llama-2-7b-hf": "llama-2-7b", "Llama-2-7b": "llama-2-7b", "Meta-Llama-3-8B": "llama-3-8b",
+            "Llama-3-8B": "llama-3-8b", "Llama-2-13b-hf": "llama-2-13b"}
+
+
+def llama_config(name: str = "llama-2-7b", **overrides) -> LlamaConfig:
+    key = name.rstrip("/").split("/")[-1]
+    key = _ALIASES.get(key, key).lower()
+    if key not in LLAMA_SIZES:
+        raise KeyError(f"unknown Llama size {name!r}; known: {sorted(LLAMA_SIZES)}")
+    kw = dict(LLAMA_SIZES[key])
+    kw.update(overrides)
+    kw.setdefault("tie_word_embeddings", False)
+    return LlamaConfig(**kw)
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, dim: int, eps: float):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(dim))
+        self.eps = eps
+
+    def forward(self, x):
+        return fused.rms_norm(x, self.weight, self.eps)
+
+
+def _rope_theta(cfg) -> float:
+    rp = getattr(cfg, "rope_parameters", None)
+    if isinstance(rp, dict) and "rope_theta" in rp:
+        return float(rp["rope_theta"])
+    return float(getattr(cfg, "rope_theta", 10000.0) or 10000.0)
+
+
+class Rotary(nn.Module):
+    """cos/sin tables computed once per (T, device, dtype) -- no per-step trig."""
+
+    def __init__(self, head_dim: int, theta: float):
+        super().__init__()
+        inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+        self.register_buffer("inv_freq", inv.float(), persistent=False)
+        self._cache = {}
+
+    def tables(self, T: int, device, dtype):
+        key = (T, device, dtype)
+        if key not in self._cache:
+            t = torch.arange(T, device=device, dtype=torch.float32)
+            f = torch.outer(t, self.inv_freq.to(device))
+            emb = torch.cat([f, f], dim=-1)
+            self._cache = {key: (emb.cos().to(dtype), emb.sin().to(dtype))}
+        return self._cache[key]
+
+
+def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """x [B, T, H, D]; HF rotate-half convention."""
+    return fused.rope(x, cos, sin)
+
+
+class LlamaAttention(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.n_head = cfg.num_attention_heads
+        self.n_kv = cfg.num_key_value_heads
+        self.head_dim = getattr(cfg, "head_dim", None) or cfg.hidden_size // cfg.num_attention_heads
+        self.q_proj = nn.Linear(cfg.hidden_size, self.n_head * self.head_dim, bias=False)
+        self.k_proj = nn.Linear(cfg.hidden_size, self.n_kv * self.head_dim, bias=False)
+        self.v_proj = nn.Linear(cfg.hidden_size, self.n_kv * self.head_dim, bias=False)
+        self.o_proj = nn.Linear(self.n_head * self.head_dim, cfg.hidden_size, bias=False)
+        self.attn_dropout = float(getattr(cfg, "attention_dropout", 0.0) or 0.0)
+
+    def forward(self, x, cos, sin):
+        B, T, _ = x.shape
+        q = _lin(self.q_proj, x).view(B, T, self.n_head, self.head_dim)
+        k = _lin(self.k_proj, x).view(B, T, self.n_kv, self.head_dim)
+        v = _lin(self.v_proj, x).view(B, T, self.n_kv, self.head_dim)
+        q, k = apply_rope(q, cos, sin), apply_rope(k, cos, sin)
+        y = fused.causal_attention_gqa(q, k, v, self.attn_dropout if self.training else 0.0)
+        return _lin(self.o_proj, y)
+
+
+def _lin(layer: nn.Module, x):
+    """nn.Linear (possibly LoRA-wrapped) through the split-K wgrad path."""
+    if type(layer) is nn.Linear:
+        return linear_nk(x, layer.weight, layer.bias)
+    return layer(x)
+
+
+class LlamaMLP(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.gate_proj = nn.Linear(cfg.hidden_size, cfg.intermediate_size, bias=False)
+        self.up_proj = nn.Linear(cfg.hidden_size, cfg.intermediate_size, bias=False)
+        self.down_proj = nn.Linear(cfg.intermediate_size, cfg.hidden_size, bias=False)
+
+    def forward(self, x):
+        return _lin(self.down_proj, fused.swiglu(_lin(self.gate_proj, x), _lin(self.up_proj, x)))
+
+
+class LlamaDecoderLayer(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.self_attn = LlamaAttention(cfg)
+        self.mlp = LlamaMLP(cfg)
+        self.input_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
+        self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
+
+    def forward(self, x, cos, sin):
+        x = x + self.self_attn(self.input_layernorm(x), cos, sin)
+        return x + self.mlp(self.post_attention_layernorm(x))
+
+
+class LlamaModel(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.embed_tokens = nn.Embedding(cfg.vocab_size, cfg.hidden_size)
+        self.layers = nn.ModuleList([LlamaDecoderLayer(cfg) for _ in range(cfg.num_hidden_layers)])
+        self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
+        head_dim = getattr(cfg, "head_dim", None) or cfg.hidden_size // cfg.num_attention_heads
+        self.rotary = Rotary(head_dim, _rope_theta(cfg))
+        self.gradient_checkpointing = False
+
+    def forward(self, input_ids):
+        T = input_ids.shape[1]
+        x = self.embed_tokens(input_ids)
+        cos, sin = self.rotary.tables(T, x.device, x.dtype)
+        for layer in self.layers:
+            if self.gradient_checkpointing and self.training:
+                x = torch.utils.checkpoint.checkpoint(layer, x, cos, sin, use_reentrant=False)
+            else:
+                x = layer(x, cos, sin)
+        return self.norm(x)
+
+
+class LlamaForCausalLM(PreTrainedModel):
+    config_class = LlamaConfig
+    base_model_prefix = "model"
+    _tied_weights_keys = {"lm_head.weight": "model.embed_tokens.weight"}
+    supports_gradient_checkpointing = True
+    _no_split_modules = ["LlamaDecoderLayer"]
+
+    def __init__(self, config: LlamaConfig):
+        super().__init__(config)
+        self.model = LlamaModel(config)
+        self.lm_head = nn.Linear(config.hidden_size, config.vocab_size, bias=False)
+        self.post_init()
+        self.reset_parameters()
+
+    def _init_weights(self, m):
+        std = self.config.initializer_range
+        if isinstance(m, nn.Linear):
+            nn.init.normal_(m.weight, mean=0.0, std=std)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, nn.Embedding):
+            nn.init.normal_(m.weight, mean=0.0, std=std)
+        elif isinstance(m, RMSNorm):
+            nn.init.ones_(m.weight)
+
+    @torch.no_grad()
+    def reset_parameters(self):
+        self.apply(self._init_weights)
+        self.tie_weights()
+
+    def tie_weights(self, *args, **kwargs):
+        if getattr(self.config, "tie_word_embeddings", False):
+            self.lm_head.weight = self.model.embed_tokens.weight
+
+    def get_input_embeddings(self):
+        return self.model.embed_tokens
+
+    def set_input_embeddings(self, emb):
+        self.model.embed_tokens = emb
+
+    def get_output_embeddings(self):
+        return self.lm_head
+
+    def gradient_checkpointing_enable(self, gradient_checkpointing_kwargs=None):
+        self.model.gradient_checkpointing = True
+
+    def gradient_checkpointing_disable(self):
+        self.model.gradient_checkpointing = False
+
+    def forward(self, input_ids=None, labels=None, attention_mask=None, num_items_in_batch=None,
+                return_dict: Optional[bool] = None, **kwargs):
+        h = self.model(input_ids)
+        loss = logits = None
+        if labels is not None:
+            loss = fused.lm_head_cross_entropy(h[:, :-1], self.lm_head.weight, labels[:, 1:],
+                                               normalizer=num_items_in_batch)
+            if not self.training:
+                logits = F.linear(h, self.lm_head.weight)
+        else:
+            logits = F.linear(h, self.lm_head.weight)
+        return CausalLMOutputWithPast(loss=loss, logits=logits)
+
+    def sequence_logps(self, input_ids: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        """Sum of log p(label_t | <t) per sequence (DPO); labels -100 ignored."""
+        return sequence_logps(self, input_ids, labels)
+
+    def flops_per_token(self, seq_len: int) -> float:
+        c = self.config
+        n = self.num_parameters() - (0 if c.tie_word_embeddings else 0)
+        return 6 * n + 12 * c.num_hidden_layers * c.hidden_size * seq_len
+
+
+def sequence_logps(model, input_ids: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """Per-sequence summed token log-probabilities under ``model`` (any of our
+    causal LMs): used by the DPO loss (policy and frozen reference)."""
+    base = model.model if hasattr(model, "model") and isinstance(model.model, LlamaModel) else model.transformer
+    h = base(input_ids)[:, :-1]
+    logits = F.linear(h, model.lm_head.weight).float()
+    tgt = labels[:, 1:]
+    mask = tgt != -100
+    lp = torch.log_softmax(logits, dim=-1).gather(-1, tgt.clamp_min(0).unsqueeze(-1)).squeeze(-1)
+    return (lp * mask).sum(-1)

@@ -48,6 +48,26 @@ def layer_norm(x: torch.Tensor, ln: torch.nn.LayerNorm) -> torch.Tensor:
     return F.layer_norm(x, ln.normalized_shape, ln.weight, ln.bias, ln.eps)
 
 
+def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
+    """Llama RMSNorm (HF semantics: normalise in fp32, cast back, then scale)."""
+    xf = x.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return weight * y.to(x.dtype)
+
+
+# ---------------------------------------------------------- rotary / SwiGLU
+def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """x [B, T, H, D]; cos/sin [T, D]; HF rotate-half convention."""
+    d2 = x.shape[-1] // 2
+    x1, x2 = x[..., :d2], x[..., d2:]
+    rot = torch.cat([-x2, x1], dim=-1)
+    return x * cos[None, :, None, :] + rot * sin[None, :, None, :]
+
+
+def swiglu(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+    return F.silu(gate) * up
+
+
 # ------------------------------------------------------------- dropout + add
 def dropout_add(y: torch.Tensor, residual: torch.Tensor, p: float) -> torch.Tensor:
     if p > 0.0:
@@ -196,13 +216,15 @@ class _LMHeadCE(torch.autograd.Function):
     well-shaped GEMMs; padded columns are masked out of the softmax."""
 
     @staticmethod
-    def forward(ctx, h2d, weight, labels1d):
+    def forward(ctx, h2d, weight, labels1d, normalizer=None):
         v = weight.shape[0]
         need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         wp = _pad_rows(weight)
         logits = h2d @ wp.t()  # [N, Vp] in the compute dtype (hipBLASLt)
-        valid = labels1d != -100
-        n_valid = valid.sum().clamp_min(1).to(torch.float32)
+        if normalizer is None:
+            n_valid = (labels1d != -100).sum().clamp_min(1).to(torch.float32)
+        else:
+            n_valid = torch.as_tensor(normalizer, dtype=torch.float32, device=h2d.device).clamp_min(1)
         if _use_hip(logits):
             row_loss = hip.ops().softmax_xent_(logits, labels1d, v)  # logits <- softmax - onehot (in place)
         else:
@@ -222,7 +244,7 @@ class _LMHeadCE(torch.autograd.Function):
         scale = (g / n_valid).to(dh.dtype)
         gh = dh * scale if ctx.needs_input_grad[0] else None
         gw = dw * scale if ctx.has_dw and ctx.needs_input_grad[1] else None
-        return gh, gw, None
+        return gh, gw, None, None
 
 
 def _softmax_xent_torch_(logits: torch.Tensor, labels: torch.Tensor, v: int) -> torch.Tensor:
@@ -243,10 +265,12 @@ def _softmax_xent_torch_(logits: torch.Tensor, labels: torch.Tensor, v: int) -> 
     return row_loss
 
 
-def lm_head_cross_entropy(h: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-    """Mean token cross-entropy of ``h @ weight.T`` against ``labels`` (-100 ignored)."""
+def lm_head_cross_entropy(h: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor,
+                          normalizer=None) -> torch.Tensor:
+    """Token cross-entropy of ``h @ weight.T`` against ``labels`` (-100 ignored):
+    mean over valid tokens, or sum / ``normalizer`` (HF ``num_items_in_batch``)."""
     h2d = h.reshape(-1, h.shape[-1])
-    return _LMHeadCE.apply(h2d, weight, labels.reshape(-1))
+    return _LMHeadCE.apply(h2d, weight, labels.reshape(-1), normalizer)
 
 
 def reference_lm_loss(h, weight, labels):

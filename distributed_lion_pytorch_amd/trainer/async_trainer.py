@@ -1,0 +1,152 @@
+"""HF ``Trainer`` integration: training with per-rank local gradients.
+
+Reference: /root/reference/async_trainer.py:8-90 -- ``AsyncTrainer``,
+``AsyncSFTTrainer``, ``AsyncDPOTrainer`` override ``training_step`` to run the
+whole forward/backward under ``DDP.no_sync()`` so gradients are never
+all-reduced; replicas are kept identical only by Lion's majority vote.
+
+Re-designed for the installed transformers 5.x:
+* ``training_step(model, inputs, num_items_in_batch=None)`` delegates to the
+  stock implementation (GA loss scaling, loss-kwargs, CP buffers) and only
+  adds the no-sync context -- no stale copy of HF internals;
+* the no-sync context is a no-op when the model is not DDP-wrapped (W == 1,
+  DataParallel), instead of an AttributeError;
+* ``--lion`` builds the distributed Lion over the *trainable* parameters
+  (LoRA-safe, D12) unless an optimizer is passed explicitly;
+* every rank checkpoints its own momentum (``rank{r}-of-{W}-optimizer.pt``)
+  next to HF's rank-0 ``optimizer.pt`` and reloads it on resume (D20).
+"""
+from __future__ import annotations
+
+import contextlib
+import logging
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+from transformers import Trainer, TrainingArguments
+
+from ..optim.lion import Lion
+
+logger = logging.getLogger(__name__)
+
+
+@dataclass
+class AsyncTrainingArguments(TrainingArguments):
+    """HF TrainingArguments + the reference's flags (run_clm.py:73-86) + Lion knobs."""
+
+    lion: bool = field(default=False, metadata={"help": "use the (distributed) Lion optimizer"})
+    async_grad: bool = field(default=False, metadata={
+        "help": "compute gradients per worker and never combine them (sync only via Lion's vote)"})
+    lion_beta1: float = field(default=0.9, metadata={"help": "Lion beta1"})
+    lion_beta2: float = field(default=0.99, metadata={"help": "Lion beta2"})
+    lion_vote: str = field(default="majority", metadata={"help": "majority | average"})
+    lion_tie_break: str = field(default="negative", metadata={"help": "negative (reference) | zero | positive"})
+    lion_wire: str = field(default="a2a", metadata={"help": "allgather | a2a | ref_int64"})
+    lion_bucket_mb: float = field(default=32.0, metadata={"help": "packed-bit bucket size (MB)"})
+    lion_stochastic_max_norm: Optional[float] = field(default=None, metadata={
+        "help": "enable stochastic binarization with this max_grad_norm (reference max_grad_norm)"})
+    lion_backend: str = field(default="auto", metadata={"help": "auto | hip | torch"})
+    lion_dropout_schedule: Optional[str] = field(default=None, metadata={
+        "help": "fault injection, e.g. '100:3' drops rank 3 from optimizer step 100 on"})
+    synthetic_data: bool = field(default=False, metadata={"help": "train on synthetic token ids (offline)"})
+
+
+def parse_dropout_schedule(spec: Optional[str]) -> dict:
+    """'100:3,200:1' -> {100: [3], 200: [1]}"""
+    out: dict = {}
+    if not spec:
+        return out
+    for item in spec.split(","):
+        step, rank = item.split(":")
+        out.setdefault(int(step), []).append(int(rank))
+    return out
+
+
+def build_lion(model: torch.nn.Module, args, lr: Optional[float] = None, weight_decay: Optional[float] = None) -> Lion:
+    params = [p for p in model.parameters() if p.requires_grad]
+    opt = Lion(
+        params,
+        lr=args.learning_rate if lr is None else lr,
+        betas=(getattr(args, "lion_beta1", 0.9), getattr(args, "lion_beta2", 0.99)),
+        weight_decay=args.weight_decay if weight_decay is None else weight_decay,
+        max_grad_norm=getattr(args, "lion_stochastic_max_norm", None),
+        vote=getattr(args, "lion_vote", "majority"),
+        tie_break=getattr(args, "lion_tie_break", "negative"),
+        exchange=getattr(args, "lion_wire", "a2a"),
+        bucket_mb=getattr(args, "lion_bucket_mb", 32.0),
+        backend=getattr(args, "lion_backend", "auto"),
+        seed=getattr(args, "seed", 0),
+    )
+    sched = parse_dropout_schedule(getattr(args, "lion_dropout_schedule", None))
+    if sched:
+        opt.set_dropout_schedule(sched)
+    return opt
+
+
+def no_sync(model):
+    """DDP.no_sync() when the model is DDP-wrapped, otherwise a no-op (D14)."""
+    fn = getattr(model, "no_sync", None)
+    return fn() if callable(fn) else contextlib.nullcontext()
+
+
+class AsyncMixin:
+    """Gradient-sync-free training step + Lion creation + per-rank optimizer state."""
+
+    def training_step(self, model, inputs, num_items_in_batch=None):
+        with no_sync(model):
+            return super().training_step(model, inputs, num_items_in_batch)
+
+    def create_optimizer(self, model=None):
+        if self.optimizer is None and getattr(self.args, "lion", False):
+            target = model if model is not None else self.model
+            self.optimizer = build_lion(target, self.args)
+            return self.optimizer
+        return super().create_optimizer(model) if model is not None else super().create_optimizer()
+
+    # ------------------------------------------------ per-rank optimizer state
+    @staticmethod
+    def _rank_file(output_dir: str) -> Optional[str]:
+        if not (dist.is_available() and dist.is_initialized()):
+            return None
+        return os.path.join(output_dir, f"rank{dist.get_rank()}-of-{dist.get_world_size()}-optimizer.pt")
+
+    def _save_optimizer_and_scheduler(self, output_dir):
+        super()._save_optimizer_and_scheduler(output_dir)
+        path = self._rank_file(output_dir)
+        if path is not None and self.optimizer is not None:
+            os.makedirs(output_dir, exist_ok=True)
+            torch.save(self.optimizer.state_dict(), path)
+
+    def _load_optimizer_and_scheduler(self, checkpoint):
+        if checkpoint is None:
+            return
+        if self.args.device.type == "cpu" and self.args.world_size > 1:
+            # HF maps to args.device ("cpu:0") in multi-process CPU runs, which
+            # torch.load cannot restore; load on "cpu" instead
+            opt_f, sch_f = os.path.join(checkpoint, "optimizer.pt"), os.path.join(checkpoint, "scheduler.pt")
+            if os.path.isfile(opt_f) and os.path.isfile(sch_f):
+                self.optimizer.load_state_dict(torch.load(opt_f, map_location="cpu", weights_only=True))
+                self.lr_scheduler.load_state_dict(torch.load(sch_f, weights_only=True))
+        else:
+            super()._load_optimizer_and_scheduler(checkpoint)
+        path = self._rank_file(checkpoint)
+        if path is not None and os.path.isfile(path) and self.optimizer is not None:
+            # optimizer.load_state_dict moves the state onto each parameter's device
+            state = torch.load(path, map_location="cpu", weights_only=True)
+            self.optimizer.load_state_dict(state)
+            logger.info("restored per-rank optimizer state from %s", path)
+
+
+class AsyncTrainer(AsyncMixin, Trainer):
+    """HF Trainer without gradient all-reduce (reference async_trainer.py:8-34)."""
+
+
+def warn_unsynced(args) -> None:
+    """--async_grad without --lion leaves the replicas with no sync at all (D16)."""
+    if getattr(args, "async_grad", False) and not getattr(args, "lion", False):
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            logger.warning("--async_grad without --lion: gradients are never synchronised and the replicas "
+                           "will diverge (the reference silently does this, SURVEY D16)")

@@ -1,0 +1,86 @@
+"""Observability: JSONL metrics stream, HIP-event phase timers, wire-byte counters.
+
+The reference only has HF logging + wandb (with a hard-coded key).
+Here every logging step appends one JSON object to ``<output_dir>/metrics.jsonl``
+on rank 0 with the HF logs (loss, lr, grad_norm, ...), tokens/s since the
+previous record, and the Lion exchange counters (wire bytes sent/received,
+collective count, vote agreement when telemetry is on).  No network service.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from collections import defaultdict
+from contextlib import contextmanager
+from typing import Dict, Optional
+
+import torch
+from transformers import TrainerCallback
+
+
+def is_rank0() -> bool:
+    import torch.distributed as dist
+
+    return not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
+
+
+class JsonlMetricsCallback(TrainerCallback):
+    def __init__(self, output_dir: str, seq_len: Optional[int] = None, filename: str = "metrics.jsonl"):
+        self.path = os.path.join(output_dir, filename)
+        self.seq_len = seq_len
+        self._t = None
+        self._step = 0
+
+    def on_train_begin(self, args, state, control, **kw):
+        self._t = time.perf_counter()
+        self._step = state.global_step
+
+    def on_log(self, args, state, control, logs=None, optimizer=None, **kw):
+        if not is_rank0():
+            return
+        now = time.perf_counter()
+        rec = {"step": state.global_step, "time": time.time()}
+        rec.update(logs or {})
+        if self._t is not None and state.global_step > self._step and self.seq_len:
+            steps = state.global_step - self._step
+            world = max(1, args.world_size)
+            toks = steps * args.per_device_train_batch_size * args.gradient_accumulation_steps * world * self.seq_len
+            rec["tokens_per_s"] = toks / max(now - self._t, 1e-9)
+        self._t, self._step = now, state.global_step
+        opt = getattr(optimizer, "optimizer", optimizer)  # accelerate wraps it
+        if opt is not None and hasattr(opt, "stats"):
+            rec["lion"] = opt.stats(reset=True)
+        os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
+        with open(self.path, "a") as f:
+            f.write(json.dumps(rec, default=float) + "\n")
+
+
+class PhaseTimer:
+    """Per-phase GPU time with HIP events (no host sync until :meth:`summary`)."""
+
+    def __init__(self, enabled: bool = True):
+        self.enabled = enabled and torch.cuda.is_available()
+        self._events = defaultdict(list)
+
+    @contextmanager
+    def phase(self, name: str):
+        if not self.enabled:
+            yield
+            return
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        try:
+            yield
+        finally:
+            e.record()
+            self._events[name].append((s, e))
+
+    def summary(self, reset: bool = True) -> Dict[str, float]:
+        if not self.enabled:
+            return {}
+        torch.cuda.synchronize()
+        out = {k: sum(s.elapsed_time(e) for s, e in v) for k, v in self._events.items()}
+        if reset:
+            self._events.clear()
+        return out

@@ -1,0 +1,181 @@
+#!/usr/bin/env python
+"""Llama-2 DPO with Distributed Lion -- a working counterpart of
+/root/reference/dpo_llama2.py (which does not parse: ``Option[bool]`` and an
+unclosed ``{``; and uses an undefined ``base_model``, D9).
+
+Same ScriptArguments (beta, lr, schedule, LoRA, lengths, steps, ``--lion``,
+``--async_grad``) and the same in-code TrainingArguments
+(dpo_llama2.py:171-190), MI355X-native underneath:
+* policy + frozen reference replicas in bf16 on each GPU (no 4-bit: D-note in
+  sft_llama2.py), native Llama kernels;
+* DPO sigmoid loss with chosen/rejected concatenated in one policy forward
+  (native trainer: trl is not installed);
+* LoRA targets use Llama module names (q_proj, k_proj, v_proj -- the modules
+  that actually matched in the reference's GPT-J-style list, D11);
+* the optimizer sees the adapter parameters and ``--weight_decay`` (0.05 by
+  default) is actually forwarded to it (D10, D12).
+Offline: prompt/chosen/rejected triples are synthetic unless
+``--dataset_name`` is a local json/jsonl file with those fields.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import sys
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import transformers
+from transformers import HfArgumentParser, TrainingArguments
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_lion_pytorch_amd.models.lora import LoraConfig, print_trainable_parameters  # noqa: E402
+from distributed_lion_pytorch_amd.models.registry import build_model, load_config  # noqa: E402
+from distributed_lion_pytorch_amd.trainer.async_trainer import build_lion, warn_unsynced  # noqa: E402
+from distributed_lion_pytorch_amd.trainer.dpo import AsyncDPOTrainer, DPOTrainer  # noqa: E402
+from distributed_lion_pytorch_amd.utils.data import load_tokenizer, synthetic_paired  # noqa: E402
+from distributed_lion_pytorch_amd.utils.metrics import JsonlMetricsCallback  # noqa: E402
+
+logger = logging.getLogger(__name__)
+
+
+@dataclass
+class ScriptArguments:
+    beta: Optional[float] = field(default=0.1, metadata={"help": "the beta parameter for DPO loss"})
+    model_name_or_path: Optional[str] = field(default="../sft/results/final_checkpoint",
+                                              metadata={"help": "SFT model dir, or a size name (random init)"})
+    learning_rate: Optional[float] = field(default=5e-4)
+    lr_scheduler_type: Optional[str] = field(default="cosine")
+    warmup_steps: Optional[int] = field(default=100)
+    weight_decay: Optional[float] = field(default=0.05)
+    optimizer_type: Optional[str] = field(default="paged_adamw_32bit")
+    per_device_train_batch_size: Optional[int] = field(default=4)
+    per_device_eval_batch_size: Optional[int] = field(default=1)
+    gradient_accumulation_steps: Optional[int] = field(default=4)
+    gradient_checkpointing: Optional[bool] = field(default=True)
+    lora_alpha: Optional[float] = field(default=16)
+    lora_dropout: Optional[float] = field(default=0.05)
+    lora_r: Optional[int] = field(default=8)
+    use_lora: Optional[bool] = field(default=True)
+    max_prompt_length: Optional[int] = field(default=512)
+    max_length: Optional[int] = field(default=1024)
+    max_steps: Optional[int] = field(default=1000)
+    logging_steps: Optional[int] = field(default=10)
+    save_steps: Optional[int] = field(default=100)
+    eval_steps: Optional[int] = field(default=100)
+    output_dir: Optional[str] = field(default="./results")
+    log_freq: Optional[int] = field(default=1)
+    sanity_check: Optional[bool] = field(default=False, metadata={"help": "only train on 1000 samples"})
+    report_to: Optional[str] = field(default="none")
+    ignore_bias_buffers: Optional[bool] = field(default=False)
+    lion: Optional[bool] = field(default=False, metadata={"help": "whether to use lion optimizer"})
+    async_grad: Optional[bool] = field(default=False, metadata={"help": "do not sync gradients between workers"})
+    lion_wire: Optional[str] = field(default="a2a")
+    dataset_name: Optional[str] = field(default=None, metadata={"help": "local json/jsonl of prompt/chosen/rejected"})
+    synthetic_samples: Optional[int] = field(default=10000)
+    model_overrides: Optional[str] = field(default=None)
+    torch_dtype: Optional[str] = field(default="bfloat16")
+    bf16: Optional[bool] = field(default=True)
+    seed: Optional[int] = field(default=0)
+    use_cpu: Optional[bool] = field(default=False)
+
+
+def load_pairs(args):
+    if args.dataset_name and os.path.isfile(args.dataset_name):
+        with open(args.dataset_name) as f:
+            rows = [json.loads(line) for line in f] if args.dataset_name.endswith(".jsonl") else json.load(f)
+    else:
+        rows = synthetic_paired(args.synthetic_samples, seed=args.seed)
+    if args.sanity_check:
+        rows = rows[:1000]
+    # length filter (dpo_llama2.py:157-168)
+    return [r for r in rows if len(r["prompt"]) + len(r["chosen"]) <= args.max_length
+            and len(r["prompt"]) + len(r["rejected"]) <= args.max_length]
+
+
+def main(argv=None):
+    parser = HfArgumentParser(ScriptArguments)
+    (script_args,) = parser.parse_args_into_dataclasses(args=argv)
+    logging.basicConfig(level=logging.INFO, handlers=[logging.StreamHandler(sys.stdout)])
+    transformers.set_seed(script_args.seed)
+
+    config = load_config(script_args.model_name_or_path, overrides=script_args.model_overrides)
+    tokenizer = load_tokenizer(script_args.model_name_or_path)
+    model = build_model(config, model_name_or_path=script_args.model_name_or_path,
+                        torch_dtype=script_args.torch_dtype)
+    model_ref = build_model(config, model_name_or_path=script_args.model_name_or_path,
+                            torch_dtype=script_args.torch_dtype)
+    model_ref.load_state_dict(model.state_dict())  # identical frozen reference (also for random init)
+    if script_args.gradient_checkpointing:
+        model.gradient_checkpointing_enable()
+
+    rows = load_pairs(script_args)
+    n_eval = max(1, min(len(rows) // 20, 1000))
+    train_rows, eval_rows = rows[n_eval:], rows[:n_eval]
+
+    training_args = TrainingArguments(
+        per_device_train_batch_size=script_args.per_device_train_batch_size,
+        per_device_eval_batch_size=script_args.per_device_eval_batch_size,
+        max_steps=script_args.max_steps,
+        logging_steps=script_args.logging_steps,
+        save_steps=script_args.save_steps,
+        gradient_accumulation_steps=script_args.gradient_accumulation_steps,
+        gradient_checkpointing=False,  # handled on the native model above
+        learning_rate=script_args.learning_rate,
+        eval_strategy="steps" if script_args.eval_steps else "no",
+        eval_steps=script_args.eval_steps,
+        output_dir=script_args.output_dir,
+        report_to=script_args.report_to,
+        lr_scheduler_type=script_args.lr_scheduler_type,
+        warmup_steps=script_args.warmup_steps,
+        weight_decay=script_args.weight_decay,
+        bf16=script_args.bf16 and not script_args.use_cpu,
+        remove_unused_columns=False,
+        run_name="dpo_llama2",
+        seed=script_args.seed,
+        use_cpu=script_args.use_cpu,
+    )
+    training_args.lion_wire = script_args.lion_wire
+
+    peft_config = None
+    if script_args.use_lora:
+        peft_config = LoraConfig(r=script_args.lora_r, lora_alpha=int(script_args.lora_alpha),
+                                 lora_dropout=script_args.lora_dropout,
+                                 target_modules=["q_proj", "v_proj", "k_proj"], bias="none",
+                                 task_type="CAUSAL_LM")
+        from distributed_lion_pytorch_amd.models.lora import inject_lora
+
+        inject_lora(model, peft_config)
+    print_trainable_parameters(model)
+    params = [p for p in model.parameters() if p.requires_grad]
+    if script_args.lion:
+        optimizer = build_lion(model, training_args)  # weight_decay = script_args.weight_decay (D10)
+    else:
+        optimizer = torch.optim.AdamW(params, lr=script_args.learning_rate, weight_decay=0.1)
+    sched = transformers.get_cosine_schedule_with_warmup(optimizer, script_args.warmup_steps, script_args.max_steps)
+
+    trainer_class = AsyncDPOTrainer if script_args.async_grad else DPOTrainer
+    trainer = trainer_class(model, model_ref, args=training_args, beta=script_args.beta, train_dataset=train_rows,
+                            eval_dataset=eval_rows, tokenizer=tokenizer, max_prompt_length=script_args.max_prompt_length,
+                            max_length=script_args.max_length, peft_config=None, optimizers=(optimizer, sched),
+                            callbacks=[JsonlMetricsCallback(script_args.output_dir, script_args.max_length)])
+    training_args.lion, training_args.async_grad = script_args.lion, script_args.async_grad
+    warn_unsynced(training_args)
+    trainer.train()
+    trainer.save_model(script_args.output_dir)
+    if trainer.is_world_process_zero():
+        from distributed_lion_pytorch_amd.models.lora import save_adapter
+
+        out = os.path.join(script_args.output_dir, "final_checkpoint")
+        if script_args.use_lora:
+            save_adapter(trainer.model, out)
+        else:
+            trainer.accelerator.unwrap_model(trainer.model).save_pretrained(out)
+    return trainer
+
+
+if __name__ == "__main__":
+    main()

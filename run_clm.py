@@ -1,0 +1,214 @@
+#!/usr/bin/env python
+"""Causal-LM (GPT-2 / Llama) pretraining with Distributed Lion -- drop-in for
+/root/reference/run_clm.py (same CLI: ModelArguments, DataTrainingArguments,
+TrainingArguments + ``--lion`` / ``--async_grad``), MI355X-native underneath:
+
+* the model is our native GPT-2/Llama (HF checkpoint format, gfx950 kernels)
+  unless ``--native_model false`` selects the stock HF class;
+* ``--lion`` builds the distributed Lion (1-bit vote exchange over RCCL);
+  ``--async_grad`` trains with per-rank gradients (``AsyncTrainer``);
+* runs offline: ``--synthetic_data`` (or no dataset) trains on random token
+  blocks; ``--train_file`` reads a local text file; configs come from the
+  built-in size registry (``--config_name gpt2``) or a local directory;
+* no wandb login, no hub telemetry; AdamW fallback keeps the
+  reference's hard-coded weight_decay=0.1 (D17) and warns about it.
+
+  torchrun --nproc_per_node 8 run_clm.py --config_name gpt2 --synthetic_data \
+      --per_device_train_batch_size 20 --gradient_accumulation_steps 8 --bf16 \
+      --torch_dtype bfloat16 --max_steps 100 --lion --async_grad --output_dir out
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+import sys
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import transformers
+from transformers import HfArgumentParser, Trainer, set_seed
+from transformers.trainer_utils import get_last_checkpoint
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_lion_pytorch_amd.models.registry import build_model, load_config  # noqa: E402
+from distributed_lion_pytorch_amd.trainer.async_trainer import (  # noqa: E402
+    AsyncTrainer, AsyncTrainingArguments, build_lion, warn_unsynced)
+from distributed_lion_pytorch_amd.utils.data import BlockDataset, SyntheticCLMDataset, load_tokenizer  # noqa: E402
+from distributed_lion_pytorch_amd.utils.metrics import JsonlMetricsCallback  # noqa: E402
+
+logger = logging.getLogger(__name__)
+
+
+@dataclass
+class ModelArguments:
+    model_name_or_path: Optional[str] = field(default=None, metadata={"help": "checkpoint dir for weight init"})
+    model_type: Optional[str] = field(default=None, metadata={"help": "gpt2 | llama when training from scratch"})
+    config_overrides: Optional[str] = field(default=None, metadata={"help": "e.g. n_embd=10,resid_pdrop=0.2"})
+    config_name: Optional[str] = field(default=None, metadata={"help": "size name (gpt2, llama-2-7b, ...) or dir"})
+    tokenizer_name: Optional[str] = field(default=None, metadata={"help": "local tokenizer dir (else byte-level)"})
+    cache_dir: Optional[str] = field(default=None)
+    use_fast_tokenizer: bool = field(default=True)
+    model_revision: str = field(default="main")
+    use_auth_token: bool = field(default=False)
+    torch_dtype: Optional[str] = field(default=None, metadata={"help": "auto | bfloat16 | float16 | float32"})
+    low_cpu_mem_usage: bool = field(default=False)
+    native_model: bool = field(default=True, metadata={"help": "native MI355X model (False: stock HF class)"})
+
+
+@dataclass
+class DataTrainingArguments:
+    dataset_name: Optional[str] = field(default=None)
+    dataset_config_name: Optional[str] = field(default=None)
+    train_file: Optional[str] = field(default=None, metadata={"help": "local text file"})
+    validation_file: Optional[str] = field(default=None)
+    max_train_samples: Optional[int] = field(default=None)
+    max_eval_samples: Optional[int] = field(default=None)
+    streaming: bool = field(default=False)
+    block_size: Optional[int] = field(default=None)
+    overwrite_cache: bool = field(default=False)
+    validation_split_percentage: Optional[int] = field(default=5)
+    preprocessing_num_workers: Optional[int] = field(default=None)
+    keep_linebreaks: bool = field(default=True)
+    synthetic_samples: int = field(default=100_000, metadata={"help": "size of the synthetic train set"})
+
+
+def _read_text(path: str, keep_linebreaks: bool):
+    with open(path, encoding="utf-8") as f:
+        lines = f.read().splitlines(keepends=keep_linebreaks)
+    return [ln for ln in lines if ln.strip()]
+
+
+def build_datasets(data_args, train_args, tokenizer, vocab_size, block_size):
+    if data_args.dataset_name and not train_args.synthetic_data:
+        try:
+            import datasets
+
+            raw = datasets.load_dataset(data_args.dataset_name, data_args.dataset_config_name)
+            col = "text" if "text" in raw["train"].column_names else raw["train"].column_names[0]
+            toks = [tokenizer(t)["input_ids"] for t in raw["train"][col]]
+            train = BlockDataset(toks, block_size, eos=tokenizer.eos_token_id)
+            n_val = max(1, len(train) * (data_args.validation_split_percentage or 5) // 100)
+            return train, torch.utils.data.Subset(train, range(n_val))
+        except Exception as e:  # offline: no hub datasets
+            logger.warning("dataset %s unavailable offline (%s); falling back to synthetic data",
+                           data_args.dataset_name, e)
+    if data_args.train_file and not train_args.synthetic_data:
+        toks = [tokenizer(t)["input_ids"] for t in _read_text(data_args.train_file, data_args.keep_linebreaks)]
+        train = BlockDataset(toks, block_size, eos=tokenizer.eos_token_id)
+        if data_args.validation_file:
+            vt = [tokenizer(t)["input_ids"] for t in _read_text(data_args.validation_file, data_args.keep_linebreaks)]
+            val = BlockDataset(vt, block_size, eos=tokenizer.eos_token_id)
+        else:
+            n_val = max(1, len(train) * (data_args.validation_split_percentage or 5) // 100)
+            val = torch.utils.data.Subset(train, range(n_val))
+        return train, val
+    n_train = data_args.max_train_samples or data_args.synthetic_samples
+    n_eval = data_args.max_eval_samples or max(8, n_train // 20)
+    return (SyntheticCLMDataset(n_train, block_size, vocab_size, seed=train_args.seed),
+            SyntheticCLMDataset(n_eval, block_size, vocab_size, seed=train_args.seed + 1))
+
+
+def main(argv=None):
+    parser = HfArgumentParser((ModelArguments, DataTrainingArguments, AsyncTrainingArguments))
+    if argv is None and len(sys.argv) == 2 and sys.argv[1].endswith(".json"):
+        model_args, data_args, training_args = parser.parse_json_file(json_file=os.path.abspath(sys.argv[1]))
+    else:
+        model_args, data_args, training_args = parser.parse_args_into_dataclasses(args=argv)
+
+    logging.basicConfig(format="%(asctime)s - %(levelname)s - %(name)s - %(message)s", datefmt="%m/%d/%Y %H:%M:%S",
+                        handlers=[logging.StreamHandler(sys.stdout)])
+    log_level = training_args.get_process_log_level()
+    logger.setLevel(log_level)
+    transformers.utils.logging.set_verbosity(log_level)
+    logger.warning(f"Process rank: {training_args.local_rank}, device: {training_args.device}, "
+                   f"n_gpu: {training_args.n_gpu}, distributed: {training_args.parallel_mode.value}, "
+                   f"bf16: {training_args.bf16}, lion: {training_args.lion}, async_grad: {training_args.async_grad}")
+
+    last_checkpoint = None
+    if os.path.isdir(training_args.output_dir) and training_args.do_train:
+        last_checkpoint = get_last_checkpoint(training_args.output_dir)
+        if last_checkpoint is not None and training_args.resume_from_checkpoint is None:
+            logger.info(f"Checkpoint detected, resuming training at {last_checkpoint}.")
+    set_seed(training_args.seed)
+
+    config = load_config(model_args.config_name or model_args.model_name_or_path or model_args.model_type or "gpt2",
+                         overrides=model_args.config_overrides)
+    tokenizer = load_tokenizer(model_args.tokenizer_name or model_args.model_name_or_path)
+    model = build_model(config, model_name_or_path=model_args.model_name_or_path, native=model_args.native_model,
+                        torch_dtype=model_args.torch_dtype)
+    n_params = sum({p.data_ptr(): p.numel() for p in model.parameters()}.values())
+    logger.info(f"model {config.model_type}: {n_params / 2 ** 20:.2f}M params")
+
+    max_pos = getattr(config, "n_positions", None) or getattr(config, "max_position_embeddings", 1024)
+    block_size = min(data_args.block_size or 1024, max_pos)
+    train_ds, eval_ds = build_datasets(data_args, training_args, tokenizer, config.vocab_size, block_size)
+
+    def preprocess_logits_for_metrics(logits, labels):
+        if isinstance(logits, tuple):
+            logits = logits[0]
+        return logits.argmax(dim=-1)
+
+    def compute_metrics(eval_preds):  # token accuracy (evaluate.load("accuracy") offline-free)
+        preds, labels = eval_preds
+        labels = labels[:, 1:].reshape(-1)
+        preds = preds[:, :-1].reshape(-1)
+        mask = labels != -100
+        return {"accuracy": float((preds[mask] == labels[mask]).mean())}
+
+    optimizers = (None, None)
+    if training_args.lion:
+        optimizer = build_lion(model, training_args)
+    else:
+        logger.warning("AdamW fallback uses weight_decay=0.1 regardless of --weight_decay (reference parity, D17)")
+        optimizer = torch.optim.AdamW(model.parameters(), lr=training_args.learning_rate, weight_decay=0.1)
+    if training_args.max_steps and training_args.max_steps > 0:
+        sched = transformers.get_cosine_schedule_with_warmup(optimizer, training_args.warmup_steps,
+                                                             training_args.max_steps)
+        optimizers = (optimizer, sched)
+    else:  # D18: a cosine schedule over max_steps=-1 is broken; let HF derive the length
+        optimizers = (optimizer, None)
+
+    trainer_class = AsyncTrainer if training_args.async_grad else Trainer
+    trainer = trainer_class(
+        model=model,
+        args=training_args,
+        train_dataset=train_ds if training_args.do_train else None,
+        eval_dataset=eval_ds if training_args.do_eval else None,
+        processing_class=None,
+        data_collator=transformers.default_data_collator,
+        compute_metrics=compute_metrics if training_args.do_eval else None,
+        preprocess_logits_for_metrics=preprocess_logits_for_metrics if training_args.do_eval else None,
+        optimizers=optimizers,
+        callbacks=[JsonlMetricsCallback(training_args.output_dir, block_size)],
+    )
+    warn_unsynced(training_args)
+
+    if training_args.do_train:
+        checkpoint = training_args.resume_from_checkpoint or last_checkpoint
+        train_result = trainer.train(resume_from_checkpoint=checkpoint)
+        trainer.save_model()
+        if hasattr(tokenizer, "save_pretrained") and trainer.is_world_process_zero():
+            tokenizer.save_pretrained(training_args.output_dir)
+        metrics = train_result.metrics
+        metrics["train_samples"] = len(train_ds)
+        trainer.log_metrics("train", metrics)
+        trainer.save_metrics("train", metrics)
+        trainer.save_state()
+
+    if training_args.do_eval:
+        metrics = trainer.evaluate()
+        metrics["eval_samples"] = len(eval_ds)
+        try:
+            metrics["perplexity"] = math.exp(metrics["eval_loss"])
+        except OverflowError:
+            metrics["perplexity"] = float("inf")
+        trainer.log_metrics("eval", metrics)
+        trainer.save_metrics("eval", metrics)
+    return trainer
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,151 @@
+#!/usr/bin/env python
+"""Llama-2 supervised fine-tuning with Distributed Lion -- drop-in for
+/root/reference/sft_llama2.py (same ScriptArguments + HF TrainingArguments,
+``--lion`` / ``--async_grad``), MI355X-native underneath:
+
+* one full bf16 replica per GPU (288 GB HBM; the reference's 4-bit NF4 base
+  model needs bitsandbytes, which is not part of this stack), native Llama
+  with the gfx950 attention / LM-head kernels;
+* LoRA (r=8, alpha=16, dropout 0.05, q_proj/v_proj, sft_llama2.py:44-51) via
+  the native adapter implementation (peft absent) -- ``--use_lora false``
+  trains all weights;
+* the optimizer is built over the trainable (adapter) parameters AFTER
+  injection (the reference builds it over the frozen base: no-op, D12);
+* packed "Question: ...\\n\\nAnswer: ..." samples (ConstantLengthDataset);
+  offline: the stack-exchange-paired data is replaced by a synthetic corpus of
+  the same format unless ``--dataset_name`` points at a local json/jsonl file;
+* saves the adapter (final_checkpoint/) and the merged model
+  (final_merged_checkpoint/, safetensors) like sft_llama2.py:183-199.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import sys
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import transformers
+from transformers import HfArgumentParser, TrainingArguments
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_lion_pytorch_amd.models.lora import (LoraConfig, merge_and_unload,  # noqa: E402
+                                                      print_trainable_parameters, save_adapter)
+from distributed_lion_pytorch_amd.models.registry import build_model, load_config  # noqa: E402
+from distributed_lion_pytorch_amd.trainer.async_trainer import build_lion, warn_unsynced  # noqa: E402
+from distributed_lion_pytorch_amd.trainer.sft import AsyncSFTTrainer, SFTTrainer  # noqa: E402
+from distributed_lion_pytorch_amd.utils.data import (ConstantLengthDataset, chars_token_ratio,  # noqa: E402
+                                                     load_tokenizer, prepare_sample_text, synthetic_qa)
+from distributed_lion_pytorch_amd.utils.metrics import JsonlMetricsCallback  # noqa: E402
+
+logger = logging.getLogger(__name__)
+
+
+@dataclass
+class ScriptArguments:
+    model_name: Optional[str] = field(default="meta-llama/Llama-2-7b-hf", metadata={"help": "size name or local dir"})
+    dataset_name: Optional[str] = field(default="lvwerra/stack-exchange-paired",
+                                        metadata={"help": "local json/jsonl file (else synthetic, offline)"})
+    subset: Optional[str] = field(default="data/finetune")
+    split: Optional[str] = field(default="train")
+    size_valid_set: Optional[int] = field(default=4000)
+    streaming: Optional[bool] = field(default=True)
+    shuffle_buffer: Optional[int] = field(default=5000)
+    seq_length: Optional[int] = field(default=1024)
+    num_workers: Optional[int] = field(default=4)
+    packing: Optional[bool] = field(default=True)
+    lora_alpha: Optional[float] = field(default=16)
+    lora_dropout: Optional[float] = field(default=0.05)
+    lora_r: Optional[int] = field(default=8)
+    use_lora: Optional[bool] = field(default=True, metadata={"help": "False: full fine-tune"})
+    lion: Optional[bool] = field(default=False, metadata={"help": "whether to use lion optimizer"})
+    async_grad: Optional[bool] = field(default=False, metadata={"help": "do not sync gradients between workers"})
+    lion_wire: Optional[str] = field(default="a2a")
+    synthetic_samples: Optional[int] = field(default=20000)
+    model_overrides: Optional[str] = field(default=None, metadata={"help": "config overrides, e.g. num_hidden_layers=4"})
+    torch_dtype: Optional[str] = field(default="bfloat16")
+
+
+def load_samples(script_args, seed):
+    path = script_args.dataset_name
+    if path and os.path.isfile(path):
+        with open(path) as f:
+            rows = [json.loads(line) for line in f] if path.endswith(".jsonl") else json.load(f)
+        return rows
+    return synthetic_qa(script_args.synthetic_samples, seed=seed)
+
+
+def create_datasets(tokenizer, script_args, seed):
+    rows = load_samples(script_args, seed)
+    n_valid = min(script_args.size_valid_set, max(1, len(rows) // 20))
+    train_rows, valid_rows = rows[n_valid:], rows[:n_valid]
+    ratio = chars_token_ratio(train_rows, tokenizer)
+    logger.info(f"The character to token ratio of the dataset is: {ratio:.2f}")
+    train = ConstantLengthDataset(tokenizer, train_rows, prepare_sample_text, seq_length=script_args.seq_length)
+    valid = ConstantLengthDataset(tokenizer, valid_rows, prepare_sample_text, seq_length=script_args.seq_length)
+    return train, valid
+
+
+def main(argv=None):
+    parser = HfArgumentParser((ScriptArguments, TrainingArguments))
+    script_args, training_args = parser.parse_args_into_dataclasses(args=argv)
+    logging.basicConfig(level=logging.INFO, handlers=[logging.StreamHandler(sys.stdout)])
+    if getattr(training_args, "group_by_length", False) and script_args.packing:
+        raise ValueError("Cannot use both packing and group by length")
+    # packing + gradient checkpointing is allowed here (the reference forbids
+    # checkpointing because of a peft/trl issue, sft_llama2.py:58-59)
+    training_args.lion = script_args.lion
+    training_args.async_grad = script_args.async_grad
+    training_args.lion_wire = script_args.lion_wire
+    transformers.set_seed(training_args.seed)
+
+    tokenizer = load_tokenizer(script_args.model_name)
+    config = load_config(script_args.model_name, overrides=script_args.model_overrides)
+    model = build_model(config, model_name_or_path=script_args.model_name, torch_dtype=script_args.torch_dtype)
+    if training_args.gradient_checkpointing:
+        model.gradient_checkpointing_enable()
+    peft_config = None
+    if script_args.use_lora:
+        peft_config = LoraConfig(r=script_args.lora_r, lora_alpha=int(script_args.lora_alpha),
+                                 lora_dropout=script_args.lora_dropout, target_modules=["q_proj", "v_proj"],
+                                 bias="none", task_type="CAUSAL_LM")
+        from distributed_lion_pytorch_amd.models.lora import inject_lora
+
+        inject_lora(model, peft_config)  # before the optimizer is built (D12)
+    print_trainable_parameters(model)
+
+    train_dataset, eval_dataset = create_datasets(tokenizer, script_args, training_args.seed)
+    params = [p for p in model.parameters() if p.requires_grad]
+    if script_args.lion:
+        optimizer = build_lion(model, training_args)
+    else:
+        optimizer = torch.optim.AdamW(params, lr=training_args.learning_rate, weight_decay=0.1)
+    sched = (transformers.get_cosine_schedule_with_warmup(optimizer, training_args.warmup_steps, training_args.max_steps)
+             if training_args.max_steps > 0 else None)
+
+    trainer_class = AsyncSFTTrainer if script_args.async_grad else SFTTrainer
+    trainer = trainer_class(model=model, train_dataset=train_dataset, eval_dataset=eval_dataset, peft_config=None,
+                            packing=script_args.packing, max_seq_length=script_args.seq_length, tokenizer=tokenizer,
+                            args=training_args, optimizers=(optimizer, sched),
+                            callbacks=[JsonlMetricsCallback(training_args.output_dir, script_args.seq_length)])
+    warn_unsynced(training_args)
+    trainer.train()
+    trainer.save_model(training_args.output_dir)
+
+    if trainer.is_world_process_zero():
+        out = os.path.join(training_args.output_dir, "final_checkpoint")
+        if script_args.use_lora:
+            save_adapter(trainer.model, out)
+            merged = merge_and_unload(trainer.accelerator.unwrap_model(trainer.model))
+            merged.save_pretrained(os.path.join(training_args.output_dir, "final_merged_checkpoint"),
+                                   safe_serialization=True)
+        else:
+            trainer.accelerator.unwrap_model(trainer.model).save_pretrained(out)
+    return trainer
+
+
+if __name__ == "__main__":
+    main()

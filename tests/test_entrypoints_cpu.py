@@ -1,0 +1,105 @@
+"""End-to-end entrypoints on CPU: run_clm (1 rank and 2 gloo ranks via torchrun,
+per-rank optimizer checkpoints, resume), sft_llama2, dpo_llama2, and the
+drop-in ``distributed_lion`` / ``async_trainer`` module names."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+COMMON = ["--synthetic_data", "--synthetic_samples", "64", "--block_size", "64", "--per_device_train_batch_size",
+          "4", "--gradient_accumulation_steps", "2", "--warmup_steps", "1", "--learning_rate", "1e-3",
+          "--report_to", "none", "--use_cpu", "--logging_steps", "1",
+          "--config_name", "gpt2-tiny", "--config_overrides", "resid_pdrop=0.0,embd_pdrop=0.0,attn_pdrop=0.0"]
+
+
+def test_dropin_module_names():
+    import async_trainer
+    import distributed_lion
+
+    assert distributed_lion.Lion.__module__.endswith("optim.lion")
+    for name in ("AsyncTrainer", "AsyncSFTTrainer", "AsyncDPOTrainer"):
+        assert hasattr(async_trainer, name)
+    for name in ("update_fn", "update_fn_distributed", "update_fn_distributed_stoc", "majority_vote",
+                 "flatten_and_pad", "restore_flattened_tensor"):
+        assert callable(getattr(distributed_lion, name))
+
+
+def test_run_clm_single_process(tmp_path):
+    import run_clm
+
+    out = str(tmp_path / "clm")
+    trainer = run_clm.main(COMMON + ["--max_steps", "3", "--lion", "--async_grad", "--do_train", "--do_eval",
+                                     "--output_dir", out])
+    assert os.path.isfile(os.path.join(out, "model.safetensors"))
+    recs = [json.loads(x) for x in open(os.path.join(out, "metrics.jsonl"))]
+    assert any("loss" in r for r in recs) and any("lion" in r for r in recs)
+    assert type(trainer.optimizer.optimizer if hasattr(trainer.optimizer, "optimizer") else trainer.optimizer
+                ).__name__ == "Lion"
+    ev = json.load(open(os.path.join(out, "eval_results.json")))
+    assert "perplexity" in ev and "eval_accuracy" in ev
+
+
+def _torchrun(args, port):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc_per_node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.join(ROOT, "run_clm.py")] + args
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r
+
+
+@pytest.mark.slow
+def test_run_clm_two_ranks_resume(tmp_path):
+    from dist_utils import free_port
+
+    out = str(tmp_path / "clm2")
+    args = COMMON + ["--lion", "--async_grad", "--do_train", "--output_dir", out, "--ddp_backend", "gloo",
+                     "--save_steps", "2"]
+    _torchrun(args + ["--max_steps", "4"], free_port())
+    ck = os.path.join(out, "checkpoint-2")
+    files = set(os.listdir(ck))
+    assert {"rank0-of-2-optimizer.pt", "rank1-of-2-optimizer.pt", "optimizer.pt"} <= files
+    m0 = torch.load(os.path.join(ck, "rank0-of-2-optimizer.pt"), weights_only=True)["state"]
+    m1 = torch.load(os.path.join(ck, "rank1-of-2-optimizer.pt"), weights_only=True)["state"]
+    assert any(not torch.equal(m0[k]["exp_avg"], m1[k]["exp_avg"]) for k in m0), "momenta must be per worker"
+    from safetensors.torch import load_file
+
+    final = load_file(os.path.join(out, "model.safetensors"))
+    # resume from checkpoint-2 in a fresh directory copy and finish the same 4 steps
+    out2 = str(tmp_path / "clm2b")
+    import shutil
+
+    shutil.copytree(ck, os.path.join(out2, "checkpoint-2"))
+    _torchrun(COMMON + ["--lion", "--async_grad", "--do_train", "--output_dir", out2, "--ddp_backend", "gloo",
+                        "--save_steps", "2", "--max_steps", "4"], free_port())
+    resumed = load_file(os.path.join(out2, "model.safetensors"))
+    for k in final:
+        assert torch.equal(final[k], resumed[k]), k
+
+
+def test_sft_and_dpo_entrypoints(tmp_path):
+    import dpo_llama2
+    import sft_llama2
+
+    sft_out = str(tmp_path / "sft")
+    sft_llama2.main(["--model_name", "llama-tiny", "--synthetic_samples", "100", "--seq_length", "64",
+                     "--output_dir", sft_out, "--max_steps", "2", "--per_device_train_batch_size", "2",
+                     "--learning_rate", "1e-3", "--lion", "--async_grad", "--report_to", "none", "--use_cpu",
+                     "--torch_dtype", "float32"])
+    assert os.path.isfile(os.path.join(sft_out, "final_checkpoint", "adapter_model.safetensors"))
+    merged = os.path.join(sft_out, "final_merged_checkpoint")
+    assert os.path.isfile(os.path.join(merged, "model.safetensors"))
+    dpo_out = str(tmp_path / "dpo")
+    tr = dpo_llama2.main(["--model_name_or_path", merged, "--synthetic_samples", "60", "--max_length", "1024",
+                          "--max_prompt_length", "256", "--output_dir", dpo_out, "--max_steps", "2",
+                          "--per_device_train_batch_size", "2", "--gradient_accumulation_steps", "1", "--lion",
+                          "--async_grad", "--use_cpu", "--torch_dtype", "float32", "--eval_steps", "0",
+                          "--warmup_steps", "1", "--logging_steps", "1"])
+    assert tr.state.global_step == 2
+    assert os.path.isfile(os.path.join(dpo_out, "final_checkpoint", "adapter_config.json"))
