@@ -138,8 +138,13 @@ class _FlashAttn(torch.autograd.Function):
 def causal_attention(qkv: torch.Tensor, dropout_p: float) -> torch.Tensor:
     """qkv: [B, T, 3, H, D] -> causal softmax attention output [B, T, H*D]."""
     B, T, _, H, D = qkv.shape
+    if qkv.is_cuda:
+        from .linear import autocast_inputs
+
+        (qkv,) = autocast_inputs(qkv)
     if _attn_ok(qkv, T, D):
-        return _FlashAttnPacked.apply(qkv, float(dropout_p), _new_seed()).view(B, T, H * D)
+        with torch.autocast("cuda", enabled=False):
+            return _FlashAttnPacked.apply(qkv, float(dropout_p), _new_seed()).view(B, T, H * D)
     q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)  # [B, H, T, D] views
     y = F.scaled_dot_product_attention(q, k, v, dropout_p=dropout_p, is_causal=True)
     return y.transpose(1, 2).reshape(B, T, H * D)
@@ -148,8 +153,13 @@ def causal_attention(qkv: torch.Tensor, dropout_p: float) -> torch.Tensor:
 def causal_attention_gqa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, dropout_p: float = 0.0) -> torch.Tensor:
     """q [B,T,H,D], k/v [B,T,Hkv,D] -> [B,T,H*D] (grouped-query causal attention)."""
     B, T, H, D = q.shape
+    if q.is_cuda:
+        from .linear import autocast_inputs
+
+        q, k, v = autocast_inputs(q, k, v)
     if _attn_ok(q, T, D):
-        return _FlashAttn.apply(q, k, v, float(dropout_p), _new_seed()).view(B, T, H * D)
+        with torch.autocast("cuda", enabled=False):
+            return _FlashAttn.apply(q, k, v, float(dropout_p), _new_seed()).view(B, T, H * D)
     rep = H // k.shape[2]
     qh, kh, vh = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
     if rep > 1:
@@ -270,6 +280,14 @@ def lm_head_cross_entropy(h: torch.Tensor, weight: torch.Tensor, labels: torch.T
     """Token cross-entropy of ``h @ weight.T`` against ``labels`` (-100 ignored):
     mean over valid tokens, or sum / ``normalizer`` (HF ``num_items_in_batch``)."""
     h2d = h.reshape(-1, h.shape[-1])
+    if h2d.is_cuda:
+        from .linear import autocast_inputs
+
+        h2d, weight = autocast_inputs(h2d, weight)
+        with torch.autocast("cuda", enabled=False):
+            return _LMHeadCE.apply(h2d, weight, labels.reshape(-1), normalizer)
+    if h2d.dtype != weight.dtype:
+        h2d = h2d.to(weight.dtype)
     return _LMHeadCE.apply(h2d, weight, labels.reshape(-1), normalizer)
 
 

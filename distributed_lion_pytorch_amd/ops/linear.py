@@ -76,13 +76,26 @@ class _LinearNK(torch.autograd.Function):
         return dx, dw, db
 
 
+def autocast_inputs(*ts):
+    """Under autocast (HF ``--bf16``/``--fp16``), cast the floating inputs of a
+    custom op to the autocast dtype with differentiable casts, so the op itself
+    runs with autocast disabled and sees one dtype (e.g. LayerNorm outputs are
+    fp32 under autocast while the GEMM computes in bf16)."""
+    if not torch.is_autocast_enabled("cuda"):
+        return ts
+    dt = torch.get_autocast_dtype("cuda")
+    return tuple(t.to(dt) if t is not None and t.is_floating_point() and t.dtype != dt else t for t in ts)
+
+
 def linear_kn(x: torch.Tensor, w: torch.Tensor, b=None) -> torch.Tensor:
     shp = x.shape[:-1] + (w.shape[1],)
     x2d = x.reshape(-1, x.shape[-1])
     if not x.is_cuda:
         y = torch.addmm(b, x2d, w) if b is not None else x2d @ w
     else:
-        y = _LinearKN.apply(x2d, w, b)
+        x2d, w, b = autocast_inputs(x2d, w, b)
+        with torch.autocast("cuda", enabled=False):
+            y = _LinearKN.apply(x2d, w, b)
     return y.view(shp)
 
 
@@ -92,5 +105,7 @@ def linear_nk(x: torch.Tensor, w: torch.Tensor, b=None) -> torch.Tensor:
     if not x.is_cuda:
         y = torch.nn.functional.linear(x2d, w, b)
     else:
-        y = _LinearNK.apply(x2d, w, b)
+        x2d, w, b = autocast_inputs(x2d, w, b)
+        with torch.autocast("cuda", enabled=False):
+            y = _LinearNK.apply(x2d, w, b)
     return y.view(shp)
