@@ -269,9 +269,79 @@ void attn_bwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, const 
   check_hip(dlion::launch_attn_bwd(a, static_cast<int>(q.size(3)), a.thresh16 > 0, cur_stream()), "attn_bwd");
 }
 
+// ------------------------------------------------- residual + dropout + norm
+void check_rows(const Tensor& t, const char* name, int64_t C) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous(), "dlion norm: ", name,
+              " must be a contiguous bf16 GPU tensor");
+  TORCH_CHECK(t.size(-1) == C, "dlion norm: ", name, " last dim mismatch");
+}
+
+std::pair<uint32_t, float> drop_params(double p) {
+  uint32_t th = static_cast<uint32_t>(std::llround(p * 65536.0));
+  if (th > 65535u) th = 65535u;
+  return {th, static_cast<float>(65536.0 / (65536.0 - th))};
+}
+
+// returns (xo, h, mean, rstd); y may be None (plain norm, xo == x)
+std::tuple<Tensor, Tensor, Tensor, Tensor> add_norm_fwd(const Tensor& x, const std::optional<Tensor>& y,
+                                                        const Tensor& gamma, const std::optional<Tensor>& beta,
+                                                        double eps, bool rms, double p, int64_t seed) {
+  const int64_t C = x.size(-1), rows = x.numel() / C;
+  check_rows(x, "x", C);
+  check_rows(gamma, "gamma", C);
+  TORCH_CHECK(C % 256 == 0, "dlion norm: hidden size must be a multiple of 256");
+  TORCH_CHECK(rms || beta.has_value(), "dlion norm: LayerNorm needs beta");
+  if (y.has_value()) check_rows(*y, "y", C);
+  const c10::DeviceGuard g(x.device());
+  Tensor xo = y.has_value() ? at::empty_like(x) : x;
+  Tensor h = at::empty_like(x);
+  auto mean = at::empty({rows}, x.options().dtype(at::kFloat));
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  const auto dp = drop_params(y.has_value() ? p : 0.0);
+  check_hip(dlion::launch_add_norm_fwd(x.data_ptr(), y.has_value() ? y->data_ptr() : nullptr, gamma.data_ptr(),
+                                       beta.has_value() ? beta->data_ptr() : nullptr, xo.data_ptr(), h.data_ptr(),
+                                       mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, static_cast<int>(C),
+                                       static_cast<float>(eps), rms, static_cast<uint32_t>(seed), dp.first, dp.second,
+                                       cur_stream()),
+            "add_norm_fwd");
+  return {xo, h, mean, rstd};
+}
+
+// returns (dx, dy, dgamma_part, dbeta_part); dy only when want_dy
+std::tuple<Tensor, Tensor, Tensor, Tensor> add_norm_bwd(const Tensor& dh, const std::optional<Tensor>& dxo_in,
+                                                        const Tensor& xo, const Tensor& gamma, const Tensor& mean,
+                                                        const Tensor& rstd, bool rms, double p, int64_t seed,
+                                                        bool want_dy, int64_t parts) {
+  const int64_t C = xo.size(-1), rows = xo.numel() / C;
+  check_rows(dh, "dh", C);
+  check_rows(xo, "xo", C);
+  check_rows(gamma, "gamma", C);
+  if (dxo_in.has_value()) check_rows(*dxo_in, "dxo_in", C);
+  const c10::DeviceGuard g(xo.device());
+  auto dx = at::empty_like(xo);
+  Tensor dy = want_dy ? at::empty_like(xo) : Tensor();
+  auto gpart = at::empty({parts * 4, C}, xo.options().dtype(at::kFloat));
+  Tensor bpart = rms ? Tensor() : at::empty({parts * 4, C}, xo.options().dtype(at::kFloat));
+  const auto dp = drop_params(want_dy ? p : 0.0);
+  check_hip(dlion::launch_add_norm_bwd(dh.data_ptr(), dxo_in.has_value() ? dxo_in->data_ptr() : nullptr, xo.data_ptr(),
+                                       gamma.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(),
+                                       want_dy ? dy.data_ptr() : nullptr, gpart.data_ptr<float>(),
+                                       rms ? nullptr : bpart.data_ptr<float>(), static_cast<int>(parts), rows,
+                                       static_cast<int>(C), rms, static_cast<uint32_t>(seed), dp.first, dp.second,
+                                       cur_stream()),
+            "add_norm_bwd");
+  return {dx, dy, gpart, bpart};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dlion, m) {
+  m.def(
+      "add_norm_fwd(Tensor x, Tensor? y, Tensor gamma, Tensor? beta, float eps, bool rms, float p, int seed)"
+      " -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def(
+      "add_norm_bwd(Tensor dh, Tensor? dxo_in, Tensor xo, Tensor gamma, Tensor mean, Tensor rstd, bool rms,"
+      " float p, int seed, bool want_dy, int parts) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("transpose_btxd(Tensor x) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float p, int seed) -> (Tensor, Tensor)");
   m.def(
@@ -300,4 +370,6 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("transpose_btxd", &transpose_btxd);
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);
+  m.impl("add_norm_fwd", &add_norm_fwd);
+  m.impl("add_norm_bwd", &add_norm_bwd);
 }

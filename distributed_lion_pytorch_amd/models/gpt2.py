@@ -126,12 +126,20 @@ class GPT2Model(nn.Module):
         x = self.wte(input_ids) + self.wpe(pos)[None]
         if self.training and self.embd_pdrop > 0:
             x = F.dropout(x, self.embd_pdrop, True)
-        for blk in self.h:
-            if self.gradient_checkpointing and self.training:
+        if self.gradient_checkpointing and self.training:
+            for blk in self.h:
                 x = torch.utils.checkpoint.checkpoint(blk, x, use_reentrant=False)
-            else:
-                x = blk(x)
-        return fused.layer_norm(x, self.ln_f)
+            return fused.layer_norm(x, self.ln_f)
+        # fused path: every "dropout(branch) + residual add + next LayerNorm"
+        # boundary is one kernel (ops/fused.dropout_add_norm -> norm_kernels.hip)
+        first = self.h[0].ln_1
+        h = fused.norm(x, first.weight, first.bias, first.eps)
+        for i, blk in enumerate(self.h):
+            p = blk.resid_pdrop if self.training else 0.0
+            x, h = fused.dropout_add_norm(blk.attn(h), x, blk.ln_2.weight, blk.ln_2.bias, blk.ln_2.eps, p)
+            nxt = self.h[i + 1].ln_1 if i + 1 < len(self.h) else self.ln_f
+            x, h = fused.dropout_add_norm(blk.mlp(h), x, nxt.weight, nxt.bias, nxt.eps, p)
+        return h
 
 
 class GPT2LMHeadModel(PreTrainedModel):

@@ -159,12 +159,19 @@ class LlamaModel(nn.Module):
         T = input_ids.shape[1]
         x = self.embed_tokens(input_ids)
         cos, sin = self.rotary.tables(T, x.device, x.dtype)
-        for layer in self.layers:
-            if self.gradient_checkpointing and self.training:
+        if self.gradient_checkpointing and self.training:
+            for layer in self.layers:
                 x = torch.utils.checkpoint.checkpoint(layer, x, cos, sin, use_reentrant=False)
-            else:
-                x = layer(x, cos, sin)
-        return self.norm(x)
+            return self.norm(x)
+        # fused path: each "residual add + next RMSNorm" is one kernel
+        first = self.layers[0].input_layernorm
+        h = fused.norm(x, first.weight, None, first.eps, rms=True)
+        for i, layer in enumerate(self.layers):
+            pn = layer.post_attention_layernorm
+            x, h = fused.dropout_add_norm(layer.self_attn(h, cos, sin), x, pn.weight, None, pn.eps, 0.0, rms=True)
+            nxt = self.layers[i + 1].input_layernorm if i + 1 < len(self.layers) else self.norm
+            x, h = fused.dropout_add_norm(layer.mlp(h), x, nxt.weight, None, nxt.eps, 0.0, rms=True)
+        return h
 
 
 class LlamaForCausalLM(PreTrainedModel):

@@ -75,6 +75,92 @@ def dropout_add(y: torch.Tensor, residual: torch.Tensor, p: float) -> torch.Tens
     return residual + y
 
 
+# --------------------------------------- fused residual + dropout + LN / RMSNorm
+def _norm_parts(rows: int) -> int:
+    return max(1, min(256, rows // 32))
+
+
+class _AddNorm(torch.autograd.Function):
+    """(xo, h) = (x + dropout(y), Norm(xo)) in one gfx950 kernel each way."""
+
+    @staticmethod
+    def forward(ctx, y, x, gamma, beta, eps, rms, p, seed):
+        xo, h, mean, rstd = hip.ops().add_norm_fwd(x, y, gamma, beta, eps, rms, p, seed)
+        ctx.save_for_backward(xo, gamma, mean, rstd)
+        ctx.rms, ctx.p, ctx.seed, ctx.has_beta = rms, p, seed, beta is not None
+        return xo, h
+
+    @staticmethod
+    def backward(ctx, dxo, dh):
+        xo, gamma, mean, rstd = ctx.saved_tensors
+        rows = xo.numel() // xo.shape[-1]
+        if dh is None:
+            dh = torch.zeros_like(xo)
+        dx, dy, gp, bp = hip.ops().add_norm_bwd(dh.contiguous(), None if dxo is None else dxo.contiguous(), xo, gamma,
+                                                mean, rstd, ctx.rms, ctx.p, ctx.seed, True, _norm_parts(rows))
+        dgamma = gp.sum(0).to(gamma.dtype)
+        dbeta = bp.sum(0).to(gamma.dtype) if ctx.has_beta else None
+        return dy, dx, dgamma, dbeta, None, None, None, None
+
+
+class _Norm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps, rms):
+        _, h, mean, rstd = hip.ops().add_norm_fwd(x, None, gamma, beta, eps, rms, 0.0, 0)
+        ctx.save_for_backward(x, gamma, mean, rstd)
+        ctx.rms, ctx.has_beta = rms, beta is not None
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, gamma, mean, rstd = ctx.saved_tensors
+        rows = x.numel() // x.shape[-1]
+        dx, _, gp, bp = hip.ops().add_norm_bwd(dh.contiguous(), None, x, gamma, mean, rstd, ctx.rms, 0.0, 0, False,
+                                               _norm_parts(rows))
+        return dx, gp.sum(0).to(gamma.dtype), (bp.sum(0).to(gamma.dtype) if ctx.has_beta else None), None, None
+
+
+def _norm_ok(x: torch.Tensor, gamma: torch.Tensor) -> bool:
+    return (x.dtype == torch.bfloat16 and gamma.dtype == torch.bfloat16 and x.shape[-1] % 256 == 0
+            and x.shape[-1] <= 5120 and _use_hip(x))
+
+
+def dropout_add_norm(y: torch.Tensor, x: torch.Tensor, gamma: torch.Tensor, beta, eps: float, p: float,
+                     rms: bool = False):
+    """Returns (x + dropout(y), Norm(x + dropout(y))) -- the residual stream and
+    the next sub-block's normalised input."""
+    if y.is_cuda:
+        from .linear import autocast_inputs
+
+        y, x = autocast_inputs(y, x)
+    if _norm_ok(x, gamma) and y.dtype == x.dtype:
+        with torch.autocast("cuda", enabled=False):
+            return _AddNorm.apply(y.contiguous(), x.contiguous(), gamma, beta, float(eps), bool(rms), float(p),
+                                  _new_seed())
+    xo = dropout_add(y, x, p)
+    if rms:
+        return xo, rms_norm(xo, gamma, eps)
+    return xo, F.layer_norm(xo, (x.shape[-1],), gamma, beta, eps)
+
+
+def norm(x: torch.Tensor, gamma: torch.Tensor, beta, eps: float, rms: bool = False) -> torch.Tensor:
+    if _norm_ok(x, gamma):
+        with torch.autocast("cuda", enabled=False):
+            return _Norm.apply(x.contiguous(), gamma, beta, float(eps), bool(rms))
+    if rms:
+        return rms_norm(x, gamma, eps)
+    return F.layer_norm(x, (x.shape[-1],), gamma, beta, eps)
+
+
+def norm_dropout_keep(rows: int, C: int, p: float, seed: int, device=None) -> torch.Tensor:
+    """bool keep-mask [rows, C] exactly as norm_kernels.hip draws it."""
+    th = min(65535, int(round(p * 65536)))
+    idx = torch.arange(rows * C, device=device, dtype=torch.int64)
+    x = (seed & _M32) ^ (((idx >> 1) * 0x9E3779B1) & _M32) ^ ((idx >> 33) & _M32)
+    u16 = (_lowbias32(x) >> ((idx & 1) * 16)) & 0xFFFF
+    return (u16 >= th).view(rows, C)
+
+
 # --------------------------------------------------------------- bias + GELU
 def linear_gelu(x2d: torch.Tensor, w_in_out: torch.Tensor, bias: torch.Tensor, exact: bool = False):
     """gelu(x @ W + b) with HF Conv1D's [in, out] weight layout."""

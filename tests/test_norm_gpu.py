@@ -1,0 +1,71 @@
+"""Fused residual + dropout + LayerNorm/RMSNorm kernels vs an fp32 PyTorch
+reference using the identical stateless dropout mask."""
+import pytest
+import torch
+
+from distributed_lion_pytorch_amd.ops import fused, hip
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(y, x, g, b, eps, p, seed, rms):
+    rows, C = x.shape
+    if p > 0:
+        th = min(65535, int(round(p * 65536)))
+        keep = fused.norm_dropout_keep(rows, C, p, seed, x.device)
+        y = y * keep * (65536.0 / (65536.0 - th))
+    xo = x + y
+    if rms:
+        h = xo * torch.rsqrt(xo.pow(2).mean(-1, keepdim=True) + eps) * g
+    else:
+        h = torch.nn.functional.layer_norm(xo, (C,), g, b, eps)
+    return xo, h
+
+
+def _rel(a, b):
+    return (a.float() - b.float()).abs().max().item() / (b.float().abs().max().item() + 1e-6)
+
+
+@pytest.mark.parametrize("C,rms", [(768, False), (1024, True), (4096, True), (1280, False)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_add_norm_fwd_bwd(C, rms, p, cuda):
+    hip.require()
+    torch.manual_seed(0)
+    rows = 333
+    x = torch.randn(rows, C, device=cuda).bfloat16()
+    y = torch.randn(rows, C, device=cuda).bfloat16()
+    g = (1 + 0.1 * torch.randn(C, device=cuda)).bfloat16()
+    b = None if rms else (0.1 * torch.randn(C, device=cuda)).bfloat16()
+    seed = 4242
+    ys, xs, gs = y.clone().requires_grad_(), x.clone().requires_grad_(), g.clone().requires_grad_()
+    bs = None if b is None else b.clone().requires_grad_()
+    xo, h = fused._AddNorm.apply(ys, xs, gs, bs, 1e-5, rms, p, seed)
+    yr, xr, gr = (t.float().requires_grad_() for t in (y, x, g))
+    br = None if b is None else b.float().requires_grad_()
+    xo_r, h_r = _ref(yr, xr, gr, br, 1e-5, p, seed, rms)
+    assert _rel(xo, xo_r) < 1e-2 and _rel(h, h_r) < 2e-2
+    dxo = torch.randn_like(x)
+    dh = torch.randn_like(x)
+    torch.autograd.backward([xo, h], [dxo, dh])
+    torch.autograd.backward([xo_r, h_r], [dxo.float(), dh.float()])
+    assert _rel(ys.grad, yr.grad) < 2e-2
+    assert _rel(xs.grad, xr.grad) < 2e-2
+    assert _rel(gs.grad, gr.grad) < 2e-2
+    if b is not None:
+        assert _rel(bs.grad, br.grad) < 2e-2
+
+
+def test_plain_norm(cuda):
+    hip.require()
+    torch.manual_seed(1)
+    x = torch.randn(100, 768, device=cuda).bfloat16().requires_grad_()
+    g = torch.ones(768, device=cuda).bfloat16().requires_grad_()
+    b = torch.zeros(768, device=cuda).bfloat16().requires_grad_()
+    h = fused._Norm.apply(x, g, b, 1e-5, False)
+    xr = x.detach().float().requires_grad_()
+    hr = torch.nn.functional.layer_norm(xr, (768,), None, None, 1e-5)
+    assert _rel(h, hr) < 2e-2
+    dh = torch.randn_like(h)
+    h.backward(dh)
+    hr.backward(dh.float())
+    assert _rel(x.grad, xr.grad) < 2e-2
