@@ -282,23 +282,26 @@ std::pair<uint32_t, float> drop_params(double p) {
   return {th, static_cast<float>(65536.0 / (65536.0 - th))};
 }
 
-// returns (xo, h, mean, rstd); y may be None (plain norm, xo == x)
+// returns (xo, h, mean, rstd); y may be None (plain norm, xo == x); bias is added to y
 std::tuple<Tensor, Tensor, Tensor, Tensor> add_norm_fwd(const Tensor& x, const std::optional<Tensor>& y,
-                                                        const Tensor& gamma, const std::optional<Tensor>& beta,
-                                                        double eps, bool rms, double p, int64_t seed) {
+                                                        const std::optional<Tensor>& bias, const Tensor& gamma,
+                                                        const std::optional<Tensor>& beta, double eps, bool rms,
+                                                        double p, int64_t seed) {
   const int64_t C = x.size(-1), rows = x.numel() / C;
   check_rows(x, "x", C);
   check_rows(gamma, "gamma", C);
-  TORCH_CHECK(C % 256 == 0, "dlion norm: hidden size must be a multiple of 256");
+  TORCH_CHECK(C % 256 == 0 && C <= 5120, "dlion norm: hidden size must be a multiple of 256, <= 5120");
   TORCH_CHECK(rms || beta.has_value(), "dlion norm: LayerNorm needs beta");
   if (y.has_value()) check_rows(*y, "y", C);
+  if (bias.has_value()) check_rows(*bias, "bias", C);
   const c10::DeviceGuard g(x.device());
   Tensor xo = y.has_value() ? at::empty_like(x) : x;
   Tensor h = at::empty_like(x);
   auto mean = at::empty({rows}, x.options().dtype(at::kFloat));
   auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
   const auto dp = drop_params(y.has_value() ? p : 0.0);
-  check_hip(dlion::launch_add_norm_fwd(x.data_ptr(), y.has_value() ? y->data_ptr() : nullptr, gamma.data_ptr(),
+  check_hip(dlion::launch_add_norm_fwd(x.data_ptr(), y.has_value() ? y->data_ptr() : nullptr,
+                                       bias.has_value() ? bias->data_ptr() : nullptr, gamma.data_ptr(),
                                        beta.has_value() ? beta->data_ptr() : nullptr, xo.data_ptr(), h.data_ptr(),
                                        mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, static_cast<int>(C),
                                        static_cast<float>(eps), rms, static_cast<uint32_t>(seed), dp.first, dp.second,
@@ -307,11 +310,11 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> add_norm_fwd(const Tensor& x, const s
   return {xo, h, mean, rstd};
 }
 
-// returns (dx, dy, dgamma_part, dbeta_part); dy only when want_dy
-std::tuple<Tensor, Tensor, Tensor, Tensor> add_norm_bwd(const Tensor& dh, const std::optional<Tensor>& dxo_in,
-                                                        const Tensor& xo, const Tensor& gamma, const Tensor& mean,
-                                                        const Tensor& rstd, bool rms, double p, int64_t seed,
-                                                        bool want_dy, int64_t parts) {
+// returns (dx, dy, part[parts, 3, C] =dgamma / dbeta / dbias partials); dy only when want_dy
+std::tuple<Tensor, Tensor, Tensor> add_norm_bwd(const Tensor& dh, const std::optional<Tensor>& dxo_in,
+                                                const Tensor& xo, const Tensor& gamma, const Tensor& mean,
+                                                const Tensor& rstd, bool rms, double p, int64_t seed, bool want_dy,
+                                                int64_t parts) {
   const int64_t C = xo.size(-1), rows = xo.numel() / C;
   check_rows(dh, "dh", C);
   check_rows(xo, "xo", C);
@@ -320,28 +323,75 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> add_norm_bwd(const Tensor& dh, const 
   const c10::DeviceGuard g(xo.device());
   auto dx = at::empty_like(xo);
   Tensor dy = want_dy ? at::empty_like(xo) : Tensor();
-  auto gpart = at::empty({parts * 4, C}, xo.options().dtype(at::kFloat));
-  Tensor bpart = rms ? Tensor() : at::empty({parts * 4, C}, xo.options().dtype(at::kFloat));
+  TORCH_CHECK(parts >= 1 && parts <= 65535, "add_norm_bwd: parts out of range");
+  auto part = at::empty({parts, 3, C}, xo.options().dtype(at::kFloat));
   const auto dp = drop_params(want_dy ? p : 0.0);
   check_hip(dlion::launch_add_norm_bwd(dh.data_ptr(), dxo_in.has_value() ? dxo_in->data_ptr() : nullptr, xo.data_ptr(),
                                        gamma.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(),
-                                       want_dy ? dy.data_ptr() : nullptr, gpart.data_ptr<float>(),
-                                       rms ? nullptr : bpart.data_ptr<float>(), static_cast<int>(parts), rows,
-                                       static_cast<int>(C), rms, static_cast<uint32_t>(seed), dp.first, dp.second,
-                                       cur_stream()),
+                                       want_dy ? dy.data_ptr() : nullptr, part.data_ptr<float>(),
+                                       static_cast<int>(parts), rows, static_cast<int>(C), rms,
+                                       static_cast<uint32_t>(seed), dp.first, dp.second, cur_stream()),
             "add_norm_bwd");
-  return {dx, dy, gpart, bpart};
+  return {dx, dy, part};
+}
+
+// ---------------------------------------------------------------- bias + GELU
+Tensor bias_gelu_fwd(const Tensor& z, const Tensor& b, bool exact) {
+  const int64_t N = z.size(-1), rows = z.numel() / N;
+  check_rows(z, "z", N);
+  check_rows(b, "b", N);
+  TORCH_CHECK(N % 8 == 0 && N <= 16384, "dlion gelu: N must be a multiple of 8 and <= 16384");
+  const c10::DeviceGuard g(z.device());
+  auto h = at::empty_like(z);
+  check_hip(dlion::launch_bias_gelu_fwd(z.data_ptr(), b.data_ptr(), h.data_ptr(), rows, static_cast<int>(N), exact,
+                                        cur_stream()),
+            "bias_gelu_fwd");
+  return h;
+}
+
+std::tuple<Tensor, Tensor> bias_gelu_bwd(const Tensor& dh, const Tensor& z, const Tensor& b, bool exact,
+                                         int64_t parts) {
+  const int64_t N = z.size(-1), rows = z.numel() / N;
+  check_rows(dh, "dh", N);
+  check_rows(z, "z", N);
+  check_rows(b, "b", N);
+  const c10::DeviceGuard g(z.device());
+  auto dz = at::empty_like(z);
+  auto part = at::empty({parts, N}, z.options().dtype(at::kFloat));
+  check_hip(dlion::launch_bias_gelu_bwd(dh.data_ptr(), z.data_ptr(), b.data_ptr(), dz.data_ptr(),
+                                        part.data_ptr<float>(), static_cast<int>(parts), rows, static_cast<int>(N),
+                                        exact, cur_stream()),
+            "bias_gelu_bwd");
+  return {dz, part};
+}
+
+// sum of fp32 partials over dim 0 -> bf16 (split-K weight grads, bias / norm param grads)
+Tensor sum_partials(const Tensor& part) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous(),
+              "dlion: partials must be contiguous fp32 on the GPU");
+  const int64_t S = part.size(0), n = part.numel() / S;
+  TORCH_CHECK(n % 4 == 0, "dlion: partial row length must be a multiple of 4");
+  const c10::DeviceGuard g(part.device());
+  auto sizes = part.sizes().vec();
+  sizes.erase(sizes.begin());
+  auto out = at::empty(sizes, part.options().dtype(at::kBFloat16));
+  check_hip(dlion::launch_sum_partials(part.data_ptr<float>(), static_cast<int>(S), n, out.data_ptr(), cur_stream()),
+            "sum_partials");
+  return out;
 }
 
 }  // namespace
 
 TORCH_LIBRARY(dlion, m) {
   m.def(
-      "add_norm_fwd(Tensor x, Tensor? y, Tensor gamma, Tensor? beta, float eps, bool rms, float p, int seed)"
-      " -> (Tensor, Tensor, Tensor, Tensor)");
+      "add_norm_fwd(Tensor x, Tensor? y, Tensor? bias, Tensor gamma, Tensor? beta, float eps, bool rms, float p,"
+      " int seed) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
       "add_norm_bwd(Tensor dh, Tensor? dxo_in, Tensor xo, Tensor gamma, Tensor mean, Tensor rstd, bool rms,"
-      " float p, int seed, bool want_dy, int parts) -> (Tensor, Tensor, Tensor, Tensor)");
+      " float p, int seed, bool want_dy, int parts) -> (Tensor, Tensor, Tensor)");
+  m.def("bias_gelu_fwd(Tensor z, Tensor b, bool exact) -> Tensor");
+  m.def("bias_gelu_bwd(Tensor dh, Tensor z, Tensor b, bool exact, int parts) -> (Tensor, Tensor)");
+  m.def("sum_partials(Tensor part) -> Tensor");
   m.def("transpose_btxd(Tensor x) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float p, int seed) -> (Tensor, Tensor)");
   m.def(
@@ -372,4 +422,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("attn_bwd", &attn_bwd);
   m.impl("add_norm_fwd", &add_norm_fwd);
   m.impl("add_norm_bwd", &add_norm_bwd);
+  m.impl("bias_gelu_fwd", &bias_gelu_fwd);
+  m.impl("bias_gelu_bwd", &bias_gelu_bwd);
+  m.impl("sum_partials", &sum_partials);
 }

@@ -27,13 +27,21 @@ hipError_t launch_transpose_btxd(const void* in, int64_t sb, int64_t st, int64_t
                                  int D, int ldt, hipStream_t stream);
 
 // ---- fused residual + dropout + LayerNorm/RMSNorm (norm_kernels.hip)
-hipError_t launch_add_norm_fwd(const void* x, const void* y, const void* gamma, const void* beta, void* xo, void* h,
-                               float* mean, float* rstd, int64_t rows, int C, float eps, bool rms, uint32_t seed,
-                               uint32_t thresh16, float inv_keep, hipStream_t st);
+// backward: `parts` blocks of kNormBwdWaves waves; part is [parts][3][C]
+constexpr int kNormBwdWaves = 4;
+hipError_t launch_add_norm_fwd(const void* x, const void* y, const void* bias, const void* gamma, const void* beta,
+                               void* xo, void* h, float* mean, float* rstd, int64_t rows, int C, float eps, bool rms,
+                               uint32_t seed, uint32_t thresh16, float inv_keep, hipStream_t st);
 hipError_t launch_add_norm_bwd(const void* dh, const void* dxo_in, const void* xo, const void* gamma, const float* mean,
-                               const float* rstd, void* dx, void* dy, float* dgamma_part, float* dbeta_part,
-                               int parts, int64_t rows, int C, bool rms, uint32_t seed, uint32_t thresh16,
-                               float inv_keep, hipStream_t st);
+                               const float* rstd, void* dx, void* dy, float* part, int parts, int64_t rows, int C,
+                               bool rms, uint32_t seed, uint32_t thresh16, float inv_keep, hipStream_t st);
+
+// ---- bias + GELU, partial sums (elementwise_kernels.hip)
+hipError_t launch_bias_gelu_fwd(const void* z, const void* b, void* h, int64_t rows, int N, bool exact,
+                                hipStream_t st);
+hipError_t launch_bias_gelu_bwd(const void* dh, const void* z, const void* b, void* dz, float* dbpart, int parts,
+                                int64_t rows, int N, bool exact, hipStream_t st);
+hipError_t launch_sum_partials(const float* part, int S, int64_t n, void* out, hipStream_t st);
 
 // ---- LM head cross-entropy (xent_kernels.hip)
 hipError_t launch_softmax_xent(int dt, void* logits, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,

@@ -71,11 +71,13 @@ class Attention(nn.Module):
         self.c_proj = Conv1D(cfg.n_embd, cfg.n_embd)
         self.attn_pdrop = cfg.attn_pdrop
 
-    def forward(self, x):
+    def forward(self, x, proj_bias: bool = True):
+        """proj_bias=False leaves c_proj's bias to the caller's fused
+        residual+dropout+LayerNorm kernel (its gradient comes out of it too)."""
         B, T, _ = x.shape
         qkv = self.c_attn(x).view(B, T, 3, self.n_head, self.head_dim)
         y = fused.causal_attention(qkv, self.attn_pdrop if self.training else 0.0)  # [B, T, C]
-        return self.c_proj(y)
+        return self.c_proj(y) if proj_bias else linear_kn(y, self.c_proj.weight, None)
 
 
 class MLP(nn.Module):
@@ -88,10 +90,11 @@ class MLP(nn.Module):
             raise ValueError(f"unsupported activation {cfg.activation_function}")
         self.exact_gelu = cfg.activation_function == "gelu"
 
-    def forward(self, x):
+    def forward(self, x, proj_bias: bool = True):
         shp = x.shape[:-1]
         h = fused.linear_gelu(x.reshape(-1, x.shape[-1]), self.c_fc.weight, self.c_fc.bias, exact=self.exact_gelu)
-        return self.c_proj(h.view(*shp, -1))
+        h = h.view(*shp, -1)
+        return self.c_proj(h) if proj_bias else linear_kn(h, self.c_proj.weight, None)
 
 
 class Block(nn.Module):
@@ -136,9 +139,11 @@ class GPT2Model(nn.Module):
         h = fused.norm(x, first.weight, first.bias, first.eps)
         for i, blk in enumerate(self.h):
             p = blk.resid_pdrop if self.training else 0.0
-            x, h = fused.dropout_add_norm(blk.attn(h), x, blk.ln_2.weight, blk.ln_2.bias, blk.ln_2.eps, p)
+            x, h = fused.dropout_add_norm(blk.attn(h, proj_bias=False), x, blk.ln_2.weight, blk.ln_2.bias,
+                                          blk.ln_2.eps, p, bias=blk.attn.c_proj.bias)
             nxt = self.h[i + 1].ln_1 if i + 1 < len(self.h) else self.ln_f
-            x, h = fused.dropout_add_norm(blk.mlp(h), x, nxt.weight, nxt.bias, nxt.eps, p)
+            x, h = fused.dropout_add_norm(blk.mlp(h, proj_bias=False), x, nxt.weight, nxt.bias, nxt.eps, p,
+                                          bias=blk.mlp.c_proj.bias)
         return h
 
 

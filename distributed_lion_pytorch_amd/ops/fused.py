@@ -76,37 +76,55 @@ def dropout_add(y: torch.Tensor, residual: torch.Tensor, p: float) -> torch.Tens
 
 
 # --------------------------------------- fused residual + dropout + LN / RMSNorm
+_NORM_BWD_WAVES = 4  # csrc/kernels.h kNormBwdWaves
+_NORM_PARTS_CAP = int(os.environ.get("DLION_NORM_PARTS", "512"))
+
+
 def _norm_parts(rows: int) -> int:
-    return max(1, min(256, rows // 32))
+    # blocks of 4 waves, one fp32 partial row triple per block: enough waves to
+    # cover the CUs a few times over while the partial stack stays a small
+    # fraction of the row traffic (tools/bench_norm.py: 512 best at 20480x768)
+    return max(1, min(_NORM_PARTS_CAP, rows // (4 * _NORM_BWD_WAVES)))
+
+
+def _sum_rows(part: torch.Tensor) -> torch.Tensor:
+    """[P, ...] fp32 partials -> bf16 sums in one kernel (row-parallel for tall stacks)."""
+    return hip.ops().sum_partials(part)
 
 
 class _AddNorm(torch.autograd.Function):
-    """(xo, h) = (x + dropout(y), Norm(xo)) in one gfx950 kernel each way."""
+    """(xo, h) = (x + dropout(y + bias), Norm(xo)) in one gfx950 kernel each way;
+    gamma / beta / bias gradients come out of the backward kernel as partials."""
 
     @staticmethod
-    def forward(ctx, y, x, gamma, beta, eps, rms, p, seed):
-        xo, h, mean, rstd = hip.ops().add_norm_fwd(x, y, gamma, beta, eps, rms, p, seed)
+    def forward(ctx, y, x, bias, gamma, beta, eps, rms, p, seed):
+        xo, h, mean, rstd = hip.ops().add_norm_fwd(x, y, bias, gamma, beta, eps, rms, p, seed)
         ctx.save_for_backward(xo, gamma, mean, rstd)
-        ctx.rms, ctx.p, ctx.seed, ctx.has_beta = rms, p, seed, beta is not None
+        ctx.rms, ctx.p, ctx.seed = rms, p, seed
+        ctx.has_beta, ctx.has_bias = beta is not None, bias is not None
         return xo, h
 
     @staticmethod
     def backward(ctx, dxo, dh):
         xo, gamma, mean, rstd = ctx.saved_tensors
-        rows = xo.numel() // xo.shape[-1]
+        C = xo.shape[-1]
+        rows = xo.numel() // C
         if dh is None:
             dh = torch.zeros_like(xo)
-        dx, dy, gp, bp = hip.ops().add_norm_bwd(dh.contiguous(), None if dxo is None else dxo.contiguous(), xo, gamma,
-                                                mean, rstd, ctx.rms, ctx.p, ctx.seed, True, _norm_parts(rows))
-        dgamma = gp.sum(0).to(gamma.dtype)
-        dbeta = bp.sum(0).to(gamma.dtype) if ctx.has_beta else None
-        return dy, dx, dgamma, dbeta, None, None, None, None
+        parts = _norm_parts(rows)
+        dx, dy, part = hip.ops().add_norm_bwd(dh.contiguous(), None if dxo is None else dxo.contiguous(), xo, gamma,
+                                              mean, rstd, ctx.rms, ctx.p, ctx.seed, True, parts)
+        sums = _sum_rows(part.view(-1, 3 * C))
+        dgamma = sums[:C]
+        dbeta = sums[C:2 * C] if ctx.has_beta else None
+        dbias = sums[2 * C:] if ctx.has_bias else None
+        return dy, dx, dbias, dgamma, dbeta, None, None, None, None
 
 
 class _Norm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, eps, rms):
-        _, h, mean, rstd = hip.ops().add_norm_fwd(x, None, gamma, beta, eps, rms, 0.0, 0)
+        _, h, mean, rstd = hip.ops().add_norm_fwd(x, None, None, gamma, beta, eps, rms, 0.0, 0)
         ctx.save_for_backward(x, gamma, mean, rstd)
         ctx.rms, ctx.has_beta = rms, beta is not None
         return h
@@ -114,33 +132,67 @@ class _Norm(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh):
         x, gamma, mean, rstd = ctx.saved_tensors
-        rows = x.numel() // x.shape[-1]
-        dx, _, gp, bp = hip.ops().add_norm_bwd(dh.contiguous(), None, x, gamma, mean, rstd, ctx.rms, 0.0, 0, False,
-                                               _norm_parts(rows))
-        return dx, gp.sum(0).to(gamma.dtype), (bp.sum(0).to(gamma.dtype) if ctx.has_beta else None), None, None
+        C = x.shape[-1]
+        parts = _norm_parts(x.numel() // C)
+        dx, _, part = hip.ops().add_norm_bwd(dh.contiguous(), None, x, gamma, mean, rstd, ctx.rms, 0.0, 0, False,
+                                             parts)
+        sums = _sum_rows(part.view(-1, 3 * C))
+        return dx, sums[:C], (sums[C:2 * C] if ctx.has_beta else None), None, None
 
 
 def _norm_ok(x: torch.Tensor, gamma: torch.Tensor) -> bool:
+    # C <= 1024: the backward keeps a row's 4-per-lane slices in registers at
+    # 16 waves/CU; wider rows (Llama) would spill -- they take the ATen path
     return (x.dtype == torch.bfloat16 and gamma.dtype == torch.bfloat16 and x.shape[-1] % 256 == 0
-            and x.shape[-1] <= 5120 and _use_hip(x))
+            and x.shape[-1] <= 1024 and _use_hip(x))
 
 
 def dropout_add_norm(y: torch.Tensor, x: torch.Tensor, gamma: torch.Tensor, beta, eps: float, p: float,
-                     rms: bool = False):
-    """Returns (x + dropout(y), Norm(x + dropout(y))) -- the residual stream and
-    the next sub-block's normalised input."""
+                     rms: bool = False, bias=None):
+    """Returns (x + dropout(y + bias), Norm(...)) -- the residual stream and the
+    next sub-block's normalised input."""
     if y.is_cuda:
         from .linear import autocast_inputs
 
-        y, x = autocast_inputs(y, x)
-    if _norm_ok(x, gamma) and y.dtype == x.dtype:
+        y, x, bias = autocast_inputs(y, x, bias)
+    if _norm_ok(x, gamma) and y.dtype == x.dtype and (bias is None or bias.dtype == x.dtype):
         with torch.autocast("cuda", enabled=False):
-            return _AddNorm.apply(y.contiguous(), x.contiguous(), gamma, beta, float(eps), bool(rms), float(p),
-                                  _new_seed())
+            return _AddNorm.apply(y.contiguous(), x.contiguous(), bias, gamma, beta, float(eps), bool(rms),
+                                  float(p), _new_seed())
+    if bias is not None:
+        y = y + bias
     xo = dropout_add(y, x, p)
     if rms:
         return xo, rms_norm(xo, gamma, eps)
     return xo, F.layer_norm(xo, (x.shape[-1],), gamma, beta, eps)
+
+
+class _BiasGelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, b, exact):
+        ctx.save_for_backward(z, b)
+        ctx.exact = exact
+        return hip.ops().bias_gelu_fwd(z, b, exact)
+
+    @staticmethod
+    def backward(ctx, dh):
+        z, b = ctx.saved_tensors
+        rows = z.numel() // z.shape[-1]
+        parts = max(1, min(1024, rows // 8))  # tools/bench_norm.py sweep: 1024 best at GPT-2 shape
+        dz, part = hip.ops().bias_gelu_bwd(dh.contiguous(), z, b, ctx.exact, parts)
+        return dz, _sum_rows(part), None
+
+
+def bias_gelu(z: torch.Tensor, b: torch.Tensor, exact: bool = False) -> torch.Tensor:
+    """gelu(z + b) (tanh approximation unless exact); fused kernel on the GPU."""
+    if z.is_cuda:
+        from .linear import autocast_inputs
+
+        z, b = autocast_inputs(z, b)
+        if z.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and z.shape[-1] % 8 == 0 and _use_hip(z):
+            with torch.autocast("cuda", enabled=False):
+                return _BiasGelu.apply(z.contiguous(), b, bool(exact))
+    return F.gelu(z + b, approximate="none" if exact else "tanh")
 
 
 def norm(x: torch.Tensor, gamma: torch.Tensor, beta, eps: float, rms: bool = False) -> torch.Tensor:
@@ -163,11 +215,11 @@ def norm_dropout_keep(rows: int, C: int, p: float, seed: int, device=None) -> to
 
 # --------------------------------------------------------------- bias + GELU
 def linear_gelu(x2d: torch.Tensor, w_in_out: torch.Tensor, bias: torch.Tensor, exact: bool = False):
-    """gelu(x @ W + b) with HF Conv1D's [in, out] weight layout."""
+    """gelu(x @ W + b) with HF Conv1D's [in, out] weight layout: GEMM without
+    bias, then one bias+GELU kernel whose backward also yields the bias grad."""
     from .linear import linear_kn
 
-    h = linear_kn(x2d, w_in_out, bias)
-    return F.gelu(h, approximate="none" if exact else "tanh")
+    return bias_gelu(linear_kn(x2d, w_in_out, None), bias, exact)
 
 
 # ------------------------------------------------------------------ attention

@@ -35,6 +35,11 @@ def wgrad(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     if s == 1:
         return a.t() @ b
     part = torch.bmm(a.view(s, M // s, K).transpose(1, 2), b.view(s, M // s, N), out_dtype=torch.float32)
+    if a.dtype == torch.bfloat16 and (K * N) % 4 == 0:
+        from . import hip
+
+        if hip.available():
+            return hip.ops().sum_partials(part)  # one pass: fp32 sum -> bf16
     return part.sum(0).to(a.dtype)
 
 

@@ -8,8 +8,10 @@ from distributed_lion_pytorch_amd.ops import fused, hip
 pytestmark = pytest.mark.gpu
 
 
-def _ref(y, x, g, b, eps, p, seed, rms):
+def _ref(y, x, g, b, eps, p, seed, rms, bias=None):
     rows, C = x.shape
+    if bias is not None:
+        y = y + bias
     if p > 0:
         th = min(65535, int(round(p * 65536)))
         keep = fused.norm_dropout_keep(rows, C, p, seed, x.device)
@@ -26,7 +28,7 @@ def _rel(a, b):
     return (a.float() - b.float()).abs().max().item() / (b.float().abs().max().item() + 1e-6)
 
 
-@pytest.mark.parametrize("C,rms", [(768, False), (1024, True), (4096, True), (1280, False)])
+@pytest.mark.parametrize("C,rms", [(768, False), (1024, True), (512, True), (256, False)])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_add_norm_fwd_bwd(C, rms, p, cuda):
     hip.require()
@@ -37,12 +39,14 @@ def test_add_norm_fwd_bwd(C, rms, p, cuda):
     g = (1 + 0.1 * torch.randn(C, device=cuda)).bfloat16()
     b = None if rms else (0.1 * torch.randn(C, device=cuda)).bfloat16()
     seed = 4242
+    bias = (0.1 * torch.randn(C, device=cuda)).bfloat16()
     ys, xs, gs = y.clone().requires_grad_(), x.clone().requires_grad_(), g.clone().requires_grad_()
     bs = None if b is None else b.clone().requires_grad_()
-    xo, h = fused._AddNorm.apply(ys, xs, gs, bs, 1e-5, rms, p, seed)
-    yr, xr, gr = (t.float().requires_grad_() for t in (y, x, g))
+    bias_s = bias.clone().requires_grad_()
+    xo, h = fused._AddNorm.apply(ys, xs, bias_s, gs, bs, 1e-5, rms, p, seed)
+    yr, xr, gr, bias_r = (t.float().requires_grad_() for t in (y, x, g, bias))
     br = None if b is None else b.float().requires_grad_()
-    xo_r, h_r = _ref(yr, xr, gr, br, 1e-5, p, seed, rms)
+    xo_r, h_r = _ref(yr, xr, gr, br, 1e-5, p, seed, rms, bias_r)
     assert _rel(xo, xo_r) < 1e-2 and _rel(h, h_r) < 2e-2
     dxo = torch.randn_like(x)
     dh = torch.randn_like(x)
@@ -51,6 +55,7 @@ def test_add_norm_fwd_bwd(C, rms, p, cuda):
     assert _rel(ys.grad, yr.grad) < 2e-2
     assert _rel(xs.grad, xr.grad) < 2e-2
     assert _rel(gs.grad, gr.grad) < 2e-2
+    assert _rel(bias_s.grad, bias_r.grad) < 2e-2
     if b is not None:
         assert _rel(bs.grad, br.grad) < 2e-2
 
@@ -69,3 +74,29 @@ def test_plain_norm(cuda):
     h.backward(dh)
     hr.backward(dh.float())
     assert _rel(x.grad, xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_bias_gelu(exact, cuda):
+    hip.require()
+    torch.manual_seed(2)
+    z = torch.randn(300, 3072, device=cuda).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(3072, device=cuda)).bfloat16().requires_grad_()
+    h = fused._BiasGelu.apply(z, b, exact)
+    zr, br = z.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    hr = torch.nn.functional.gelu(zr + br, approximate="none" if exact else "tanh")
+    assert _rel(h, hr) < 1e-2
+    dh = torch.randn_like(h)
+    h.backward(dh)
+    hr.backward(dh.float())
+    assert _rel(z.grad, zr.grad) < 2e-2 and _rel(b.grad, br.grad) < 2e-2
+
+
+@pytest.mark.parametrize("S,shape", [(7, (3, 256)), (2048, (3, 768)), (1000, (3076,)), (16, (768, 3072))])
+def test_sum_partials(S, shape, cuda):
+    hip.require()
+    part = torch.randn(S, *shape, device=cuda)
+    out = hip.ops().sum_partials(part)
+    assert out.dtype == torch.bfloat16 and out.shape == shape
+    ref = part.double().sum(0)
+    assert ((out.double() - ref).abs() <= ref.abs() * 2 ** -7 + 1e-3 * S ** 0.5).all()

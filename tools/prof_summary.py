@@ -1,0 +1,13 @@
+"""Summarize a rocprofv3 kernel_stats.csv per micro-batch: python tools/prof_summary.py <csv> [micro_batches] [top]"""
+import csv
+import sys
+
+path = sys.argv[1]
+mb = int(sys.argv[2]) if len(sys.argv) > 2 else 24
+top = int(sys.argv[3]) if len(sys.argv) > 3 else 30
+rows = list(csv.DictReader(open(path)))
+tot = sum(float(r["TotalDurationNs"]) for r in rows)
+print(f"total {tot / 1e6:.1f} ms = {tot / 1e6 / mb:.2f} ms per micro-batch")
+for r in rows[:top]:
+    print(f"{float(r['Percentage']):6.2f}% {float(r['TotalDurationNs']) / 1e6 / mb:7.3f}ms/mb "
+          f"calls/mb={int(r['Calls']) / mb:6.1f} avg={float(r['AverageNs']) / 1e3:8.1f}us  {r['Name'][:90]}")
