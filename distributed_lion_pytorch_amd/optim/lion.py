@@ -24,6 +24,9 @@ Keyword-only extensions (all optional):
   backend      "auto" | "hip" | "torch"
   seed         base seed of the stochastic-binarization RNG
   telemetry    collect vote-agreement counts (see :meth:`stats`)
+  elastic_timeout  seconds; enables real worker-dropout handling: a heartbeat
+               before each step's vote detects dead ranks and the survivors
+               continue in a shrunken group (parallel/elastic.py)
 """
 from __future__ import annotations
 
@@ -67,6 +70,7 @@ class Lion(Optimizer):
         seed: int = 0,
         telemetry: bool = False,
         verify_consistency: bool = True,
+        elastic_timeout: Optional[float] = None,
     ):
         if not lr > 0.0:
             raise ValueError(f"Invalid learning rate: {lr}")
@@ -102,6 +106,8 @@ class Lion(Optimizer):
         self._agree: Optional[torch.Tensor] = None
         self._agree_total = 0
         self.last_world = 1
+        self.elastic_timeout = elastic_timeout
+        self._elastic = None
 
     # ------------------------------------------------------------ topology
     def _world(self):
@@ -138,6 +144,21 @@ class Lion(Optimizer):
             self._alive_dev = t.to(device)
             self._alive_host = host
         return self._alive_dev
+
+    def _elastic_check(self) -> None:
+        """Real dropout: heartbeat before the vote; on a drop, switch to the
+        survivors' group (the plan is rebuilt below because the world changed)."""
+        if self.elastic_timeout is None or not (dist.is_available() and dist.is_initialized()):
+            return
+        if self._elastic is None:
+            from ..parallel.elastic import ElasticMembership
+
+            self._elastic = ElasticMembership(self.elastic_timeout, group=self.process_group)
+        grp = self._elastic.check(self._n_steps)
+        if grp is not None:
+            self.process_group = grp
+            self._dropped.clear()  # simulated-dropout ranks were numbered in the old group
+            self._alive_dev = None
 
     # --------------------------------------------------------------- plan
     def _get_plan(self, entries, world: int, rank: int):
@@ -201,6 +222,7 @@ class Lion(Optimizer):
         if not entries:
             return loss
 
+        self._elastic_check()
         world, rank = self._world()
         self.last_world = world
         plan = self._get_plan(entries, world, rank)
@@ -251,6 +273,9 @@ class Lion(Optimizer):
             out["numel"] = sum(s.numel for s in self._plan.segments)
             out["n_buckets"] = len(self._plan.buckets)
             out["wire_bytes_analytic"] = wire_bytes_per_step(out["numel"], self.last_world, self.exchange_name)
+        if self._elastic is not None:
+            out["live_ranks"] = list(self._elastic.members)
+            out["dropout_events"] = list(self._elastic.events)
         if self._agree is not None:
             out["vote_agree"] = int(self._agree.item())
             if reset:

@@ -51,6 +51,8 @@ class AsyncTrainingArguments(TrainingArguments):
     lion_backend: str = field(default="auto", metadata={"help": "auto | hip | torch"})
     lion_dropout_schedule: Optional[str] = field(default=None, metadata={
         "help": "fault injection, e.g. '100:3' drops rank 3 from optimizer step 100 on"})
+    lion_elastic_timeout: Optional[float] = field(default=None, metadata={
+        "help": "real worker dropout: heartbeat timeout (s) before each vote; survivors regroup and continue"})
     synthetic_data: bool = field(default=False, metadata={"help": "train on synthetic token ids (offline)"})
 
 
@@ -79,6 +81,7 @@ def build_lion(model: torch.nn.Module, args, lr: Optional[float] = None, weight_
         bucket_mb=getattr(args, "lion_bucket_mb", 32.0),
         backend=getattr(args, "lion_backend", "auto"),
         seed=getattr(args, "seed", 0),
+        elastic_timeout=getattr(args, "lion_elastic_timeout", None),
     )
     sched = parse_dropout_schedule(getattr(args, "lion_dropout_schedule", None))
     if sched:

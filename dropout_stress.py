@@ -1,0 +1,122 @@
+#!/usr/bin/env python
+"""Worker-dropout stress run (BASELINE config #5: "Llama-3 8B bf16 Distributed
+Lion async worker-dropout stress, 1 rank drops mid-run").
+
+Every rank trains its own replica on its own synthetic data through the
+native engine (no gradient all-reduce, Lion vote sync).  At ``--drop_step``
+rank ``--drop_rank`` dies without warning (``os._exit``: no teardown, no
+goodbye).  With ``--elastic_timeout`` the survivors detect it at the next
+vote heartbeat, regroup and carry on (parallel/elastic.py); the run then
+checks that the survivors' parameters are still bit-identical and reports
+tokens/s before and after the drop.  Without ``--elastic_timeout`` the
+survivors hang in the collective exactly like the reference does
+(/root/reference/distributed_lion.py:81) -- do not run that on shared boxes.
+
+  torchrun --nproc-per-node 8 --master-addr 127.0.0.1 dropout_stress.py \
+      --model llama-3-8b --micro_batch 1 --seq_len 2048 --steps 20 --drop_rank 5 --drop_step 8
+  # CPU smoke (gloo): --model llama-tiny / gpt2-tiny --device cpu
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_lion_pytorch_amd import Lion  # noqa: E402
+from distributed_lion_pytorch_amd.models.registry import build_model, load_config  # noqa: E402
+from distributed_lion_pytorch_amd.trainer.engine import TrainStep, broadcast_parameters  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
+    ap.add_argument("--micro_batch", type=int, default=1)
+    ap.add_argument("--seq_len", type=int, default=2048)
+    ap.add_argument("--grad_accum", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--drop_rank", type=int, default=1)
+    ap.add_argument("--drop_step", type=int, default=8)
+    ap.add_argument("--elastic_timeout", type=float, default=30.0)
+    ap.add_argument("--exchange", default="a2a")
+    ap.add_argument("--lr", type=float, default=1e-5)
+    ap.add_argument("--weight_decay", type=float, default=0.0)
+    ap.add_argument("--gradient_checkpointing", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.device == "cuda":
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        dist.init_process_group("nccl", device_id=dev)
+        dtype = torch.bfloat16
+    else:
+        dev = torch.device("cpu")
+        dist.init_process_group("gloo")
+        dtype = torch.float32
+    if a.drop_rank == 0:
+        raise SystemExit("--drop_rank 0: rank 0 may host the rendezvous store; drop another rank")
+    cfg = load_config(a.model)
+    torch.manual_seed(0)
+    model = build_model(cfg, native=True).to(device=dev, dtype=dtype)
+    if a.gradient_checkpointing:
+        model.gradient_checkpointing_enable()
+    broadcast_parameters(model)
+    opt = Lion([p for p in model.parameters() if p.requires_grad], lr=a.lr, weight_decay=a.weight_decay,
+               exchange=a.exchange, elastic_timeout=a.elastic_timeout)
+    step_fn = TrainStep(model, opt, grad_accum=a.grad_accum, max_grad_norm=1.0)
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+
+    def batches():
+        for _ in range(a.grad_accum):
+            ids = torch.randint(0, cfg.vocab_size, (a.micro_batch, a.seq_len), device=dev, generator=gen)
+            yield {"input_ids": ids, "labels": ids}
+
+    log = []
+    for s in range(a.steps):
+        if rank == a.drop_rank and s == a.drop_step:
+            print(json.dumps({"rank": rank, "event": "dying", "step": s}), flush=True)
+            os._exit(0)
+        t0 = time.perf_counter()
+        loss = step_fn(batches())
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        w = opt.last_world
+        log.append({"step": s, "world": w, "loss": float(loss), "s": dt,
+                    "tokens_per_s": w * a.grad_accum * a.micro_batch * a.seq_len / dt})
+    # survivors: compare replicas inside the shrunken group
+    h = hashlib.sha256()
+    for p in model.parameters():
+        h.update(p.detach().float().cpu().numpy().tobytes())
+    d = torch.tensor([int.from_bytes(h.digest()[:7], "little")], dtype=torch.int64, device=dev)
+    lo, hi = d.clone(), d.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=opt.process_group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=opt.process_group)
+    st = opt.stats()
+    if dist.get_rank(opt.process_group) == 0:
+        pre = [r["tokens_per_s"] for r in log if r["step"] < a.drop_step and r["step"] > 0]
+        post = [r["tokens_per_s"] for r in log if r["step"] > a.drop_step + 1]
+        print(json.dumps({
+            "metric": "worker-dropout stress", "model": a.model, "world_start": world, "world_end": st["world"],
+            "dropout_events": st.get("dropout_events"), "replicas_identical": bool(int(lo) == int(hi)),
+            "tokens_per_s_before": sum(pre) / max(1, len(pre)), "tokens_per_s_after": sum(post) / max(1, len(post)),
+            "final_loss": log[-1]["loss"], "steps": log}), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
