@@ -16,6 +16,9 @@ Every step is a full training step (8 micro-batches fwd+bwd, clip, vote
 exchange over RCCL, Lion update).  Rank 0 prints one JSON line.
 `--impl reference` runs the reference algorithm on the same hardware (HF
 GPT2LMHeadModel + per-tensor int64 all_gather Lion) for an A/B comparison.
+`--task sft` measures BASELINE config #3 instead: Llama-2-7B, LoRA r=8 on
+q_proj/v_proj (bf16 base instead of the reference's 4-bit NF4), per-device
+batch 4 x seq 1024, grad-accum 2, Lion lr 1e-4 / wd 0.05.
 """
 from __future__ import annotations
 
@@ -31,9 +34,20 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from distributed_lion_pytorch_amd import Lion  # noqa: E402
-from distributed_lion_pytorch_amd.models.gpt2 import GPT2LMHeadModel, gpt2_config  # noqa: E402
+from distributed_lion_pytorch_amd.models.gpt2 import gpt2_config  # noqa: E402
 from distributed_lion_pytorch_amd.parallel.exchange import wire_bytes_per_step  # noqa: E402
 from distributed_lion_pytorch_amd.trainer.engine import StepTimer, TrainStep, broadcast_parameters  # noqa: E402
+
+
+# reference configs: run_clm README (/root/reference/README.md:20-37) and
+# sft_llama2 README + defaults (README.md:41-62, sft_llama2.py:29-51)
+PRESETS = {
+    "clm": dict(model="gpt2", micro_batch=20, seq_len=1024, grad_accum=8, lr=1e-4, weight_decay=0.1, lora=None,
+                metric="tokens/sec + all-reduce bytes/step, GPT-2 CLM at 1/2/4/8 MI355X"),
+    "sft": dict(model="llama-2-7b", micro_batch=4, seq_len=1024, grad_accum=2, lr=1e-4, weight_decay=0.05,
+                lora=dict(r=8, lora_alpha=16, lora_dropout=0.05, target_modules=["q_proj", "v_proj"]),
+                metric="tokens/sec + all-reduce bytes/step, Llama-2-7B LoRA SFT (sft_llama2 config)"),
+}
 
 
 def parse():
@@ -41,12 +55,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--model", default="gpt2")
-    ap.add_argument("--micro_batch", type=int, default=20)
-    ap.add_argument("--seq_len", type=int, default=1024)
-    ap.add_argument("--grad_accum", type=int, default=8)
-    ap.add_argument("--lr", type=float, default=1e-4)
-    ap.add_argument("--weight_decay", type=float, default=0.1)
+    ap.add_argument("--task", default="clm", choices=sorted(PRESETS),
+                    help="clm: GPT-2 pretraining (headline); sft: Llama-2-7B LoRA SFT (sft_llama2 config)")
+    ap.add_argument("--model", default=None)
+    ap.add_argument("--micro_batch", type=int, default=None)
+    ap.add_argument("--seq_len", type=int, default=None)
+    ap.add_argument("--grad_accum", type=int, default=None)
+    ap.add_argument("--lr", type=float, default=None)
+    ap.add_argument("--weight_decay", type=float, default=None)
+    ap.add_argument("--gradient_checkpointing", action="store_true")
     ap.add_argument("--max_grad_norm", type=float, default=1.0)
     ap.add_argument("--exchange", default="a2a", help="allgather | a2a | ref_int64")
     ap.add_argument("--bucket_mb", type=float, default=32.0)
@@ -55,7 +72,11 @@ def parse():
     ap.add_argument("--dropout", type=float, default=None, help="override GPT-2 dropout (default 0.1)")
     ap.add_argument("--profile_dir", default=None)
     ap.add_argument("--rocm_fa", default=None, help="PyTorch SDPA flash library on ROCm: ck | aotriton")
-    return ap.parse_args()
+    a = ap.parse_args()
+    for k, v in PRESETS[a.task].items():
+        if getattr(a, k, None) is None:
+            setattr(a, k, v)
+    return a
 
 
 def setup_dist(args):
@@ -73,17 +94,26 @@ def setup_dist(args):
 
 
 def build_native(args, dev):
+    from distributed_lion_pytorch_amd.models.registry import build_model, load_config
     from distributed_lion_pytorch_amd.ops import fused
 
     fused.set_impl(args.fused)
-    cfg = gpt2_config(args.model)
-    if args.dropout is not None:
+    cfg = load_config(args.model)
+    if args.dropout is not None and cfg.model_type == "gpt2":
         cfg.resid_pdrop = cfg.embd_pdrop = cfg.attn_pdrop = args.dropout
     torch.manual_seed(0)
-    model = GPT2LMHeadModel(cfg).to(device=dev, dtype=torch.bfloat16)
+    with torch.device(dev):  # materialise weights on the GPU directly (7B: no host round trip)
+        model = build_model(cfg, native=True).to(dtype=torch.bfloat16)
+    if args.lora:
+        from distributed_lion_pytorch_amd.models.lora import LoraConfig, inject_lora
+
+        inject_lora(model, LoraConfig(**args.lora))
+        model.to(device=dev, dtype=torch.bfloat16)
+    if args.gradient_checkpointing:
+        model.gradient_checkpointing_enable()
     broadcast_parameters(model)
-    opt = Lion(model.parameters(), lr=args.lr, weight_decay=args.weight_decay, exchange=args.exchange,
-               bucket_mb=args.bucket_mb)
+    opt = Lion([p for p in model.parameters() if p.requires_grad], lr=args.lr, weight_decay=args.weight_decay,
+               exchange=args.exchange, bucket_mb=args.bucket_mb)
     return model, opt, cfg
 
 
@@ -131,6 +161,7 @@ def main():
     build = build_native if args.impl == "native" else build_reference
     model, opt, cfg = build(args, dev)
     n_params = sum({p.data_ptr(): p.numel() for p in model.parameters()}.values())
+    n_train = sum({p.data_ptr(): p.numel() for p in model.parameters() if p.requires_grad}.values())
 
     if args.impl == "native":
         loss_fn = None
@@ -173,10 +204,10 @@ def main():
     ms = 1000.0 * elapsed / args.steps
     stats = opt.stats() if hasattr(opt, "stats") else {}
     exchange = args.exchange if args.impl == "native" else "ref_int64"
-    wire = wire_bytes_per_step(n_params, world, exchange)
+    wire = wire_bytes_per_step(n_train, world, exchange)
     if rank == 0:
         out = {
-            "metric": "tokens/sec + all-reduce bytes/step, GPT-2 CLM at 1/2/4/8 MI355X",
+            "metric": args.metric,
             "value": round(tps, 1),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -187,20 +218,22 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (random token ids, GPT-2 vocab), random-init weights",
+            "data": f"synthetic (random token ids of the {args.model} vocab), random-init weights",
             "config": {
                 "model": f"{args.model} ({n_params / 1e6:.1f}M params)",
+                "trainable_params": n_train,
+                "lora": args.lora,
                 "global_batch": world * args.grad_accum * args.micro_batch,
                 "micro_batch": args.micro_batch,
                 "grad_accum": args.grad_accum,
                 "seq_len": args.seq_len,
                 "parallelism": f"dp{world}",
-                "optimizer": "distributed Lion (majority vote), lr 1e-4, wd 0.1",
+                "optimizer": f"distributed Lion (majority vote), lr {args.lr:g}, wd {args.weight_decay:g}",
                 "exchange": exchange,
                 "impl": args.impl,
             },
             "wire_bytes_per_step_per_rank": wire,
-            "bf16_allreduce_bytes_per_step_per_rank": 0 if world == 1 else int(2 * (world - 1) / world * 2 * n_params),
+            "bf16_allreduce_bytes_per_step_per_rank": 0 if world == 1 else int(2 * (world - 1) / world * 2 * n_train),
             "loss": round(float(loss.item()), 4),
             "optimizer_stats": stats,
         }

@@ -380,9 +380,58 @@ Tensor sum_partials(const Tensor& part) {
   return out;
 }
 
+// ---------------------------------------------------------------- SwiGLU / RoPE
+void check_same(const Tensor& a, const Tensor& b, const char* what) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.is_contiguous(), "dlion ", what,
+              ": inputs must be contiguous bf16 GPU tensors");
+  TORCH_CHECK(b.is_cuda() && b.scalar_type() == at::kBFloat16 && b.is_contiguous() && b.sizes() == a.sizes(),
+              "dlion ", what, ": operand shapes / dtypes differ");
+  TORCH_CHECK(a.numel() % 8 == 0, "dlion ", what, ": numel must be a multiple of 8");
+}
+
+Tensor swiglu_fwd(const Tensor& g, const Tensor& u) {
+  check_same(g, u, "swiglu");
+  const c10::DeviceGuard dg(g.device());
+  auto h = at::empty_like(g);
+  check_hip(dlion::launch_swiglu_fwd(g.data_ptr(), u.data_ptr(), h.data_ptr(), g.numel(), cur_stream()), "swiglu_fwd");
+  return h;
+}
+
+std::tuple<Tensor, Tensor> swiglu_bwd(const Tensor& dh, const Tensor& g, const Tensor& u) {
+  check_same(g, u, "swiglu");
+  check_same(g, dh, "swiglu");
+  const c10::DeviceGuard dg(g.device());
+  auto dgate = at::empty_like(g), dup = at::empty_like(u);
+  check_hip(dlion::launch_swiglu_bwd(dh.data_ptr(), g.data_ptr(), u.data_ptr(), dgate.data_ptr(), dup.data_ptr(),
+                                     g.numel(), cur_stream()),
+            "swiglu_bwd");
+  return {dgate, dup};
+}
+
+// x [B, T, H, D] contiguous, cos / sin [>= T, D] bf16 (row t = position t)
+Tensor rope(const Tensor& x, const Tensor& cos, const Tensor& sin, bool inverse) {
+  TORCH_CHECK(x.dim() == 4 && x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(),
+              "dlion rope: x must be a contiguous bf16 [B, T, H, D] GPU tensor");
+  const int64_t B = x.size(0), T = x.size(1), H = x.size(2), D = x.size(3);
+  TORCH_CHECK(D % 8 == 0, "dlion rope: head_dim must be a multiple of 8");
+  for (const Tensor* t : {&cos, &sin})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->dim() == 2 &&
+                    t->size(0) >= T && t->size(1) == D,
+                "dlion rope: cos/sin must be contiguous bf16 [>=T, D]");
+  const c10::DeviceGuard dg(x.device());
+  auto y = at::empty_like(x);
+  check_hip(dlion::launch_rope(x.data_ptr(), cos.data_ptr(), sin.data_ptr(), y.data_ptr(), B * T,
+                               static_cast<int>(T), static_cast<int>(H), static_cast<int>(D), inverse, cur_stream()),
+            "rope");
+  return y;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dlion, m) {
+  m.def("swiglu_fwd(Tensor g, Tensor u) -> Tensor");
+  m.def("swiglu_bwd(Tensor dh, Tensor g, Tensor u) -> (Tensor, Tensor)");
+  m.def("rope(Tensor x, Tensor cos, Tensor sin, bool inverse) -> Tensor");
   m.def(
       "add_norm_fwd(Tensor x, Tensor? y, Tensor? bias, Tensor gamma, Tensor? beta, float eps, bool rms, float p,"
       " int seed) -> (Tensor, Tensor, Tensor, Tensor)");
@@ -425,4 +474,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("bias_gelu_fwd", &bias_gelu_fwd);
   m.impl("bias_gelu_bwd", &bias_gelu_bwd);
   m.impl("sum_partials", &sum_partials);
+  m.impl("swiglu_fwd", &swiglu_fwd);
+  m.impl("swiglu_bwd", &swiglu_bwd);
+  m.impl("rope", &rope);
 }

@@ -1,5 +1,5 @@
-// Bias + GELU (forward / backward with fused bias gradient) and fp32 partial-sum
-// reduction to bf16, for gfx950.
+// Elementwise epilogues for gfx950: bias + GELU (forward / backward with fused
+// bias gradient), SwiGLU, rotary embedding, and fp32 partial-sum reduction to bf16.
 //
 // MLP up-projection in the reference (HF GPT-2 NewGELU on ATen): GEMM with
 // bias epilogue -> GELU kernel; backward: GELU-backward kernel -> separate
@@ -118,6 +118,102 @@ __global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restri
   }
 }
 
+// ------------------------------------------------------------------ SwiGLU
+// Llama MLP activation h = silu(g) * u (HF LlamaMLP: act_fn(gate_proj(x)) *
+// up_proj(x)), one pass each way: ATen needs silu + mul forward and
+// mul / silu_backward / mul backward with fp32 -> bf16 round trips between.
+__device__ __forceinline__ float sigmoid_f(float a) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-a * 1.4426950408889634f));
+}
+
+__global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ u,
+                                                        uint16_t* __restrict__ h, int64_t n8) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n8;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    float gv[8], uv[8], o[8];
+    Elem<kBF16>::load8(g + i * 8, gv);
+    Elem<kBF16>::load8(u + i * 8, uv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = gv[j] * sigmoid_f(gv[j]) * uv[j];
+    Elem<kBF16>::store8(h + i * 8, o);
+  }
+}
+
+__global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restrict__ dh,
+                                                        const uint16_t* __restrict__ g,
+                                                        const uint16_t* __restrict__ u, uint16_t* __restrict__ dg,
+                                                        uint16_t* __restrict__ du, int64_t n8) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n8;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    float dv[8], gv[8], uv[8], og[8], ou[8];
+    Elem<kBF16>::load8(dh + i * 8, dv);
+    Elem<kBF16>::load8(g + i * 8, gv);
+    Elem<kBF16>::load8(u + i * 8, uv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float sg = sigmoid_f(gv[j]);
+      ou[j] = dv[j] * gv[j] * sg;
+      og[j] = dv[j] * uv[j] * sg * (1.f + gv[j] * (1.f - sg));
+    }
+    Elem<kBF16>::store8(dg + i * 8, og);
+    Elem<kBF16>::store8(du + i * 8, ou);
+  }
+}
+
+// 4 bf16 <-> fp32 (one 8-byte access)
+__device__ __forceinline__ void load4(const uint16_t* p, float (&o)[4]) {
+  const uint2 v = *reinterpret_cast<const uint2*>(p);
+  o[0] = bf16_to_f32(v.x & 0xffffu);
+  o[1] = bf16_to_f32(v.x >> 16);
+  o[2] = bf16_to_f32(v.y & 0xffffu);
+  o[3] = bf16_to_f32(v.y >> 16);
+}
+__device__ __forceinline__ void store4(uint16_t* p, const float (&o)[4]) {
+  uint2 v;
+  v.x = static_cast<uint32_t>(f32_to_bf16(o[0])) | (static_cast<uint32_t>(f32_to_bf16(o[1])) << 16);
+  v.y = static_cast<uint32_t>(f32_to_bf16(o[2])) | (static_cast<uint32_t>(f32_to_bf16(o[3])) << 16);
+  *reinterpret_cast<uint2*>(p) = v;
+}
+
+// ------------------------------------------------------------------- RoPE
+// HF rotate-half rotary embedding on x [rows = B*T, H, D] (row r is position
+// r % T) with cos/sin tables [T, D]; one rounding per output instead of
+// ATen's slice / neg / cat / 2 mul / add chain.  inverse = the transpose
+// rotation (the backward).  Thread = 4 consecutive dims of the first half and
+// their partners in the second half.
+__global__ void __launch_bounds__(256) rope_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ cs,
+                                                  const uint16_t* __restrict__ sn, uint16_t* __restrict__ y,
+                                                  int64_t rows, int T, int H, int D, bool inverse) {
+  const int hd = D / 2, q = hd / 4;  // quads per half
+  const int64_t n = rows * H * q;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int d0 = static_cast<int>(i % q) * 4;
+    const int64_t rh = i / q;  // row * H + head
+    const int t = static_cast<int>((rh / H) % T);
+    const int64_t o = rh * D;
+    float a[4], b[4], ca[4], cb[4], sa[4], sb[4], oa[4], ob[4];
+    load4(x + o + d0, a);
+    load4(x + o + hd + d0, b);
+    load4(cs + static_cast<int64_t>(t) * D + d0, ca);
+    load4(cs + static_cast<int64_t>(t) * D + hd + d0, cb);
+    load4(sn + static_cast<int64_t>(t) * D + d0, sa);
+    load4(sn + static_cast<int64_t>(t) * D + hd + d0, sb);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!inverse) {
+        oa[j] = a[j] * ca[j] - b[j] * sa[j];
+        ob[j] = b[j] * cb[j] + a[j] * sb[j];
+      } else {
+        oa[j] = a[j] * ca[j] + b[j] * sb[j];
+        ob[j] = b[j] * cb[j] - a[j] * sa[j];
+      }
+    }
+    store4(y + o + d0, oa);
+    store4(y + o + hd + d0, ob);
+  }
+}
+
 // Tall stacks (S in the hundreds/thousands, n a few thousand: the per-block /
 // per-wave partials of the norm and bias-GELU backward kernels).  Block = 8
 // float4 column quads x 32 row lanes; each thread strides the rows by 32 and
@@ -193,6 +289,31 @@ hipError_t launch_bias_gelu_bwd(const void* dh, const void* z, const void* b, vo
     default: return hipErrorInvalidValue;  // N <= 16384
   }
 #undef GELU_BWD
+  return hipGetLastError();
+}
+
+hipError_t launch_swiglu_fwd(const void* g, const void* u, void* h, int64_t n, hipStream_t st) {
+  if (n % 8 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, st, static_cast<const uint16_t*>(g),
+                     static_cast<const uint16_t*>(u), static_cast<uint16_t*>(h), n / 8);
+  return hipGetLastError();
+}
+
+hipError_t launch_swiglu_bwd(const void* dh, const void* g, const void* u, void* dg, void* du, int64_t n,
+                             hipStream_t st) {
+  if (n % 8 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, st, static_cast<const uint16_t*>(dh),
+                     static_cast<const uint16_t*>(g), static_cast<const uint16_t*>(u), static_cast<uint16_t*>(dg),
+                     static_cast<uint16_t*>(du), n / 8);
+  return hipGetLastError();
+}
+
+hipError_t launch_rope(const void* x, const void* cos, const void* sin, void* y, int64_t rows, int T, int H, int D,
+                       bool inverse, hipStream_t st) {
+  if (D % 8 != 0 || T <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rope_kernel, dim3(grid_for(rows * H * (D / 8), 256)), dim3(256), 0, st,
+                     static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(cos),
+                     static_cast<const uint16_t*>(sin), static_cast<uint16_t*>(y), rows, T, H, D, inverse);
   return hipGetLastError();
 }
 

@@ -27,8 +27,8 @@ hipError_t launch_transpose_btxd(const void* in, int64_t sb, int64_t st, int64_t
                                  int D, int ldt, hipStream_t stream);
 
 // ---- fused residual + dropout + LayerNorm/RMSNorm (norm_kernels.hip)
-// backward: `parts` blocks of kNormBwdWaves waves; part is [parts][3][C]
-constexpr int kNormBwdWaves = 4;
+// backward: `parts` blocks (4 rows of C <= 1024, or one wide row, per block
+// iteration); part is [parts][3][C]
 hipError_t launch_add_norm_fwd(const void* x, const void* y, const void* bias, const void* gamma, const void* beta,
                                void* xo, void* h, float* mean, float* rstd, int64_t rows, int C, float eps, bool rms,
                                uint32_t seed, uint32_t thresh16, float inv_keep, hipStream_t st);
@@ -36,11 +36,16 @@ hipError_t launch_add_norm_bwd(const void* dh, const void* dxo_in, const void* x
                                const float* rstd, void* dx, void* dy, float* part, int parts, int64_t rows, int C,
                                bool rms, uint32_t seed, uint32_t thresh16, float inv_keep, hipStream_t st);
 
-// ---- bias + GELU, partial sums (elementwise_kernels.hip)
+// ---- bias + GELU, SwiGLU, RoPE, partial sums (elementwise_kernels.hip)
 hipError_t launch_bias_gelu_fwd(const void* z, const void* b, void* h, int64_t rows, int N, bool exact,
                                 hipStream_t st);
 hipError_t launch_bias_gelu_bwd(const void* dh, const void* z, const void* b, void* dz, float* dbpart, int parts,
                                 int64_t rows, int N, bool exact, hipStream_t st);
+hipError_t launch_swiglu_fwd(const void* g, const void* u, void* h, int64_t n, hipStream_t st);
+hipError_t launch_swiglu_bwd(const void* dh, const void* g, const void* u, void* dg, void* du, int64_t n,
+                             hipStream_t st);
+hipError_t launch_rope(const void* x, const void* cos, const void* sin, void* y, int64_t rows, int T, int H, int D,
+                       bool inverse, hipStream_t st);
 hipError_t launch_sum_partials(const float* part, int S, int64_t n, void* out, hipStream_t st);
 
 // ---- LM head cross-entropy (xent_kernels.hip)

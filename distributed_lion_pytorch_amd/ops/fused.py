@@ -56,15 +56,62 @@ def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
 
 
 # ---------------------------------------------------------- rotary / SwiGLU
-def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
-    """x [B, T, H, D]; cos/sin [T, D]; HF rotate-half convention."""
+def rope_reference(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """x [B, T, H, D]; cos/sin [T, D]; HF rotate-half convention (ATen chain)."""
     d2 = x.shape[-1] // 2
     x1, x2 = x[..., :d2], x[..., d2:]
     rot = torch.cat([-x2, x1], dim=-1)
-    return x * cos[None, :, None, :] + rot * sin[None, :, None, :]
+    T = x.shape[1]
+    return x * cos[None, :T, None, :] + rot * sin[None, :T, None, :]
+
+
+class _Rope(torch.autograd.Function):
+    """One gfx950 kernel each way (csrc/elementwise_kernels.hip rope_kernel);
+    the backward is the inverse rotation."""
+
+    @staticmethod
+    def forward(ctx, x, cos, sin):
+        ctx.save_for_backward(cos, sin)
+        return hip.ops().rope(x, cos, sin, False)
+
+    @staticmethod
+    def backward(ctx, dy):
+        cos, sin = ctx.saved_tensors
+        return hip.ops().rope(dy.contiguous(), cos, sin, True), None, None
+
+
+def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """x [B, T, H, D]; cos/sin [>=T, D]; HF rotate-half convention."""
+    if (x.dtype == torch.bfloat16 and cos.dtype == torch.bfloat16 and sin.dtype == torch.bfloat16
+            and x.shape[-1] % 8 == 0 and _use_hip(x)):
+        with torch.autocast("cuda", enabled=False):
+            return _Rope.apply(x.contiguous(), cos.contiguous(), sin.contiguous())
+    return rope_reference(x, cos, sin)
+
+
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gate, up):
+        ctx.save_for_backward(gate, up)
+        return hip.ops().swiglu_fwd(gate, up)
+
+    @staticmethod
+    def backward(ctx, dh):
+        gate, up = ctx.saved_tensors
+        dg, du = hip.ops().swiglu_bwd(dh.contiguous(), gate, up)
+        return dg, du
 
 
 def swiglu(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+    """silu(gate) * up (Llama MLP); one fused kernel each way on the GPU."""
+    if gate.is_cuda:
+        from .linear import autocast_inputs
+
+        gate, up = autocast_inputs(gate, up)
+    if (gate.dtype == torch.bfloat16 and up.dtype == torch.bfloat16 and gate.shape == up.shape
+            and gate.numel() % 8 == 0 and _use_hip(gate)):
+        with torch.autocast("cuda", enabled=False):
+            return _SwiGLU.apply(gate.contiguous(), up.contiguous())
     return F.silu(gate) * up
 
 
@@ -76,15 +123,17 @@ def dropout_add(y: torch.Tensor, residual: torch.Tensor, p: float) -> torch.Tens
 
 
 # --------------------------------------- fused residual + dropout + LN / RMSNorm
-_NORM_BWD_WAVES = 4  # csrc/kernels.h kNormBwdWaves
+_NORM_BWD_ROWS = 4  # rows per backward block-iteration for C <= 1024 (csrc/norm_kernels.hip RowGroup)
 _NORM_PARTS_CAP = int(os.environ.get("DLION_NORM_PARTS", "512"))
 
 
-def _norm_parts(rows: int) -> int:
+def _norm_parts(rows: int, C: int) -> int:
     # blocks of 4 waves, one fp32 partial row triple per block: enough waves to
     # cover the CUs a few times over while the partial stack stays a small
-    # fraction of the row traffic (tools/bench_norm.py: 512 best at 20480x768)
-    return max(1, min(_NORM_PARTS_CAP, rows // (4 * _NORM_BWD_WAVES)))
+    # fraction of the row traffic (tools/bench_norm.py: 512 best at 20480x768).
+    # C <= 1024: 4 rows per block-iteration, wider: 1 (4-wave rows)
+    rows_per_iter = _NORM_BWD_ROWS if C <= 1024 else 1
+    return max(1, min(_NORM_PARTS_CAP, rows // (4 * rows_per_iter)))
 
 
 def _sum_rows(part: torch.Tensor) -> torch.Tensor:
@@ -111,7 +160,7 @@ class _AddNorm(torch.autograd.Function):
         rows = xo.numel() // C
         if dh is None:
             dh = torch.zeros_like(xo)
-        parts = _norm_parts(rows)
+        parts = _norm_parts(rows, C)
         dx, dy, part = hip.ops().add_norm_bwd(dh.contiguous(), None if dxo is None else dxo.contiguous(), xo, gamma,
                                               mean, rstd, ctx.rms, ctx.p, ctx.seed, True, parts)
         sums = _sum_rows(part.view(-1, 3 * C))
@@ -133,18 +182,21 @@ class _Norm(torch.autograd.Function):
     def backward(ctx, dh):
         x, gamma, mean, rstd = ctx.saved_tensors
         C = x.shape[-1]
-        parts = _norm_parts(x.numel() // C)
+        parts = _norm_parts(x.numel() // C, C)
         dx, _, part = hip.ops().add_norm_bwd(dh.contiguous(), None, x, gamma, mean, rstd, ctx.rms, 0.0, 0, False,
                                              parts)
         sums = _sum_rows(part.view(-1, 3 * C))
         return dx, sums[:C], (sums[C:2 * C] if ctx.has_beta else None), None, None
 
 
+NORM_WIDTHS = (256, 512, 768, 1024, 2048, 3072, 4096, 5120, 6144, 8192)  # csrc/norm_kernels.hip NORM_DISPATCH
+
+
 def _norm_ok(x: torch.Tensor, gamma: torch.Tensor) -> bool:
-    # C <= 1024: the backward keeps a row's 4-per-lane slices in registers at
-    # 16 waves/CU; wider rows (Llama) would spill -- they take the ATen path
-    return (x.dtype == torch.bfloat16 and gamma.dtype == torch.bfloat16 and x.shape[-1] % 256 == 0
-            and x.shape[-1] <= 1024 and _use_hip(x))
+    # the kernels hold a whole row in registers: one wave per row up to 1024,
+    # one 4-wave block per row for the Llama widths
+    return (x.dtype == torch.bfloat16 and gamma.dtype == torch.bfloat16 and x.shape[-1] in NORM_WIDTHS
+            and _use_hip(x))
 
 
 def dropout_add_norm(y: torch.Tensor, x: torch.Tensor, gamma: torch.Tensor, beta, eps: float, p: float,
