@@ -290,7 +290,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> add_norm_fwd(const Tensor& x, const s
   const int64_t C = x.size(-1), rows = x.numel() / C;
   check_rows(x, "x", C);
   check_rows(gamma, "gamma", C);
-  TORCH_CHECK(C % 256 == 0 && C <= 5120, "dlion norm: hidden size must be a multiple of 256, <= 5120");
+  TORCH_CHECK((C % 256 == 0 && C <= 1024) || (C % 1024 == 0 && C >= 2048 && C <= 8192 && C != 7168),
+              "dlion norm: hidden size must be one of 256, 512, 768, 1024, 2048, 3072, 4096, 5120, 6144, 8192");
   TORCH_CHECK(rms || beta.has_value(), "dlion norm: LayerNorm needs beta");
   if (y.has_value()) check_rows(*y, "y", C);
   if (bias.has_value()) check_rows(*bias, "bias", C);
