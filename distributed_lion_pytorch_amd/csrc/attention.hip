@@ -20,6 +20,8 @@
 // Dropout: keep(q, key) is a stateless hash of (seed, b*H+h, q, key) with
 // 16-bit resolution, so forward and both backward kernels regenerate the
 // identical mask in any register layout.
+#include <cstdlib>
+
 #include "common.h"
 #include "attention.h"
 
@@ -40,12 +42,27 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   return x;
 }
 // 32 random bits shared by keys (2i, 2i+1) of query q; key & 1 picks the half
+// (low 16 bits: even key).  Keep tests run in the high half so the low half
+// needs one shift and the high half none: with thr_hi = thresh16 << 16,
+//   keep(even) = (hash << 16) >= thr_hi,  keep(odd) = hash >= thr_hi.
 __device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint32_t bh, uint32_t q, uint32_t key) {
   return lowbias32(seed ^ (bh * 0x9E3779B9u) ^ (q * 0x85EBCA6Bu) ^ ((key >> 1) * 0xC2B2AE35u));
 }
-__device__ __forceinline__ bool drop_keep(uint32_t hash, uint32_t key, uint32_t thresh16) {
-  return ((hash >> ((key & 1u) * 16u)) & 0xffffu) >= thresh16;
+
+// x op x(lane ^ 32) via v_permlane32_swap (guide T12): no LDS round trip,
+// and max / sum are symmetric so the swapped pair needs no lane select
+__device__ __forceinline__ float xmax32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float a = __uint_as_float(r[0]), b = __uint_as_float(r[1]);
+  return a > b ? a : b;
 }
+__device__ __forceinline__ float xsum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// forward online softmax: rescale O only when a row max grew by more than this (log2 units)
+constexpr float kDeferLog2 = 8.f;
 
 __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -123,9 +140,11 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const __bf16* kbase = a.k + b * a.k_sb + hk * a.k_sh + 8 * hf;
   const __bf16* vtb = a.vt + static_cast<int64_t>(b * a.Hkv + hk) * D * a.ldt + 4 * hf;
 
-  // register double-buffering: the K / V^T fragments of tile kt+1 are in
-  // flight while tile kt is computed (the loop is latency-bound otherwise)
-  bf16x8 kc[D / 16], vc[2][D / 32];
+  // register double-buffering with two NAMED fragment sets (A, B) and a 2x
+  // unrolled loop: tile kt+1 loads into one set while tile kt computes from the
+  // other -- no per-iteration register copies (a runtime-indexed or copied
+  // buffer costs ~64 v_mov per tile)
+  bf16x8 ka[D / 16], va[2][D / 32], kb_[D / 16], vb[2][D / 32];
   auto load_kv = [&](int kt, bf16x8(&kf)[D / 16], bf16x8(&vf)[2][D / 32]) {
     const __bf16* kp = kbase + static_cast<int64_t>(kt * 32 + r) * a.k_st;
 #pragma unroll
@@ -136,49 +155,53 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
       for (int t = 0; t < D / 32; ++t)
         vf[s2][t] = ld4x2(vtb + static_cast<int64_t>(32 * t + r) * a.ldt + kt * 32 + 16 * s2);
   };
-  load_kv(0, kc, vc);
-
-  for (int kt = 0; kt <= qtile; ++kt) {
+  const uint32_t hbase = a.seed ^ (static_cast<uint32_t>(bh) * 0x9E3779B9u) ^ (static_cast<uint32_t>(q) * 0x85EBCA6Bu);
+  const uint32_t thr_hi = a.thresh16 << 16;
+  auto tile = [&](int kt, const bf16x8(&kc)[D / 16], const bf16x8(&vc)[2][D / 32]) {
     const int kb = kt * 32;
-    bf16x8 kn[D / 16], vn[2][D / 32];
-    if (kt < qtile) load_kv(kt + 1, kn, vn);
     f32x16 s = zero16();
 #pragma unroll
     for (int ks = 0; ks < D / 16; ++ks) s = mfma32(kc[ks], qf[ks], s);
-    float mx = m;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) s[reg] *= a.scale_log2;
     if (kt == qtile) {  // causal mask only on the diagonal tile (wave-uniform branch)
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg)
         if (kb + acc_row(reg, hf) > q) s[reg] = -INFINITY;
     }
+    // row max on the raw scores (scale > 0); the scale is folded into the
+    // exponent's FMA below instead of a separate multiply pass
+    float tmax = s[0];
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) mx = fmaxf(mx, s[reg]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float alpha = __builtin_amdgcn_exp2f(m - mx);
+    for (int reg = 1; reg < 16; ++reg) tmax = fmaxf(tmax, s[reg]);
+    tmax = xmax32(tmax) * a.scale_log2;
+    // deferred rescale (guide T13): keep the running max while no row of the
+    // wave grew by more than kDeferLog2 -- P stays <= 2^kDeferLog2, exact in
+    // fp32 l / O, and the O-wide rescale pass is skipped on most tiles
+    float alpha = 1.f;
+    if (!__all(tmax - m <= kDeferLog2)) {
+      const float mn = fmaxf(m, tmax);
+      alpha = __builtin_amdgcn_exp2f(m - mn);
+      m = mn;
+#pragma unroll
+      for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[t][i] *= alpha;
+    }
     float rs = 0.f;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      const float p = __builtin_amdgcn_exp2f(s[reg] - mx);
+      const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -m));
       rs += p;
       s[reg] = p;
     }
-    rs += __shfl_xor(rs, 32);
-    l = l * alpha + rs;
-    m = mx;
-#pragma unroll
-    for (int t = 0; t < D / 32; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) oacc[t][i] *= alpha;
+    l = l * alpha + xsum32(rs);
     if constexpr (DROP) {  // 1/(1-p) is applied once to O at the end
-      const uint32_t hbase = a.seed ^ (static_cast<uint32_t>(bh) * 0x9E3779B9u) ^ (static_cast<uint32_t>(q) * 0x85EBCA6Bu);
 #pragma unroll
       for (int reg = 0; reg < 16; reg += 2) {  // regs (2i, 2i+1) hold keys (2j, 2j+1)
         const uint32_t key = kb + acc_row(reg, hf);
         const uint32_t hsh = lowbias32(hbase ^ ((key >> 1) * 0xC2B2AE35u));
-        if ((hsh & 0xffffu) < a.thresh16) s[reg] = 0.f;
-        if ((hsh >> 16) < a.thresh16) s[reg + 1] = 0.f;
+        // 16-bit halves compared in the high half: (h & 0xffff) < t <=> (h << 16) < (t << 16)
+        if ((hsh << 16) < thr_hi) s[reg] = 0.f;
+        if (hsh < thr_hi) s[reg + 1] = 0.f;
       }
     }
 #pragma unroll
@@ -187,15 +210,16 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int t = 0; t < D / 32; ++t) oacc[t] = mfma32(vc[s2][t], pf, oacc[t]);
     }
-    if (kt < qtile) {
-#pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) kc[ks] = kn[ks];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int t = 0; t < D / 32; ++t) vc[s2][t] = vn[s2][t];
-    }
+  };
+  load_kv(0, ka, va);
+  int kt = 0;
+  for (; kt < qtile; kt += 2) {  // pairs (kt, kt+1), both <= qtile
+    load_kv(kt + 1, kb_, vb);
+    tile(kt, ka, va);
+    if (kt + 2 <= qtile) load_kv(kt + 2, ka, va);
+    tile(kt + 1, kb_, vb);
   }
+  if (kt == qtile) tile(kt, ka, va);  // odd tile count: the last tile sits in set A
   const float inv_l = (DROP ? a.inv_keep : 1.f) / l;
   __bf16* op = a.out + b * a.o_sb + static_cast<int64_t>(q) * a.o_st + h * a.o_sh;
 #pragma unroll
@@ -206,6 +230,153 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) w[i] = static_cast<__bf16>(oacc[t][4 * g + i] * inv_l);
       *reinterpret_cast<bf16x4*>(op + 32 * t + 8 * g + 4 * hf) = w;
+    }
+  if (hf == 0) a.lse[static_cast<int64_t>(bh) * a.T + q] = m + log2f(l);
+}
+
+// ------------------------------------------------- forward, LDS-shared K / V
+// Same math as attn_fwd_kernel, but the 4 waves of a block own 4 consecutive
+// query tiles of ONE head and share every K / V^T tile through LDS: one
+// cooperative 16-byte load per thread per operand instead of 4 private copies
+// per wave (the private-copy kernel streams ~1 GB of L2/MALL traffic per
+// GPT-2 layer and is cache-bandwidth bound).  Global loads for tile kt+1 are
+// issued before tile kt's math and written to the other LDS buffer after it
+// (guide T14).  Waves whose causal range ended idle through the block's
+// remaining tiles (the last <= 3) but keep the barriers.
+constexpr int kKPad = 8;   // K tile rows: 64 + 8 bf16 (144 B) -- breaks the 128-B bank period
+constexpr int kVPad = 8;   // V^T tile rows: 32 + 8 bf16 (80 B)
+
+template <int D, bool DROP>
+__global__ void __launch_bounds__(256) attn_fwd_lds_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) __bf16 ks_[2][32][D + kKPad];
+  __shared__ __attribute__((aligned(16))) __bf16 vs_[2][D][32 + kVPad];
+  const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5, w = threadIdx.x >> 6;
+  const int ntiles = a.T >> 5, ngroups = (ntiles + 3) >> 2, nbh = a.B * a.H;
+  // heads fastest, heavy (late) query groups first
+  const int bh = static_cast<int>(blockIdx.x % nbh);
+  const int grp = ngroups - 1 - static_cast<int>(blockIdx.x / nbh);
+  const int qtile = grp * 4 + w;
+  const int last = min(grp * 4 + 3, ntiles - 1);  // block-uniform loop bound
+  const bool active = qtile < ntiles;
+  const int b = bh / a.H, h = bh % a.H, hk = h / (a.H / a.Hkv);
+  const int q = qtile * 32 + r;
+
+  bf16x8 qf[D / 16];
+  if (active) {
+    const __bf16* qp = a.q + b * a.q_sb + static_cast<int64_t>(q) * a.q_st + h * a.q_sh + 8 * hf;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) qf[s] = ld8(qp + 16 * s);
+  }
+  f32x16 oacc[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) oacc[t] = zero16();
+  float m = -INFINITY, l = 0.f;
+
+  // cooperative tile load: K [32 keys][D] and V^T [D][32 keys], 16 B per thread-chunk
+  constexpr int KCH = 32 * D / 8, VCH = D * 32 / 8;  // 16-byte chunks per tile
+  constexpr int KPT = (KCH + 255) / 256, VPT = (VCH + 255) / 256;
+  const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
+  const __bf16* vg = a.vt + static_cast<int64_t>(b * a.Hkv + hk) * D * a.ldt;
+  uint4 kreg[KPT], vreg[VPT];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c / (D / 8), col = (c % (D / 8)) * 8;
+      if (c < KCH) kreg[i] = *reinterpret_cast<const uint4*>(kg + static_cast<int64_t>(kt * 32 + row) * a.k_st + col);
+    }
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c / 4, col = (c % 4) * 8;
+      if (c < VCH) vreg[i] = *reinterpret_cast<const uint4*>(vg + static_cast<int64_t>(row) * a.ldt + kt * 32 + col);
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c / (D / 8), col = (c % (D / 8)) * 8;
+      if (c < KCH) *reinterpret_cast<uint4*>(&ks_[buf][row][col]) = kreg[i];
+    }
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c / 4, col = (c % 4) * 8;
+      if (c < VCH) *reinterpret_cast<uint4*>(&vs_[buf][row][col]) = vreg[i];
+    }
+  };
+
+  const uint32_t hbase = a.seed ^ (static_cast<uint32_t>(bh) * 0x9E3779B9u) ^ (static_cast<uint32_t>(q) * 0x85EBCA6Bu);
+  const uint32_t thr_hi = a.thresh16 << 16;
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int kt = 0; kt <= last; ++kt) {
+    const int buf = kt & 1;
+    if (kt < last) gload(kt + 1);
+    if (active && kt <= qtile) {  // wave-uniform
+      const int kb = kt * 32;
+      f32x16 s = zero16();
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) s = mfma32(*reinterpret_cast<const bf16x8*>(&ks_[buf][r][16 * ks + 8 * hf]),
+                                                     qf[ks], s);
+      if (kt == qtile) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+          if (kb + acc_row(reg, hf) > q) s[reg] = -INFINITY;
+      }
+      float tmax = s[0];
+#pragma unroll
+      for (int reg = 1; reg < 16; ++reg) tmax = fmaxf(tmax, s[reg]);
+      tmax = xmax32(tmax) * a.scale_log2;
+      float alpha = 1.f;
+      if (!__all(tmax - m <= kDeferLog2)) {
+        const float mn = fmaxf(m, tmax);
+        alpha = __builtin_amdgcn_exp2f(m - mn);
+        m = mn;
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) oacc[t][i] *= alpha;
+      }
+      float rs = 0.f;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -m));
+        rs += p;
+        s[reg] = p;
+      }
+      l = l * alpha + xsum32(rs);
+      if constexpr (DROP) {
+#pragma unroll
+        for (int reg = 0; reg < 16; reg += 2) {
+          const uint32_t key = kb + acc_row(reg, hf);
+          const uint32_t hsh = lowbias32(hbase ^ ((key >> 1) * 0xC2B2AE35u));
+          if ((hsh << 16) < thr_hi) s[reg] = 0.f;
+          if (hsh < thr_hi) s[reg + 1] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pf = acc_frag(s, s2);
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) {
+          const __bf16* vp = &vs_[buf][32 * t + r][16 * s2 + 4 * hf];
+          oacc[t] = mfma32(ld4x2(vp), pf, oacc[t]);
+        }
+      }
+    }
+    if (kt < last) swrite(buf ^ 1);
+    __syncthreads();
+  }
+  if (!active) return;
+  const float inv_l = (DROP ? a.inv_keep : 1.f) / l;
+  __bf16* op = a.out + b * a.o_sb + static_cast<int64_t>(q) * a.o_st + h * a.o_sh;
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 wv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) wv[i] = static_cast<__bf16>(oacc[t][4 * g + i] * inv_l);
+      *reinterpret_cast<bf16x4*>(op + 32 * t + 8 * g + 4 * hf) = wv;
     }
   if (hf == 0) a.lse[static_cast<int64_t>(bh) * a.T + q] = m + log2f(l);
 }
@@ -229,6 +400,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   }
   const float lse2 = a.lse[static_cast<int64_t>(bh) * a.T + q];
   const float dlt = a.delta[static_cast<int64_t>(bh) * a.T + q];
+  const uint32_t thr_hi = a.thresh16 << 16;
   f32x16 dq[D / 32];
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) dq[t] = zero16();
@@ -237,7 +409,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   const __bf16* ktb = a.kt + static_cast<int64_t>(b * a.Hkv + hk) * D * a.ldt + 4 * hf;
 
   // K / V rows and K^T fragments of tile kt+1 are prefetched during tile kt
-  bf16x8 kc[D / 16], vc[D / 16], tc[2][D / 32];
+  // into the other of two named fragment sets (2x unrolled, no copies)
+  bf16x8 ka[D / 16], va[D / 16], ta[2][D / 32], kb2[D / 16], vb2[D / 16], tb2[2][D / 32];
   auto load_kv = [&](int kt, bf16x8(&kf)[D / 16], bf16x8(&vf)[D / 16], bf16x8(&tf)[2][D / 32]) {
     const __bf16* kp = kbase + static_cast<int64_t>(kt * 32 + r) * a.k_st;
     const __bf16* vp = vbase + static_cast<int64_t>(kt * 32 + r) * a.v_st;
@@ -252,11 +425,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
       for (int t = 0; t < D / 32; ++t)
         tf[s2][t] = ld4x2(ktb + static_cast<int64_t>(32 * t + r) * a.ldt + kt * 32 + 16 * s2);
   };
-  load_kv(0, kc, vc, tc);
-  for (int kt = 0; kt <= qtile; ++kt) {
+  const uint32_t hq = a.seed ^ (static_cast<uint32_t>(bh) * 0x9E3779B9u) ^ (static_cast<uint32_t>(q) * 0x85EBCA6Bu);
+  auto tile = [&](int kt, const bf16x8(&kc)[D / 16], const bf16x8(&vc)[D / 16], const bf16x8(&tc)[2][D / 32]) {
     const int kb = kt * 32;
-    bf16x8 kn[D / 16], vn[D / 16], tn[2][D / 32];
-    if (kt < qtile) load_kv(kt + 1, kn, vn, tn);
     f32x16 s = zero16(), dp = zero16();
 #pragma unroll
     for (int ks = 0; ks < D / 16; ++ks) {
@@ -265,15 +436,15 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
     }
 #pragma unroll
     for (int reg = 0; reg < 16; reg += 2) {
-      const int key = kb + acc_row(reg, hf);
+      const int key = kb + acc_row(reg, hf);  // even: regs (reg, reg+1) = keys (key, key+1)
       uint32_t hsh = 0;
-      if constexpr (DROP) hsh = drop_hash(a.seed, bh, q, key);
+      if constexpr (DROP) hsh = lowbias32(hq ^ ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u));
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int kk = key + e;
-        float p = (kt == qtile && kk > q) ? 0.f : __builtin_amdgcn_exp2f(s[reg + e] * a.scale_log2 - lse2);
+        float p = (kt == qtile && kk > q) ? 0.f : __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg + e], a.scale_log2, -lse2));
         float dpv = dp[reg + e];
-        if constexpr (DROP) dpv = drop_keep(hsh, kk, a.thresh16) ? dpv * a.inv_keep : 0.f;
+        if constexpr (DROP) dpv = ((e == 0 ? hsh << 16 : hsh) >= thr_hi) ? dpv * a.inv_keep : 0.f;
         s[reg + e] = p * (dpv - dlt);  // dS^T
       }
     }
@@ -283,18 +454,16 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
       for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tc[s2][t], dq[t]);
     }
-    if (kt < qtile) {
-#pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) {
-        kc[ks] = kn[ks];
-        vc[ks] = vn[ks];
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int t = 0; t < D / 32; ++t) tc[s2][t] = tn[s2][t];
-    }
+  };
+  load_kv(0, ka, va, ta);
+  int kt = 0;
+  for (; kt < qtile; kt += 2) {
+    load_kv(kt + 1, kb2, vb2, tb2);
+    tile(kt, ka, va, ta);
+    if (kt + 2 <= qtile) load_kv(kt + 2, ka, va, ta);
+    tile(kt + 1, kb2, vb2, tb2);
   }
+  if (kt == qtile) tile(kt, ka, va, ta);
   // dq[t]: rows = q (registers), cols = d (lane)
   __bf16* base = a.dq + b * a.dq_sb + h * a.dq_sh;
 #pragma unroll
@@ -303,6 +472,279 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
     for (int reg = 0; reg < 16; ++reg) {
       const int qq = qtile * 32 + acc_row(reg, hf);
       base[static_cast<int64_t>(qq) * a.dq_st + 32 * t + r] = static_cast<__bf16>(dq[t][reg] * a.scale);
+    }
+}
+
+// ---------------------------------------------- cooperative LDS tile staging
+// A 32-row x D tile (rows at `stride` elements) and a D-row x 32-column tile
+// of a [.., D, T] transposed operand, moved 16 B per thread-chunk by a
+// 256-thread block: global -> registers (issued early) -> LDS (written late).
+template <int D>
+struct RowTile {  // [32][D + kKPad]
+  static constexpr int CH = 32 * D / 8, PT = (CH + 255) / 256;
+  uint4 reg[PT];
+  __device__ __forceinline__ void load(const __bf16* base, int64_t stride) {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c / (D / 8), col = (c % (D / 8)) * 8;
+      if (c < CH) reg[i] = *reinterpret_cast<const uint4*>(base + static_cast<int64_t>(row) * stride + col);
+    }
+  }
+  __device__ __forceinline__ void store(__bf16 (*dst)[D + kKPad]) const {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c / (D / 8), col = (c % (D / 8)) * 8;
+      if (c < CH) *reinterpret_cast<uint4*>(&dst[row][col]) = reg[i];
+    }
+  }
+};
+template <int D>
+struct ColTile {  // [D][32 + kVPad]
+  static constexpr int CH = D * 32 / 8, PT = (CH + 255) / 256;
+  uint4 reg[PT];
+  __device__ __forceinline__ void load(const __bf16* base, int64_t ldt) {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c / 4, col = (c % 4) * 8;
+      if (c < CH) reg[i] = *reinterpret_cast<const uint4*>(base + static_cast<int64_t>(row) * ldt + col);
+    }
+  }
+  __device__ __forceinline__ void store(__bf16 (*dst)[32 + kVPad]) const {
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c / 4, col = (c % 4) * 8;
+      if (c < CH) *reinterpret_cast<uint4*>(&dst[row][col]) = reg[i];
+    }
+  }
+};
+
+// --------------------------------------------------- backward dQ, LDS-shared
+// 4 waves = 4 consecutive query tiles of one head; K, V (rows) and K^T tiles
+// staged once per block per key tile.
+template <int D, bool DROP>
+__global__ void __launch_bounds__(256) attn_bwd_dq_lds_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) __bf16 ks_[2][32][D + kKPad];
+  __shared__ __attribute__((aligned(16))) __bf16 vs_[2][32][D + kKPad];
+  __shared__ __attribute__((aligned(16))) __bf16 ts_[2][D][32 + kVPad];
+  const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5, w = threadIdx.x >> 6;
+  const int ntiles = a.T >> 5, ngroups = (ntiles + 3) >> 2, nbh = a.B * a.H;
+  const int bh = static_cast<int>(blockIdx.x % nbh);
+  const int grp = ngroups - 1 - static_cast<int>(blockIdx.x / nbh);
+  const int qtile = grp * 4 + w;
+  const int last = min(grp * 4 + 3, ntiles - 1);
+  const bool active = qtile < ntiles;
+  const int b = bh / a.H, h = bh % a.H, hk = h / (a.H / a.Hkv);
+  const int q = qtile * 32 + r;
+
+  bf16x8 qf[D / 16], dof[D / 16];
+  float lse2 = 0.f, dlt = 0.f;
+  if (active) {
+    const __bf16* qp = a.q + b * a.q_sb + static_cast<int64_t>(q) * a.q_st + h * a.q_sh + 8 * hf;
+    const __bf16* dop = a.dout + b * a.o_sb + static_cast<int64_t>(q) * a.o_st + h * a.o_sh + 8 * hf;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      qf[s] = ld8(qp + 16 * s);
+      dof[s] = ld8(dop + 16 * s);
+    }
+    lse2 = a.lse[static_cast<int64_t>(bh) * a.T + q];
+    dlt = a.delta[static_cast<int64_t>(bh) * a.T + q];
+  }
+  const uint32_t thr_hi = a.thresh16 << 16;
+  const uint32_t hq = a.seed ^ (static_cast<uint32_t>(bh) * 0x9E3779B9u) ^ (static_cast<uint32_t>(q) * 0x85EBCA6Bu);
+  f32x16 dq[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) dq[t] = zero16();
+  const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
+  const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
+  const __bf16* tg = a.kt + static_cast<int64_t>(b * a.Hkv + hk) * D * a.ldt;
+  RowTile<D> kr, vr;
+  ColTile<D> tr;
+  auto gload = [&](int kt) {
+    kr.load(kg + static_cast<int64_t>(kt * 32) * a.k_st, a.k_st);
+    vr.load(vg + static_cast<int64_t>(kt * 32) * a.v_st, a.v_st);
+    tr.load(tg + kt * 32, a.ldt);
+  };
+  auto swrite = [&](int buf) {
+    kr.store(ks_[buf]);
+    vr.store(vs_[buf]);
+    tr.store(ts_[buf]);
+  };
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int kt = 0; kt <= last; ++kt) {
+    const int buf = kt & 1;
+    if (kt < last) gload(kt + 1);
+    if (active && kt <= qtile) {
+      const int kb = kt * 32;
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        s = mfma32(*reinterpret_cast<const bf16x8*>(&ks_[buf][r][16 * ks + 8 * hf]), qf[ks], s);
+        dp = mfma32(*reinterpret_cast<const bf16x8*>(&vs_[buf][r][16 * ks + 8 * hf]), dof[ks], dp);
+      }
+#pragma unroll
+      for (int reg = 0; reg < 16; reg += 2) {
+        const int key = kb + acc_row(reg, hf);
+        uint32_t hsh = 0;
+        if constexpr (DROP) hsh = lowbias32(hq ^ ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u));
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int kk = key + e;
+          float p = (kt == qtile && kk > q) ? 0.f
+                                            : __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg + e], a.scale_log2, -lse2));
+          float dpv = dp[reg + e];
+          if constexpr (DROP) dpv = ((e == 0 ? hsh << 16 : hsh) >= thr_hi) ? dpv * a.inv_keep : 0.f;
+          s[reg + e] = p * (dpv - dlt);
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 dsf = acc_frag(s, s2);
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, ld4x2(&ts_[buf][32 * t + r][16 * s2 + 4 * hf]), dq[t]);
+      }
+    }
+    if (kt < last) swrite(buf ^ 1);
+    __syncthreads();
+  }
+  if (!active) return;
+  __bf16* base = a.dq + b * a.dq_sb + h * a.dq_sh;
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int qq = qtile * 32 + acc_row(reg, hf);
+      base[static_cast<int64_t>(qq) * a.dq_st + 32 * t + r] = static_cast<__bf16>(dq[t][reg] * a.scale);
+    }
+}
+
+// -------------------------------------------------- backward dKV, LDS-shared
+// 4 waves = 4 consecutive key tiles of one (b, kv-head); every query tile of
+// every head in the GQA group is staged once per block: Q, dO (rows), Q^T,
+// dO^T (columns) and the 32 lse / delta values.
+template <int D, bool DROP>
+__global__ void __launch_bounds__(256) attn_bwd_dkv_lds_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) __bf16 qs_[2][32][D + kKPad];
+  __shared__ __attribute__((aligned(16))) __bf16 ds_[2][32][D + kKPad];
+  __shared__ __attribute__((aligned(16))) __bf16 qts_[2][D][32 + kVPad];
+  __shared__ __attribute__((aligned(16))) __bf16 dts_[2][D][32 + kVPad];
+  __shared__ __attribute__((aligned(16))) float ls_[2][2][32];  // [buf][lse | delta][q]
+  const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5, w = threadIdx.x >> 6;
+  const int ntiles = a.T >> 5, ngroups = (ntiles + 3) >> 2, nbhk = a.B * a.Hkv;
+  // heads fastest; low key groups (most query tiles) first
+  const int bhk = static_cast<int>(blockIdx.x % nbhk);
+  const int grp = static_cast<int>(blockIdx.x / nbhk);
+  const int ktile = grp * 4 + w;
+  const bool active = ktile < ntiles;
+  const int first = grp * 4;  // block's first query tile = its lowest key tile
+  const int b = bhk / a.Hkv, hk = bhk % a.Hkv, group = a.H / a.Hkv;
+  const int kb = ktile * 32, key = kb + r;
+
+  bf16x8 kf[D / 16], vf[D / 16];
+  if (active) {
+    const __bf16* kp = a.k + b * a.k_sb + static_cast<int64_t>(key) * a.k_st + hk * a.k_sh + 8 * hf;
+    const __bf16* vp = a.v + b * a.v_sb + static_cast<int64_t>(key) * a.v_st + hk * a.v_sh + 8 * hf;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      kf[s] = ld8(kp + 16 * s);
+      vf[s] = ld8(vp + 16 * s);
+    }
+  }
+  f32x16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) {
+    dk[t] = zero16();
+    dv[t] = zero16();
+  }
+  const uint32_t thr_hi = a.thresh16 << 16, kshift = (key & 1) ? 0u : 16u;
+  RowTile<D> qr, dr;
+  ColTile<D> qtr, dtr;
+  float lsr = 0.f;  // threads 0..63: lse (0..31) / delta (32..63) of the staged tile
+  const int nq = ntiles - first;  // query tiles per head
+  const int total = group * nq;   // (head, query tile) steps, head-major
+  auto gload = [&](int i) {
+    const int gh = i / nq, qt = first + i % nq;
+    const int h = hk * group + gh, bh = b * a.H + h;
+    const int64_t qrow = static_cast<int64_t>(qt * 32);
+    qr.load(a.q + b * a.q_sb + h * a.q_sh + qrow * a.q_st, a.q_st);
+    dr.load(a.dout + b * a.o_sb + h * a.o_sh + qrow * a.o_st, a.o_st);
+    qtr.load(a.qt + static_cast<int64_t>(bh) * D * a.ldt + qt * 32, a.ldt);
+    dtr.load(a.dot + static_cast<int64_t>(bh) * D * a.ldt + qt * 32, a.ldt);
+    if (threadIdx.x < 64) {
+      const float* src = (threadIdx.x < 32 ? a.lse : a.delta) + static_cast<int64_t>(bh) * a.T + qt * 32;
+      lsr = src[threadIdx.x & 31];
+    }
+  };
+  auto swrite = [&](int buf) {
+    qr.store(qs_[buf]);
+    dr.store(ds_[buf]);
+    qtr.store(qts_[buf]);
+    dtr.store(dts_[buf]);
+    if (threadIdx.x < 64) ls_[buf][threadIdx.x >> 5][threadIdx.x & 31] = lsr;
+  };
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int i = 0; i < total; ++i) {
+    const int buf = i & 1;
+    if (i + 1 < total) gload(i + 1);
+    const int gh = i / nq, qt = first + i % nq;
+    if (active && qt >= ktile) {
+      const int bh = b * a.H + hk * group + gh;
+      const int qb = qt * 32;
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        s = mfma32(*reinterpret_cast<const bf16x8*>(&qs_[buf][r][16 * ks + 8 * hf]), kf[ks], s);
+        dp = mfma32(*reinterpret_cast<const bf16x8*>(&ds_[buf][r][16 * ks + 8 * hf]), vf[ks], dp);
+      }
+      const uint32_t hkey = a.seed ^ (static_cast<uint32_t>(bh) * 0x9E3779B9u) ^
+                            ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u);
+      const uint32_t hq = static_cast<uint32_t>(qb + 4 * hf) * 0x85EBCA6Bu;
+      f32x16 pd;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int row = acc_row(reg, hf), qq = qb + row;
+        const float p = (qt == ktile && key > qq)
+                            ? 0.f
+                            : __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -ls_[buf][0][row]));
+        float dpv = dp[reg];
+        float pdv = p;
+        if constexpr (DROP) {
+          const uint32_t rowc = static_cast<uint32_t>((reg & 3) + 8 * (reg >> 2)) * 0x85EBCA6Bu;
+          const uint32_t hsh = lowbias32(hkey ^ (hq + rowc));
+          const bool kp_ = (hsh << kshift) >= thr_hi;
+          dpv = kp_ ? dpv * a.inv_keep : 0.f;
+          pdv = kp_ ? p * a.inv_keep : 0.f;
+        }
+        pd[reg] = pdv;
+        s[reg] = p * (dpv - ls_[buf][1][row]);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pf = acc_frag(pd, s2);
+        const bf16x8 dsf = acc_frag(s, s2);
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) {
+          dv[t] = mfma32(pf, ld4x2(&dts_[buf][32 * t + r][16 * s2 + 4 * hf]), dv[t]);
+          dk[t] = mfma32(dsf, ld4x2(&qts_[buf][32 * t + r][16 * s2 + 4 * hf]), dk[t]);
+        }
+      }
+    }
+    if (i + 1 < total) swrite(buf ^ 1);
+    __syncthreads();
+  }
+  if (!active) return;
+  __bf16* dkb = a.dk + b * a.dk_sb + hk * a.dk_sh;
+  __bf16* dvb = a.dv + b * a.dk_sb + hk * a.dk_sh;
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int64_t off = static_cast<int64_t>(kb + acc_row(reg, hf)) * a.dk_st + 32 * t + r;
+      dkb[off] = static_cast<__bf16>(dk[t][reg] * a.scale);
+      dvb[off] = static_cast<__bf16>(dv[t][reg]);
     }
 }
 
@@ -316,6 +758,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
   const int group = a.H / a.Hkv;
   const int kb = ktile * 32;
   const int key = kb + r;
+  const uint32_t thr_hi = a.thresh16 << 16, kshift = (key & 1) ? 0u : 16u;
 
   bf16x8 kf[D / 16], vf[D / 16];
   const __bf16* kp = a.k + b * a.k_sb + static_cast<int64_t>(key) * a.k_st + hk * a.k_sh + 8 * hf;
@@ -340,10 +783,14 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
     const __bf16* dotb = a.dot + static_cast<int64_t>(bh) * D * a.ldt + 4 * hf;
     const float* lseb = a.lse + static_cast<int64_t>(bh) * a.T;
     const float* dlb = a.delta + static_cast<int64_t>(bh) * a.T;
-    // Q / dO rows of tile qt+1 are prefetched while tile qt is computed; the
-    // transposed fragments and row statistics of tile qt are issued at the top
-    // of the iteration so their latency hides under the S / dP MFMAs.
-    bf16x8 qc[D / 16], dc[D / 16];
+    // loop-invariant part of drop_hash(seed, bh, q, key) for this lane's key
+    const uint32_t hkey = a.seed ^ (static_cast<uint32_t>(bh) * 0x9E3779B9u) ^
+                          ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u);
+    // Q / dO rows of tile qt+1 are prefetched while tile qt is computed (two
+    // named fragment sets, 2x unrolled); the transposed fragments and row
+    // statistics of tile qt are issued at the top of the tile so their latency
+    // hides under the S / dP MFMAs.
+    bf16x8 qa[D / 16], da[D / 16], qb2[D / 16], db2[D / 16];
     auto load_qd = [&](int qt, bf16x8(&qf)[D / 16], bf16x8(&df)[D / 16]) {
       const __bf16* qp = qbase + static_cast<int64_t>(qt * 32 + r) * a.q_st;
       const __bf16* dop = dobase + static_cast<int64_t>(qt * 32 + r) * a.o_st;
@@ -353,8 +800,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
         df[ks] = ld8(dop + 16 * ks);
       }
     };
-    load_qd(ktile, qc, dc);
-    for (int qt = ktile; qt < (a.T >> 5); ++qt) {
+    auto tile = [&](int qt, const bf16x8(&qc)[D / 16], const bf16x8(&dc)[D / 16]) {
       const int qb = qt * 32;
       float lse4[16], dl4[16];
 #pragma unroll
@@ -373,9 +819,6 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
           qtf[s2][t] = ld4x2(qtb + row);
           dtf[s2][t] = ld4x2(dotb + row);
         }
-      bf16x8 qn[D / 16], dn[D / 16];
-      const bool more = qt + 1 < (a.T >> 5);
-      if (more) load_qd(qt + 1, qn, dn);
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
@@ -383,15 +826,20 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
         dp = mfma32(dc[ks], vf[ks], dp);  // dP = dO V^T
       }
       f32x16 pd;
+      const uint32_t hq = static_cast<uint32_t>(qb + 4 * hf) * 0x85EBCA6Bu;
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         const int qq = qb + acc_row(reg, hf);
-        const float p =
-            (qt == ktile && key > qq) ? 0.f : __builtin_amdgcn_exp2f(s[reg] * a.scale_log2 - lse4[reg]);
+        const float p = (qt == ktile && key > qq)
+                            ? 0.f
+                            : __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -lse4[reg]));
         float dpv = dp[reg];
         float pdv = p;
         if constexpr (DROP) {
-          const bool kp_ = drop_keep(drop_hash(a.seed, bh, qq, key), key, a.thresh16);
+          // one hash per element here (the lane is the key): q * C2 = (qb + 4hf) * C2 + row * C2
+          const uint32_t rowc = static_cast<uint32_t>((reg & 3) + 8 * (reg >> 2)) * 0x85EBCA6Bu;
+          const uint32_t hsh = lowbias32(hkey ^ (hq + rowc));
+          const bool kp_ = (hsh << kshift) >= thr_hi;
           dpv = kp_ ? dpv * a.inv_keep : 0.f;
           pdv = kp_ ? p * a.inv_keep : 0.f;
         }
@@ -408,14 +856,17 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
           dk[t] = mfma32(dsf, qtf[s2][t], dk[t]);  // dK += dS^T Q
         }
       }
-      if (more) {
-#pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          qc[ks] = qn[ks];
-          dc[ks] = dn[ks];
-        }
-      }
+    };
+    const int nq = a.T >> 5;
+    load_qd(ktile, qa, da);
+    int qt = ktile;
+    for (; qt + 1 < nq; qt += 2) {
+      load_qd(qt + 1, qb2, db2);
+      tile(qt, qa, da);
+      if (qt + 2 < nq) load_qd(qt + 2, qa, da);
+      tile(qt + 1, qb2, db2);
     }
+    if (qt < nq) tile(qt, qa, da);
   }
   // dk/dv[t]: rows = key (registers), cols = d (lane)
   __bf16* dkb = a.dk + b * a.dk_sb + hk * a.dk_sh;
@@ -482,8 +933,30 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(AttnArgs a) {
 // grid of tile_map(): ceil(tiles / 4) blocks of 4 waves per head
 static inline int64_t tile_blocks(int64_t nbh, int T) { return nbh * (((T >> 5) + 3) >> 2); }
 
+static int fwd_impl() {
+  static const int v = [] {
+    const char* e = std::getenv("DLION_ATTN_FWD");
+    return e ? std::atoi(e) : 1;  // 1: LDS-shared K/V (default), 0: per-wave private loads
+  }();
+  return v;
+}
+
 hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) {
   const int64_t blocks = tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T);
+  if (fwd_impl() == 1) {
+#define FWD_LDS(DD)                                                                              \
+  if (drop) hipLaunchKernelGGL((attn_fwd_lds_kernel<DD, true>), dim3(blocks), dim3(256), 0, st, a); \
+  else hipLaunchKernelGGL((attn_fwd_lds_kernel<DD, false>), dim3(blocks), dim3(256), 0, st, a);
+    if (D == 64) {
+      FWD_LDS(64)
+    } else if (D == 128) {
+      FWD_LDS(128)
+    } else {
+      return hipErrorInvalidValue;
+    }
+#undef FWD_LDS
+    return hipGetLastError();
+  }
   if (D == 64) {
     if (drop) hipLaunchKernelGGL((attn_fwd_kernel<64, true>), dim3(blocks), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((attn_fwd_kernel<64, false>), dim3(blocks), dim3(256), 0, st, a);
@@ -502,7 +975,15 @@ hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
   const int64_t bkv = tile_blocks(static_cast<int64_t>(a.B) * a.Hkv, a.T);
 #define BWD(DD)                                                                                         \
   hipLaunchKernelGGL((attn_delta_kernel<DD>), dim3((rows + 15) / 16), dim3(256), 0, st, a);             \
-  if (drop) {                                                                                           \
+  if (fwd_impl() == 1) {                                                                                \
+    if (drop) {                                                                                         \
+      hipLaunchKernelGGL((attn_bwd_dkv_lds_kernel<DD, true>), dim3(bkv), dim3(256), 0, st, a);         \
+      hipLaunchKernelGGL((attn_bwd_dq_lds_kernel<DD, true>), dim3(bq), dim3(256), 0, st, a);           \
+    } else {                                                                                            \
+      hipLaunchKernelGGL((attn_bwd_dkv_lds_kernel<DD, false>), dim3(bkv), dim3(256), 0, st, a);        \
+      hipLaunchKernelGGL((attn_bwd_dq_lds_kernel<DD, false>), dim3(bq), dim3(256), 0, st, a);          \
+    }                                                                                                   \
+  } else if (drop) {                                                                                    \
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), dim3(bkv), dim3(256), 0, st, a);               \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, true>), dim3(bq), dim3(256), 0, st, a);                 \
   } else {                                                                                              \

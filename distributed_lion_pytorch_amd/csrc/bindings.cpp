@@ -376,9 +376,25 @@ Tensor sum_partials(const Tensor& part) {
   auto sizes = part.sizes().vec();
   sizes.erase(sizes.begin());
   auto out = at::empty(sizes, part.options().dtype(at::kBFloat16));
-  check_hip(dlion::launch_sum_partials(part.data_ptr<float>(), static_cast<int>(S), n, out.data_ptr(), cur_stream()),
+  check_hip(dlion::launch_sum_partials(part.data_ptr<float>(), static_cast<int>(S), n, out.data_ptr(), false,
+                                       cur_stream()),
             "sum_partials");
   return out;
+}
+
+// out += sum_s part[s] in place (bf16 out, one rounding): gradient accumulation
+// fused into the split-K weight-gradient reduction
+void sum_partials_acc_(const Tensor& part, const Tensor& out) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous(),
+              "dlion: partials must be contiguous fp32 on the GPU");
+  const int64_t S = part.size(0), n = part.numel() / S;
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == n,
+              "dlion: accumulation target must be a contiguous bf16 tensor of the partial row size");
+  TORCH_CHECK(n % 4 == 0, "dlion: partial row length must be a multiple of 4");
+  const c10::DeviceGuard g(part.device());
+  check_hip(dlion::launch_sum_partials(part.data_ptr<float>(), static_cast<int>(S), n, out.data_ptr(), true,
+                                       cur_stream()),
+            "sum_partials_acc_");
 }
 
 // ---------------------------------------------------------------- SwiGLU / RoPE
@@ -442,6 +458,7 @@ TORCH_LIBRARY(dlion, m) {
   m.def("bias_gelu_fwd(Tensor z, Tensor b, bool exact) -> Tensor");
   m.def("bias_gelu_bwd(Tensor dh, Tensor z, Tensor b, bool exact, int parts) -> (Tensor, Tensor)");
   m.def("sum_partials(Tensor part) -> Tensor");
+  m.def("sum_partials_acc_(Tensor part, Tensor(a!) out) -> ()");
   m.def("transpose_btxd(Tensor x) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float p, int seed) -> (Tensor, Tensor)");
   m.def(
@@ -475,6 +492,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("bias_gelu_fwd", &bias_gelu_fwd);
   m.impl("bias_gelu_bwd", &bias_gelu_bwd);
   m.impl("sum_partials", &sum_partials);
+  m.impl("sum_partials_acc_", &sum_partials_acc_);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("rope", &rope);

@@ -100,7 +100,9 @@ __global__ void __launch_bounds__(1024) bias_gelu_bwd_kernel(const uint16_t* __r
   }
 }
 
-// out[i] = bf16(sum_s part[s][i]), 4 elements per thread
+// out[i] = bf16(sum_s part[s][i] (+ out[i] when ACC: gradient accumulation
+// fused into the split-K reduction)), 4 elements per thread
+template <bool ACC>
 __global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restrict__ part, int S, int64_t n,
                                                           uint16_t* __restrict__ out) {
   const int64_t n4 = n / 4;
@@ -110,6 +112,13 @@ __global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restri
     for (int s = 1; s < S; ++s) {
       const float4 v = reinterpret_cast<const float4*>(part + static_cast<int64_t>(s) * n)[i];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    if constexpr (ACC) {
+      const uint2 o = reinterpret_cast<const uint2*>(out)[i];
+      acc.x += bf16_to_f32(o.x & 0xffffu);
+      acc.y += bf16_to_f32(o.x >> 16);
+      acc.z += bf16_to_f32(o.y & 0xffffu);
+      acc.w += bf16_to_f32(o.y >> 16);
     }
     uint2 w;
     w.x = static_cast<uint32_t>(f32_to_bf16(acc.x)) | (static_cast<uint32_t>(f32_to_bf16(acc.y)) << 16);
@@ -219,6 +228,7 @@ __global__ void __launch_bounds__(256) rope_kernel(const uint16_t* __restrict__ 
 // float4 column quads x 32 row lanes; each thread strides the rows by 32 and
 // the 32 row lanes are folded through LDS.  128-byte row segments per load.
 constexpr int kTallQ = 8, kTallR = 32;
+template <bool ACC>
 __global__ void __launch_bounds__(kTallQ * kTallR) sum_partials_tall_kernel(const float* __restrict__ part, int S,
                                                                            int64_t n, uint16_t* __restrict__ out) {
   __shared__ float4 red[kTallR][kTallQ];
@@ -240,6 +250,13 @@ __global__ void __launch_bounds__(kTallQ * kTallR) sum_partials_tall_kernel(cons
     for (int i = 1; i < kTallR; ++i) {
       const float4 v = red[i][q];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    if constexpr (ACC) {
+      const uint2 o = reinterpret_cast<const uint2*>(out)[col4];
+      acc.x += bf16_to_f32(o.x & 0xffffu);
+      acc.y += bf16_to_f32(o.x >> 16);
+      acc.z += bf16_to_f32(o.y & 0xffffu);
+      acc.w += bf16_to_f32(o.y >> 16);
     }
     uint2 w;
     w.x = static_cast<uint32_t>(f32_to_bf16(acc.x)) | (static_cast<uint32_t>(f32_to_bf16(acc.y)) << 16);
@@ -317,19 +334,22 @@ hipError_t launch_rope(const void* x, const void* cos, const void* sin, void* y,
   return hipGetLastError();
 }
 
-hipError_t launch_sum_partials(const float* part, int S, int64_t n, void* out, hipStream_t st) {
+hipError_t launch_sum_partials(const float* part, int S, int64_t n, void* out, bool accumulate, hipStream_t st) {
   if (n % 4 != 0) return hipErrorInvalidValue;
   const int64_t n4 = n / 4;
+  auto O = static_cast<uint16_t*>(out);
   if (S > 64 || n4 < 256 * static_cast<int64_t>(S)) {
     // tall / narrow stack: parallelise over rows too
     const int64_t blocks = (n4 + kTallQ - 1) / kTallQ;
     if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(sum_partials_tall_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kTallQ * kTallR), 0, st,
-                       part, S, n, static_cast<uint16_t*>(out));
+    const dim3 g(static_cast<unsigned>(blocks)), blk(kTallQ * kTallR);
+    if (accumulate) hipLaunchKernelGGL(sum_partials_tall_kernel<true>, g, blk, 0, st, part, S, n, O);
+    else hipLaunchKernelGGL(sum_partials_tall_kernel<false>, g, blk, 0, st, part, S, n, O);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(n / 4, 256)), dim3(256), 0, st, part, S, n,
-                     static_cast<uint16_t*>(out));
+  const dim3 g(grid_for(n / 4, 256)), blk(256);
+  if (accumulate) hipLaunchKernelGGL(sum_partials_kernel<true>, g, blk, 0, st, part, S, n, O);
+  else hipLaunchKernelGGL(sum_partials_kernel<false>, g, blk, 0, st, part, S, n, O);
   return hipGetLastError();
 }
 

@@ -8,12 +8,42 @@ fills 9-36 of the 256 CUs.  Measured on MI355X (tools/bench_gemm.py):
 182-490 TF/s for hipBLASLt's own choice vs 540-840 TF/s when the token axis
 is split S ways into a batched GEMM with fp32 output (``bmm(out_dtype=f32)``),
 summed in fp32 and rounded once.  S is picked so that S x tiles ~ 160.
+
+Gradient-accumulation fusion (``grad_accumulation_fusion``): with gradient
+accumulation every micro-batch's weight gradient would otherwise be written
+to a fresh tensor and then added into ``param.grad`` by autograd's
+AccumulateGrad (one extra read-read-write pass over every weight per
+micro-batch).  With fusion on, the backward deposits the weight gradient
+straight into ``param.grad``: the split-K reduction adds the running gradient
+in the same pass (``sum_partials_acc_``), the unsplit GEMM accumulates with
+beta = 1 (``addmm_``).  The backward then returns no gradient for the weight,
+so this bypasses AccumulateGrad and its hooks -- enable it only in loops
+that own the gradients (the native TrainStep does; DDP gradient hooks would
+not see these weights).
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import torch
+
+_FUSE_ACCUM = {"on": False}
+
+
+@contextlib.contextmanager
+def grad_accumulation_fusion(enabled: bool = True):
+    prev = _FUSE_ACCUM["on"]
+    _FUSE_ACCUM["on"] = bool(enabled)
+    try:
+        yield
+    finally:
+        _FUSE_ACCUM["on"] = prev
+
+
+def _fuse_target(w: torch.Tensor) -> bool:
+    return (_FUSE_ACCUM["on"] and isinstance(w, torch.nn.Parameter) and w.is_cuda
+            and w.dtype == torch.bfloat16 and w.is_contiguous())
 
 
 def split_k_factor(M: int, K: int, N: int) -> int:
@@ -25,6 +55,26 @@ def split_k_factor(M: int, K: int, N: int) -> int:
     while s > 1 and M % s:
         s //= 2
     return s
+
+
+def wgrad_into(a: torch.Tensor, b: torch.Tensor, w: torch.nn.Parameter) -> None:
+    """w.grad (+)= a^T @ b, deposited in place (a [M, K], b [M, N], w [K, N])."""
+    g = w.grad
+    if g is None or not (g.is_contiguous() and g.dtype == w.dtype):
+        fresh = wgrad(a, b)
+        w.grad = fresh if g is None else g + fresh
+        return
+    M, K = a.shape
+    N = b.shape[1]
+    s = split_k_factor(M, K, N)
+    if s > 1 and (K * N) % 4 == 0:
+        from . import hip
+
+        if hip.available():
+            part = torch.bmm(a.view(s, M // s, K).transpose(1, 2), b.view(s, M // s, N), out_dtype=torch.float32)
+            hip.ops().sum_partials_acc_(part, g)
+            return
+    g.addmm_(a.t(), b)
 
 
 def wgrad(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -50,6 +100,8 @@ class _LinearKN(torch.autograd.Function):
     def forward(ctx, x2d, w, b):
         ctx.save_for_backward(x2d, w)
         ctx.has_b = b is not None
+        ctx.fuse = _fuse_target(w)
+        ctx.param = w if ctx.fuse else None
         return torch.addmm(b, x2d, w) if b is not None else x2d @ w
 
     @staticmethod
@@ -57,7 +109,12 @@ class _LinearKN(torch.autograd.Function):
         x2d, w = ctx.saved_tensors
         dy = dy.contiguous()
         dx = dy @ w.t() if ctx.needs_input_grad[0] else None
-        dw = wgrad(x2d, dy) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            if ctx.fuse:
+                wgrad_into(x2d, dy, ctx.param)
+            else:
+                dw = wgrad(x2d, dy)
         db = dy.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db
 
@@ -69,6 +126,8 @@ class _LinearNK(torch.autograd.Function):
     def forward(ctx, x2d, w, b):
         ctx.save_for_backward(x2d, w)
         ctx.has_b = b is not None
+        ctx.fuse = _fuse_target(w)
+        ctx.param = w if ctx.fuse else None
         return torch.nn.functional.linear(x2d, w, b)
 
     @staticmethod
@@ -76,7 +135,12 @@ class _LinearNK(torch.autograd.Function):
         x2d, w = ctx.saved_tensors
         dy = dy.contiguous()
         dx = dy @ w if ctx.needs_input_grad[0] else None
-        dw = wgrad(dy, x2d) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            if ctx.fuse:
+                wgrad_into(dy, x2d, ctx.param)
+            else:
+                dw = wgrad(dy, x2d)
         db = dy.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db
 

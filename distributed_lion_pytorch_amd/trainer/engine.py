@@ -48,7 +48,7 @@ class TrainStep:
     """One optimizer step = ``grad_accum`` micro-batches + clip + Lion step."""
 
     def __init__(self, model, optimizer, grad_accum: int = 1, max_grad_norm: Optional[float] = 1.0,
-                 scheduler=None, loss_fn: Optional[Callable] = None):
+                 scheduler=None, loss_fn: Optional[Callable] = None, fuse_grad_accumulation: Optional[bool] = None):
         self.model = model
         self.optimizer = optimizer
         self.grad_accum = max(1, int(grad_accum))
@@ -56,14 +56,22 @@ class TrainStep:
         self.scheduler = scheduler
         self.loss_fn = loss_fn or (lambda m, b: m(b["input_ids"], labels=b["labels"])["loss"])
         self.params = [p for p in model.parameters() if p.requires_grad]
+        # weight gradients land straight in param.grad (ops/linear.py); off under
+        # DDP, whose reducer relies on AccumulateGrad hooks
+        if fuse_grad_accumulation is None:
+            fuse_grad_accumulation = not isinstance(model, torch.nn.parallel.DistributedDataParallel)
+        self.fuse_grad_accumulation = fuse_grad_accumulation
 
     def __call__(self, micro_batches: Iterable[dict]) -> torch.Tensor:
+        from ..ops.linear import grad_accumulation_fusion
+
         self.model.train()
         total = None
-        for batch in micro_batches:
-            loss = self.loss_fn(self.model, batch) / self.grad_accum
-            loss.backward()
-            total = loss.detach() if total is None else total + loss.detach()
+        with grad_accumulation_fusion(self.fuse_grad_accumulation):
+            for batch in micro_batches:
+                loss = self.loss_fn(self.model, batch) / self.grad_accum
+                loss.backward()
+                total = loss.detach() if total is None else total + loss.detach()
         if self.max_grad_norm is not None and self.max_grad_norm > 0:
             torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm, foreach=True)
         self.optimizer.step()

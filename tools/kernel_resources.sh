@@ -1,7 +1,7 @@
 # Per-kernel VGPR / AGPR / spill / LDS / occupancy of a .hip file for gfx950.
 # Usage: bash tools/kernel_resources.sh <file.hip> [name-filter]
 f=$1; filt=${2:-.}
-/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -I$(dirname $f) -c $f -o /tmp/_kr.o \
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -I$(dirname $f) $EXTRA -c $f -o /tmp/_kr.o \
   -Rpass-analysis=kernel-resource-usage 2>&1 | sed -n 's/.*remark: *//p' | awk -v filt="$filt" '
   /Function Name:/ {name=$3}
   /^ *VGPRs:/ {v=$2}

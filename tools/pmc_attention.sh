@@ -1,22 +1,33 @@
-# PMC counters for the attention fwd kernel (rocprofv3 --pmc, kernel-trace only).
+# PMC counters for the attention kernels (rocprofv3 --pmc with kernel-trace only;
+# one counter group per run).  Summary -> gpurun_out/pmc_attn/summary.txt
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp
-mkdir -p gpurun_out/pmc_attn
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc_attn -o pmc1 \
-  --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
-  -- python3 tools/bench_attention.py > gpurun_out/pmc_attn/log1.txt 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc_attn -o pmc2 \
-  --pmc FETCH_SIZE TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum \
-  -- python3 tools/bench_attention.py > gpurun_out/pmc_attn/log2.txt 2>&1 || exit 1
-python3 - <<'PY'
+rm -rf gpurun_out/pmc_attn; mkdir -p gpurun_out/pmc_attn
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
+           "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS" \
+           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_INST_LEVEL_VMEM"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc_attn -o pmc$i --pmc $grp \
+    -- python3 tools/bench_attention.py > gpurun_out/pmc_attn/log$i.txt 2>&1 || exit 1
+done
+python3 - > gpurun_out/pmc_attn/summary.txt <<'PY'
 import csv, glob, collections
+agg = collections.defaultdict(lambda: collections.defaultdict(float))
+calls = collections.defaultdict(set)
 for f in sorted(glob.glob("gpurun_out/pmc_attn/**/*counter_collection.csv", recursive=True)):
-    agg = collections.defaultdict(lambda: collections.defaultdict(float)); cnt = collections.Counter()
     for row in csv.DictReader(open(f)):
-        k = row["Kernel_Name"][:60]
-        if "attn" not in k and "bwd" not in k: continue
+        k = row["Kernel_Name"]
+        if "dlion::attn" not in k:
+            continue
+        k = k.split("(")[0].replace("void ", "")
         agg[k][row["Counter_Name"]] += float(row["Counter_Value"])
-        cnt[k] += 1
-    print(f)
-    for k, d in agg.items():
-        print(" ", k, {c: f"{v:.3g}" for c, v in d.items()})
+        calls[k].add((f, row.get("Dispatch_Id", "")))
+for k, d in agg.items():
+    n = max(1, len([c for c in calls[k] if "pmc1" in c[0]]))
+    print(k, "dispatches/pass", n)
+    for c in sorted(d):
+        print(f"   {c:28s} {d[c] / n:14.4g}")
+    if d.get("SQ_INSTS_MFMA"):
+        print(f"   VALU/MFMA = {d['SQ_INSTS_VALU'] / d['SQ_INSTS_MFMA']:.1f}")
 PY
+cat gpurun_out/pmc_attn/summary.txt
