@@ -11,10 +11,6 @@ struct AttnArgs {
   const __bf16* v;
   const __bf16* o;
   const __bf16* dout;
-  const __bf16* qt;   // [B][H][D][T]   (bwd dKV)
-  const __bf16* kt;   // [B][Hkv][D][T] (bwd dQ)
-  const __bf16* vt;   // [B][Hkv][D][T] (fwd)
-  const __bf16* dot;  // [B][H][D][T]   (bwd dKV)
   __bf16* out;        // fwd O
   __bf16* dq;
   __bf16* dk;
@@ -33,8 +29,6 @@ struct AttnArgs {
   uint32_t thresh16; // dropout threshold (keep if u16 >= thresh16), 0 = no dropout
   float inv_keep;
   uint32_t seed;
-  int ldt;    // row stride (elements) of the [.., D, T] transposed operands (padded off a power of 2)
-  int order;  // tile_map() ordering (0: heads fastest, 1: head-grouped + XCD remap)
 };
 
 }  // namespace dlion

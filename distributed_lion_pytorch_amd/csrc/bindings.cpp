@@ -146,33 +146,6 @@ void check_bthd(const Tensor& t, const char* name) {
               "dlion attn: ", name, " must be 16-byte aligned");
 }
 
-// Row stride of the transposed [.., D, T] operands: T padded by 32 elements
-// (64 B) so the 32 rows a wave gathers are not a power-of-two apart (a 2 KB
-// stride puts every lane of a fragment load in the same L2 channel).
-int64_t attn_ldt(int64_t T) {
-  static const int64_t pad = [] {
-    const char* e = std::getenv("DLION_ATTN_TPAD");
-    return e ? static_cast<int64_t>(std::atoi(e)) : int64_t{32};
-  }();
-  return T + pad;
-}
-
-Tensor transpose_padded(const Tensor& x) {
-  check_bthd(x, "x");
-  const int64_t B = x.size(0), T = x.size(1), X = x.size(2), D = x.size(3);
-  TORCH_CHECK(T % 64 == 0 && (D == 64 || D == 128), "dlion attn: need T % 64 == 0 and D in {64, 128}");
-  const int64_t ldt = attn_ldt(T);
-  auto out = at::empty({B, X, D, ldt}, x.options());
-  const c10::DeviceGuard g(x.device());
-  check_hip(dlion::launch_transpose_btxd(x.data_ptr(), x.stride(0), x.stride(1), x.stride(2), out.data_ptr(),
-                                         static_cast<int>(B), static_cast<int>(T), static_cast<int>(X),
-                                         static_cast<int>(D), static_cast<int>(ldt), cur_stream()),
-            "transpose_btxd");
-  return out;
-}
-
-Tensor transpose_btxd(const Tensor& x) { return transpose_padded(x).narrow(3, 0, x.size(1)); }
-
 dlion::AttnArgs attn_args(const Tensor& q, const Tensor& k, const Tensor& v, double p, int64_t seed) {
   check_bthd(q, "q");
   check_bthd(k, "k");
@@ -197,37 +170,14 @@ dlion::AttnArgs attn_args(const Tensor& q, const Tensor& k, const Tensor& v, dou
   a.thresh16 = th;
   a.inv_keep = static_cast<float>(65536.0 / (65536.0 - th));
   a.seed = static_cast<uint32_t>(seed);
-  static const int order = [] {
-    const char* e = std::getenv("DLION_ATTN_ORDER");
-    return e ? std::atoi(e) : 0;
-  }();
-  a.order = order;
-  a.ldt = static_cast<int>(attn_ldt(T));
   return a;
 }
 
-bool attn_repack() {
-  static const bool on = [] {
-    const char* e = std::getenv("DLION_ATTN_REPACK");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return on;
-}
-
-// [B,T,X,D] strided view -> head-major [B,X,T,D] copy viewed back as [B,T,X,D]
-// (rows of one head become contiguous 2*D-byte lines for the fragment gathers)
-Tensor head_major(const Tensor& x) { return x.transpose(1, 2).contiguous().transpose(1, 2); }
-
-std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v, double p, int64_t seed) {
-  const bool rp = attn_repack();
-  const Tensor q = q_in;
-  const Tensor k = rp ? head_major(k_in) : k_in;
+std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, double p, int64_t seed) {
   auto a = attn_args(q, k, v, p, seed);
   const c10::DeviceGuard g(q.device());
-  const Tensor vt = transpose_padded(v);
   auto out = at::empty({q.size(0), q.size(1), q.size(2), q.size(3)}, q.options());
   auto lse = at::empty({q.size(0), q.size(2), q.size(1)}, q.options().dtype(at::kFloat));
-  a.vt = static_cast<const __bf16*>(vt.data_ptr());
   a.out = static_cast<__bf16*>(out.data_ptr());
   a.o_sb = out.stride(0); a.o_st = out.stride(1); a.o_sh = out.stride(2);
   a.lse = lse.data_ptr<float>();
@@ -235,12 +185,8 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q_in, const Tensor& k_in, cons
   return {out, lse};
 }
 
-void attn_bwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, const Tensor& out, const Tensor& dout,
+void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& out, const Tensor& dout,
               const Tensor& lse, double p, int64_t seed, const Tensor& dq, const Tensor& dk, const Tensor& dv) {
-  const bool rp = attn_repack();
-  const Tensor q = rp ? head_major(q_in) : q_in;
-  const Tensor k = rp ? head_major(k_in) : k_in;
-  const Tensor v = rp ? head_major(v_in) : v_in;
   auto a = attn_args(q, k, v, p, seed);
   check_bthd(out, "out");
   check_bthd(dout, "dout");
@@ -251,14 +197,10 @@ void attn_bwd(const Tensor& q_in, const Tensor& k_in, const Tensor& v_in, const 
   TORCH_CHECK(dk.strides() == dv.strides(), "dlion attn: dk and dv must share strides");
   TORCH_CHECK(lse.is_contiguous() && lse.scalar_type() == at::kFloat, "dlion attn: lse must be contiguous fp32");
   const c10::DeviceGuard g(q.device());
-  const Tensor qt = transpose_padded(q), kt = transpose_padded(k), dot = transpose_padded(dout);
   auto delta = at::empty_like(lse);
   a.o = static_cast<const __bf16*>(out.data_ptr());
   a.dout = static_cast<const __bf16*>(dout.data_ptr());
   a.o_sb = out.stride(0); a.o_st = out.stride(1); a.o_sh = out.stride(2);
-  a.qt = static_cast<const __bf16*>(qt.data_ptr());
-  a.kt = static_cast<const __bf16*>(kt.data_ptr());
-  a.dot = static_cast<const __bf16*>(dot.data_ptr());
   a.lse = lse.data_ptr<float>();
   a.delta = delta.data_ptr<float>();
   a.dq = static_cast<__bf16*>(dq.data_ptr());
@@ -459,7 +401,6 @@ TORCH_LIBRARY(dlion, m) {
   m.def("bias_gelu_bwd(Tensor dh, Tensor z, Tensor b, bool exact, int parts) -> (Tensor, Tensor)");
   m.def("sum_partials(Tensor part) -> Tensor");
   m.def("sum_partials_acc_(Tensor part, Tensor(a!) out) -> ()");
-  m.def("transpose_btxd(Tensor x) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float p, int seed) -> (Tensor, Tensor)");
   m.def(
       "attn_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout, Tensor lse, float p, int seed,"
@@ -484,7 +425,6 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("lion_vote_apply", &lion_vote_apply);
   m.impl("vote_reduce", &vote_reduce);
   m.impl("softmax_xent_", &softmax_xent_);
-  m.impl("transpose_btxd", &transpose_btxd);
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);
   m.impl("add_norm_fwd", &add_norm_fwd);

@@ -23,8 +23,6 @@ hipError_t launch_vote_reduce(const uint8_t* recv, int64_t nbytes, const uint8_t
 // ---- flash attention (attention.hip)
 hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st);
 hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st);
-hipError_t launch_transpose_btxd(const void* in, int64_t sb, int64_t st, int64_t sx, void* out, int B, int T, int X,
-                                 int D, int ldt, hipStream_t stream);
 
 // ---- fused residual + dropout + LayerNorm/RMSNorm (norm_kernels.hip)
 // backward: `parts` blocks (4 rows of C <= 1024, or one wide row, per block

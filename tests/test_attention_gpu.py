@@ -59,11 +59,3 @@ def test_packed_qkv_attention_matches_reference(p, cuda):
     ref.backward(dout.float())
     _close(out, ref, 2e-2)
     _close(a.grad, r.grad, 3e-2)
-
-
-@pytest.mark.gpu
-def test_transpose_kernel(cuda):
-    hip.require()
-    x = torch.randn(2, 128, 3, 5, 64, device=cuda, dtype=torch.bfloat16)[:, :, 1]
-    xt = hip.ops().transpose_btxd(x)
-    assert torch.equal(xt, x.permute(0, 2, 3, 1).contiguous())
