@@ -47,11 +47,22 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-// drop hash: 32 random bits shared by keys (2i, 2i+1) of query q,
-//   lowbias32(seed ^ bh*0x9E3779B9 ^ q*0x85EBCA6B ^ (key>>1)*0xC2B2AE35),
+// drop hash: 32 random bits shared by keys (2i, 2i+1) of query q, in two
+// stages so the per-element cost is one 32-bit multiply (v_mul_lo_u32 is a
+// slow multi-cycle op; the first version's two per pair cost ~20% of the
+// backward):
+//   arow(bh, q)  = lowbias32(seed ^ bh*0x9E3779B9 ^ q*0x85EBCA6B)   (per row)
+//   hash(q, key) = mix1(arow ^ (key>>1)*0xC2B2AE35),  mix1(x) = y ^ (y >> 16), y = x*0x7FEB352D
 // low 16 bits for the even key.  Keep tests run in the high half (one shift
 // for the low half, none for the high one): with thr_hi = thresh16 << 16,
 //   keep(even) = (hash << 16) >= thr_hi,  keep(odd) = hash >= thr_hi.
+__device__ __forceinline__ uint32_t drop_row(uint32_t seed, uint32_t bh, uint32_t q) {
+  return lowbias32(seed ^ (bh * 0x9E3779B9u) ^ (q * 0x85EBCA6Bu));
+}
+__device__ __forceinline__ uint32_t mix1(uint32_t x) {
+  x *= 0x7feb352du;
+  return x ^ (x >> 16);
+}
 
 // x op x(lane ^ 32) via v_permlane32_swap (guide T12): no LDS round trip,
 // and max / sum are symmetric so the swapped pair needs no lane select
@@ -181,7 +192,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
   const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
   RowTile<D> kr, vr;
-  const uint32_t hbase = a.seed ^ (static_cast<uint32_t>(bh) * 0x9E3779B9u) ^ (static_cast<uint32_t>(q) * 0x85EBCA6Bu);
+  const uint32_t arow = drop_row(a.seed, bh, q);
   const uint32_t thr_hi = a.thresh16 << 16;
   kr.load(kg, a.k_st);
   vr.load(vg, a.v_st);
@@ -235,7 +246,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int reg = 0; reg < 16; reg += 2) {  // regs (2i, 2i+1) hold keys (2j, 2j+1)
           const uint32_t key = kb + acc_row(reg, hf);
-          const uint32_t hsh = lowbias32(hbase ^ ((key >> 1) * 0xC2B2AE35u));
+          const uint32_t hsh = mix1(arow ^ ((key >> 1) * 0xC2B2AE35u));
           if ((hsh << 16) < thr_hi) s[reg] = 0.f;
           if (hsh < thr_hi) s[reg + 1] = 0.f;
         }
@@ -293,7 +304,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
     dlt = a.delta[static_cast<int64_t>(bh) * a.T + q];
   }
   const uint32_t thr_hi = a.thresh16 << 16;
-  const uint32_t hq = a.seed ^ (static_cast<uint32_t>(bh) * 0x9E3779B9u) ^ (static_cast<uint32_t>(q) * 0x85EBCA6Bu);
+  const uint32_t arow = drop_row(a.seed, bh, q);
   f32x16 dq[D / 32];
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) dq[t] = zero16();
@@ -323,7 +334,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
       for (int reg = 0; reg < 16; reg += 2) {
         const int key = kb + acc_row(reg, hf);  // even: regs (reg, reg+1) = keys (key, key+1)
         uint32_t hsh = 0;
-        if constexpr (DROP) hsh = lowbias32(hq ^ ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u));
+        if constexpr (DROP) hsh = mix1(arow ^ ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u));
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const int kk = key + e;
@@ -368,7 +379,7 @@ template <int D, bool DROP>
 __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) LdsTile<D> qs_[2];
   __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[2];
-  __shared__ __attribute__((aligned(16))) float ls_[2][2][32];  // [buf][lse | delta][row]
+  __shared__ __attribute__((aligned(16))) float ls_[2][3][32];  // [buf][lse | delta | drop row key][row]
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5, w = threadIdx.x >> 6;
   const int ntiles = a.T >> 5, nbhk = a.B * a.Hkv;
   const int bhk = static_cast<int>(blockIdx.x % nbhk);
@@ -397,7 +408,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
   }
   const uint32_t thr_hi = a.thresh16 << 16, kshift = (key & 1) ? 0u : 16u;
   RowTile<D> qr, dr;
-  float lsr = 0.f;                 // threads 0..63 stage lse (0..31) / delta (32..63)
+  float lsr = 0.f;                 // threads 0..95 stage lse (0..31) / delta (32..63) / drop_row (64..95)
   const int nq = ntiles - first;   // query tiles per head
   const int total = group * nq;    // (head, query tile) steps, head-major
   auto gload = [&](int i) {
@@ -409,22 +420,24 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
     if (threadIdx.x < 64) {
       const float* src = (threadIdx.x < 32 ? a.lse : a.delta) + static_cast<int64_t>(bh) * a.T + qt * 32;
       lsr = src[threadIdx.x & 31];
+    } else if (DROP && threadIdx.x < 96) {
+      lsr = __uint_as_float(drop_row(a.seed, bh, qt * 32 + (threadIdx.x & 31)));
     }
   };
   auto swrite = [&](int buf) {
     qr.store(qs_[buf]);
     dr.store(ds_[buf]);
-    if (threadIdx.x < 64) ls_[buf][threadIdx.x >> 5][threadIdx.x & 31] = lsr;
+    if (threadIdx.x < (DROP ? 96 : 64)) ls_[buf][threadIdx.x >> 5][threadIdx.x & 31] = lsr;
   };
+  const uint32_t kmix = (static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u;
   gload(0);
   swrite(0);
   __syncthreads();
   for (int i = 0; i < total; ++i) {
     const int buf = i & 1;
     if (i + 1 < total) gload(i + 1);
-    const int gh = i / nq, qt = first + i % nq;
+    const int qt = first + i % nq;
     if (active && qt >= ktile) {  // wave-uniform
-      const int bh = b * a.H + hk * group + gh;
       const int qb = qt * 32;
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
@@ -432,29 +445,37 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
         s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), kf[ks], s);   // S  = Q K^T : rows q, cols key
         dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), vf[ks], dp);  // dP = dO V^T
       }
-      // loop-invariant parts of the drop hash: the lane is the key here, so
-      // one hash per element; q * C = (qb + 4hf) * C + row * C
-      const uint32_t hkey = a.seed ^ (static_cast<uint32_t>(bh) * 0x9E3779B9u) ^
-                            ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u);
-      const uint32_t hq = static_cast<uint32_t>(qb + 4 * hf) * 0x85EBCA6Bu;
+      // row statistics of the lane's 16 query rows: rows (reg&3) + 8(reg>>2) + 4hf
+      // come in 4 runs of 4 consecutive rows -> 16-byte LDS reads (broadcast)
+      float lse_r[16], dl_r[16];
+      uint32_t ar_r[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 lv = *reinterpret_cast<const float4*>(&ls_[buf][0][8 * g + 4 * hf]);
+        const float4 dv4 = *reinterpret_cast<const float4*>(&ls_[buf][1][8 * g + 4 * hf]);
+        lse_r[4 * g] = lv.x; lse_r[4 * g + 1] = lv.y; lse_r[4 * g + 2] = lv.z; lse_r[4 * g + 3] = lv.w;
+        dl_r[4 * g] = dv4.x; dl_r[4 * g + 1] = dv4.y; dl_r[4 * g + 2] = dv4.z; dl_r[4 * g + 3] = dv4.w;
+        if constexpr (DROP) {
+          const uint4 av = *reinterpret_cast<const uint4*>(&ls_[buf][2][8 * g + 4 * hf]);
+          ar_r[4 * g] = av.x; ar_r[4 * g + 1] = av.y; ar_r[4 * g + 2] = av.z; ar_r[4 * g + 3] = av.w;
+        }
+      }
       f32x16 pd;
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
-        const int row = acc_row(reg, hf), qq = qb + row;
+        const int qq = qb + acc_row(reg, hf);
         const float p = (qt == ktile && key > qq)
                             ? 0.f
-                            : __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -ls_[buf][0][row]));
+                            : __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -lse_r[reg]));
         float dpv = dp[reg];
         float pdv = p;
-        if constexpr (DROP) {
-          const uint32_t rowc = static_cast<uint32_t>((reg & 3) + 8 * (reg >> 2)) * 0x85EBCA6Bu;
-          const uint32_t hsh = lowbias32(hkey ^ (hq + rowc));
-          const bool kp_ = (hsh << kshift) >= thr_hi;
+        if constexpr (DROP) {  // the lane is the key here: one (cheap) hash per element
+          const bool kp_ = (mix1(ar_r[reg] ^ kmix) << kshift) >= thr_hi;
           dpv = kp_ ? dpv * a.inv_keep : 0.f;
           pdv = kp_ ? p * a.inv_keep : 0.f;
         }
         pd[reg] = pdv;
-        s[reg] = p * (dpv - ls_[buf][1][row]);  // dS
+        s[reg] = p * (dpv - dl_r[reg]);  // dS
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {

@@ -12,6 +12,12 @@ def test_dropout_mask_statistics_cpu():
     assert abs(frac - 0.9) < 0.01
     keep2 = fused.attention_dropout_keep(2, 3, 128, 0.1, seed=8)
     assert (keep != keep2).float().mean().item() > 0.1
+    # no structure between neighbours: adjacent keys (same hash word), adjacent
+    # queries and adjacent heads drop independently (P(both dropped) ~ p^2)
+    d = (~fused.attention_dropout_keep(1, 4, 512, 0.1, seed=3)).float()
+    for a, b in ((d[..., 0::2], d[..., 1::2]), (d[:, :, :-1], d[:, :, 1:]), (d[:, :-1], d[:, 1:])):
+        both = (a * b).mean().item()
+        assert abs(both - 0.01) < 0.003, both
 
 
 def _close(a, b, tol):
