@@ -64,6 +64,7 @@ def parse():
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--weight_decay", type=float, default=None)
     ap.add_argument("--gradient_checkpointing", action="store_true")
+    ap.add_argument("--fuse_accum", type=int, default=1, help="gradient-accumulation fusion (ops/linear.py)")
     ap.add_argument("--max_grad_norm", type=float, default=1.0)
     ap.add_argument("--exchange", default="a2a", help="allgather | a2a | ref_int64")
     ap.add_argument("--bucket_mb", type=float, default=32.0)
@@ -169,7 +170,8 @@ def main():
         def loss_fn(m, b):
             return m(input_ids=b["input_ids"], labels=b["labels"]).loss
 
-    step = TrainStep(model, opt, grad_accum=args.grad_accum, max_grad_norm=args.max_grad_norm, loss_fn=loss_fn)
+    step = TrainStep(model, opt, grad_accum=args.grad_accum, max_grad_norm=args.max_grad_norm, loss_fn=loss_fn,
+                     fuse_grad_accumulation=bool(args.fuse_accum))
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
 

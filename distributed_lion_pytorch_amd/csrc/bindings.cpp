@@ -309,34 +309,58 @@ std::tuple<Tensor, Tensor> bias_gelu_bwd(const Tensor& dh, const Tensor& z, cons
 }
 
 // sum of fp32 partials over dim 0 -> bf16 (split-K weight grads, bias / norm param grads)
+// partials: a [S, ...] contiguous stack, or a row-strided 2-D view [S, n]
+// (stride(1) == 1, e.g. one of the three [S, 3, C] norm parameter slices)
+struct Partials {
+  const float* ptr;
+  int64_t S, n, ld;
+};
+Partials partials(const Tensor& part) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat, "dlion: partials must be fp32 on the GPU");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(part.data_ptr()) % 16 == 0, "dlion: partials must be 16-byte aligned");
+  if (part.is_contiguous()) return {part.data_ptr<float>(), part.size(0), part.numel() / part.size(0),
+                                    part.numel() / part.size(0)};
+  TORCH_CHECK(part.dim() == 2 && part.stride(1) == 1 && part.stride(0) % 4 == 0,
+              "dlion: strided partials must be 2-D with unit column stride");
+  return {part.data_ptr<float>(), part.size(0), part.size(1), part.stride(0)};
+}
+
 Tensor sum_partials(const Tensor& part) {
-  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous(),
-              "dlion: partials must be contiguous fp32 on the GPU");
-  const int64_t S = part.size(0), n = part.numel() / S;
-  TORCH_CHECK(n % 4 == 0, "dlion: partial row length must be a multiple of 4");
+  const auto P = partials(part);
+  TORCH_CHECK(P.n % 4 == 0, "dlion: partial row length must be a multiple of 4");
   const c10::DeviceGuard g(part.device());
   auto sizes = part.sizes().vec();
   sizes.erase(sizes.begin());
   auto out = at::empty(sizes, part.options().dtype(at::kBFloat16));
-  check_hip(dlion::launch_sum_partials(part.data_ptr<float>(), static_cast<int>(S), n, out.data_ptr(), false,
-                                       cur_stream()),
+  check_hip(dlion::launch_sum_partials(P.ptr, static_cast<int>(P.S), P.n, P.ld, out.data_ptr(), false, cur_stream()),
             "sum_partials");
   return out;
 }
 
 // out += sum_s part[s] in place (bf16 out, one rounding): gradient accumulation
-// fused into the split-K weight-gradient reduction
+// fused into the partial-sum reduction
 void sum_partials_acc_(const Tensor& part, const Tensor& out) {
-  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous(),
-              "dlion: partials must be contiguous fp32 on the GPU");
-  const int64_t S = part.size(0), n = part.numel() / S;
-  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == n,
+  const auto P = partials(part);
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == P.n,
               "dlion: accumulation target must be a contiguous bf16 tensor of the partial row size");
-  TORCH_CHECK(n % 4 == 0, "dlion: partial row length must be a multiple of 4");
+  TORCH_CHECK(P.n % 4 == 0, "dlion: partial row length must be a multiple of 4");
   const c10::DeviceGuard g(part.device());
-  check_hip(dlion::launch_sum_partials(part.data_ptr<float>(), static_cast<int>(S), n, out.data_ptr(), true,
-                                       cur_stream()),
+  check_hip(dlion::launch_sum_partials(P.ptr, static_cast<int>(P.S), P.n, P.ld, out.data_ptr(), true, cur_stream()),
             "sum_partials_acc_");
+}
+
+// fp32 [parts, N] column-sum partials of a bf16 [rows, N] matrix
+Tensor colsum_partials(const Tensor& x, int64_t parts) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(),
+              "dlion colsum: x must be a contiguous bf16 GPU tensor");
+  const int64_t N = x.size(-1), rows = x.numel() / N;
+  TORCH_CHECK(N % 8 == 0 && N <= 16384 && parts >= 1 && parts <= 65535, "dlion colsum: bad shape");
+  const c10::DeviceGuard g(x.device());
+  auto part = at::empty({parts, N}, x.options().dtype(at::kFloat));
+  check_hip(dlion::launch_colsum(x.data_ptr(), part.data_ptr<float>(), static_cast<int>(parts), rows,
+                                 static_cast<int>(N), cur_stream()),
+            "colsum");
+  return part;
 }
 
 // ---------------------------------------------------------------- SwiGLU / RoPE
@@ -401,6 +425,7 @@ TORCH_LIBRARY(dlion, m) {
   m.def("bias_gelu_bwd(Tensor dh, Tensor z, Tensor b, bool exact, int parts) -> (Tensor, Tensor)");
   m.def("sum_partials(Tensor part) -> Tensor");
   m.def("sum_partials_acc_(Tensor part, Tensor(a!) out) -> ()");
+  m.def("colsum_partials(Tensor x, int parts) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float p, int seed) -> (Tensor, Tensor)");
   m.def(
       "attn_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout, Tensor lse, float p, int seed,"
@@ -433,6 +458,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("bias_gelu_bwd", &bias_gelu_bwd);
   m.impl("sum_partials", &sum_partials);
   m.impl("sum_partials_acc_", &sum_partials_acc_);
+  m.impl("colsum_partials", &colsum_partials);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("rope", &rope);

@@ -104,13 +104,13 @@ __global__ void __launch_bounds__(1024) bias_gelu_bwd_kernel(const uint16_t* __r
 // fused into the split-K reduction)), 4 elements per thread
 template <bool ACC>
 __global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restrict__ part, int S, int64_t n,
-                                                          uint16_t* __restrict__ out) {
+                                                          int64_t ld, uint16_t* __restrict__ out) {
   const int64_t n4 = n / 4;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n4;
        i += static_cast<int64_t>(gridDim.x) * 256) {
     float4 acc = reinterpret_cast<const float4*>(part)[i];
     for (int s = 1; s < S; ++s) {
-      const float4 v = reinterpret_cast<const float4*>(part + static_cast<int64_t>(s) * n)[i];
+      const float4 v = reinterpret_cast<const float4*>(part + static_cast<int64_t>(s) * ld)[i];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
     if constexpr (ACC) {
@@ -124,6 +124,40 @@ __global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restri
     w.x = static_cast<uint32_t>(f32_to_bf16(acc.x)) | (static_cast<uint32_t>(f32_to_bf16(acc.y)) << 16);
     w.y = static_cast<uint32_t>(f32_to_bf16(acc.z)) | (static_cast<uint32_t>(f32_to_bf16(acc.w)) << 16);
     reinterpret_cast<uint2*>(out)[i] = w;
+  }
+}
+
+// Column sums of a bf16 [rows, N] matrix as fp32 per-block partial rows (the
+// bias gradient of a linear layer whose output gradient has no other consumer
+// to fuse into); same thread layout as bias_gelu_bwd.
+template <int NC>
+__global__ void __launch_bounds__(1024) colsum_kernel(const uint16_t* __restrict__ x, float* __restrict__ part,
+                                                     int64_t rows, int N) {
+  const int groups = N / 8, bd = blockDim.x;
+  float acc[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int g = c * bd + threadIdx.x;
+      if (g >= groups) continue;
+      float v[8];
+      Elem<kBF16>::load8(x + r * N + g * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[c][j] += v[j];
+    }
+  }
+  float* out = part + static_cast<int64_t>(blockIdx.x) * N;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int g = c * bd + threadIdx.x;
+    if (g < groups) {
+      *reinterpret_cast<float4*>(out + g * 8) = make_float4(acc[c][0], acc[c][1], acc[c][2], acc[c][3]);
+      *reinterpret_cast<float4*>(out + g * 8 + 4) = make_float4(acc[c][4], acc[c][5], acc[c][6], acc[c][7]);
+    }
   }
 }
 
@@ -230,7 +264,8 @@ __global__ void __launch_bounds__(256) rope_kernel(const uint16_t* __restrict__ 
 constexpr int kTallQ = 8, kTallR = 32;
 template <bool ACC>
 __global__ void __launch_bounds__(kTallQ * kTallR) sum_partials_tall_kernel(const float* __restrict__ part, int S,
-                                                                           int64_t n, uint16_t* __restrict__ out) {
+                                                                           int64_t n, int64_t ld,
+                                                                           uint16_t* __restrict__ out) {
   __shared__ float4 red[kTallR][kTallQ];
   const int q = threadIdx.x % kTallQ, r = threadIdx.x / kTallQ;
   const int64_t col4 = static_cast<int64_t>(blockIdx.x) * kTallQ + q;  // float4 column index
@@ -239,7 +274,7 @@ __global__ void __launch_bounds__(kTallQ * kTallR) sum_partials_tall_kernel(cons
   if (col4 < n4) {
     const float4* p = reinterpret_cast<const float4*>(part) + col4;
     for (int s = r; s < S; s += kTallR) {
-      const float4 v = p[static_cast<int64_t>(s) * n4];
+      const float4 v = p[static_cast<int64_t>(s) * (ld / 4)];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
   }
@@ -309,6 +344,20 @@ hipError_t launch_bias_gelu_bwd(const void* dh, const void* z, const void* b, vo
   return hipGetLastError();
 }
 
+hipError_t launch_colsum(const void* x, float* part, int parts, int64_t rows, int N, hipStream_t st) {
+  if (N % 8 != 0) return hipErrorInvalidValue;
+  const int groups = N / 8;
+  const int bd = groups <= 1024 ? (groups + 63) / 64 * 64 : 1024;
+  const int nc = (groups + bd - 1) / bd;
+  auto X = static_cast<const uint16_t*>(x);
+  switch (nc) {
+    case 1: hipLaunchKernelGGL(colsum_kernel<1>, dim3(parts), dim3(bd), 0, st, X, part, rows, N); break;
+    case 2: hipLaunchKernelGGL(colsum_kernel<2>, dim3(parts), dim3(bd), 0, st, X, part, rows, N); break;
+    default: return hipErrorInvalidValue;  // N <= 16384
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_swiglu_fwd(const void* g, const void* u, void* h, int64_t n, hipStream_t st) {
   if (n % 8 != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, st, static_cast<const uint16_t*>(g),
@@ -334,8 +383,9 @@ hipError_t launch_rope(const void* x, const void* cos, const void* sin, void* y,
   return hipGetLastError();
 }
 
-hipError_t launch_sum_partials(const float* part, int S, int64_t n, void* out, bool accumulate, hipStream_t st) {
-  if (n % 4 != 0) return hipErrorInvalidValue;
+hipError_t launch_sum_partials(const float* part, int S, int64_t n, int64_t ld, void* out, bool accumulate,
+                               hipStream_t st) {
+  if (n % 4 != 0 || ld % 4 != 0 || ld < n) return hipErrorInvalidValue;
   const int64_t n4 = n / 4;
   auto O = static_cast<uint16_t*>(out);
   if (S > 64 || n4 < 256 * static_cast<int64_t>(S)) {
@@ -343,13 +393,13 @@ hipError_t launch_sum_partials(const float* part, int S, int64_t n, void* out, b
     const int64_t blocks = (n4 + kTallQ - 1) / kTallQ;
     if (blocks > 0x7fffffff) return hipErrorInvalidValue;
     const dim3 g(static_cast<unsigned>(blocks)), blk(kTallQ * kTallR);
-    if (accumulate) hipLaunchKernelGGL(sum_partials_tall_kernel<true>, g, blk, 0, st, part, S, n, O);
-    else hipLaunchKernelGGL(sum_partials_tall_kernel<false>, g, blk, 0, st, part, S, n, O);
+    if (accumulate) hipLaunchKernelGGL(sum_partials_tall_kernel<true>, g, blk, 0, st, part, S, n, ld, O);
+    else hipLaunchKernelGGL(sum_partials_tall_kernel<false>, g, blk, 0, st, part, S, n, ld, O);
     return hipGetLastError();
   }
   const dim3 g(grid_for(n / 4, 256)), blk(256);
-  if (accumulate) hipLaunchKernelGGL(sum_partials_kernel<true>, g, blk, 0, st, part, S, n, O);
-  else hipLaunchKernelGGL(sum_partials_kernel<false>, g, blk, 0, st, part, S, n, O);
+  if (accumulate) hipLaunchKernelGGL(sum_partials_kernel<true>, g, blk, 0, st, part, S, n, ld, O);
+  else hipLaunchKernelGGL(sum_partials_kernel<false>, g, blk, 0, st, part, S, n, ld, O);
   return hipGetLastError();
 }
 

@@ -44,7 +44,9 @@ hipError_t launch_swiglu_bwd(const void* dh, const void* g, const void* u, void*
                              hipStream_t st);
 hipError_t launch_rope(const void* x, const void* cos, const void* sin, void* y, int64_t rows, int T, int H, int D,
                        bool inverse, hipStream_t st);
-hipError_t launch_sum_partials(const float* part, int S, int64_t n, void* out, bool accumulate, hipStream_t st);
+hipError_t launch_sum_partials(const float* part, int S, int64_t n, int64_t ld, void* out, bool accumulate,
+                               hipStream_t st);
+hipError_t launch_colsum(const void* x, float* part, int parts, int64_t rows, int N, hipStream_t st);
 
 // ---- LM head cross-entropy (xent_kernels.hip)
 hipError_t launch_softmax_xent(int dt, void* logits, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,

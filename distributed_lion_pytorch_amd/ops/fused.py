@@ -141,6 +141,35 @@ def _sum_rows(part: torch.Tensor) -> torch.Tensor:
     return hip.ops().sum_partials(part)
 
 
+def _fused_params(*params):
+    """Which of (gamma, beta, bias) get their gradient deposited in place
+    (gradient-accumulation fusion, ops/linear.py); None entries are not fused."""
+    from .linear import _fuse_target
+
+    return tuple(p if p is not None and _fuse_target(p) else None for p in params)
+
+
+def _param_grads(part2d, C, fused, present):
+    """(dgamma, dbeta, dbias) from the [S, 3C] partials: fused parameters get
+    their .grad accumulated in place (returned as None), the rest come back as
+    bf16 gradients."""
+    from .linear import deposit_grad
+
+    out = [None, None, None]
+    need = [i for i in range(3) if present[i] and fused[i] is None]
+    if len(need) == 3 or (len(need) >= 1 and all(f is None for f in fused)):
+        sums = _sum_rows(part2d)
+        for i in need:
+            out[i] = sums[i * C:(i + 1) * C]
+    else:
+        for i in need:
+            out[i] = _sum_rows(part2d[:, i * C:(i + 1) * C])
+    for i in range(3):
+        if present[i] and fused[i] is not None:
+            deposit_grad(fused[i], part2d[:, i * C:(i + 1) * C])
+    return tuple(out)
+
+
 class _AddNorm(torch.autograd.Function):
     """(xo, h) = (x + dropout(y + bias), Norm(xo)) in one gfx950 kernel each way;
     gamma / beta / bias gradients come out of the backward kernel as partials."""
@@ -151,6 +180,7 @@ class _AddNorm(torch.autograd.Function):
         ctx.save_for_backward(xo, gamma, mean, rstd)
         ctx.rms, ctx.p, ctx.seed = rms, p, seed
         ctx.has_beta, ctx.has_bias = beta is not None, bias is not None
+        ctx.fused_params = _fused_params(gamma, beta, bias)
         return xo, h
 
     @staticmethod
@@ -163,10 +193,8 @@ class _AddNorm(torch.autograd.Function):
         parts = _norm_parts(rows, C)
         dx, dy, part = hip.ops().add_norm_bwd(dh.contiguous(), None if dxo is None else dxo.contiguous(), xo, gamma,
                                               mean, rstd, ctx.rms, ctx.p, ctx.seed, True, parts)
-        sums = _sum_rows(part.view(-1, 3 * C))
-        dgamma = sums[:C]
-        dbeta = sums[C:2 * C] if ctx.has_beta else None
-        dbias = sums[2 * C:] if ctx.has_bias else None
+        dgamma, dbeta, dbias = _param_grads(part.view(-1, 3 * C), C, ctx.fused_params,
+                                            (True, ctx.has_beta, ctx.has_bias))
         return dy, dx, dbias, dgamma, dbeta, None, None, None, None
 
 
@@ -176,6 +204,7 @@ class _Norm(torch.autograd.Function):
         _, h, mean, rstd = hip.ops().add_norm_fwd(x, None, None, gamma, beta, eps, rms, 0.0, 0)
         ctx.save_for_backward(x, gamma, mean, rstd)
         ctx.rms, ctx.has_beta = rms, beta is not None
+        ctx.fused_params = _fused_params(gamma, beta, None)
         return h
 
     @staticmethod
@@ -185,8 +214,8 @@ class _Norm(torch.autograd.Function):
         parts = _norm_parts(x.numel() // C, C)
         dx, _, part = hip.ops().add_norm_bwd(dh.contiguous(), None, x, gamma, mean, rstd, ctx.rms, 0.0, 0, False,
                                              parts)
-        sums = _sum_rows(part.view(-1, 3 * C))
-        return dx, sums[:C], (sums[C:2 * C] if ctx.has_beta else None), None, None
+        dgamma, dbeta, _ = _param_grads(part.view(-1, 3 * C), C, ctx.fused_params, (True, ctx.has_beta, False))
+        return dx, dgamma, dbeta, None, None
 
 
 NORM_WIDTHS = (256, 512, 768, 1024, 2048, 3072, 4096, 5120, 6144, 8192)  # csrc/norm_kernels.hip NORM_DISPATCH
@@ -224,6 +253,7 @@ class _BiasGelu(torch.autograd.Function):
     def forward(ctx, z, b, exact):
         ctx.save_for_backward(z, b)
         ctx.exact = exact
+        ctx.fused_b = _fused_params(b)[0]
         return hip.ops().bias_gelu_fwd(z, b, exact)
 
     @staticmethod
@@ -232,6 +262,11 @@ class _BiasGelu(torch.autograd.Function):
         rows = z.numel() // z.shape[-1]
         parts = max(1, min(1024, rows // 8))  # tools/bench_norm.py sweep: 1024 best at GPT-2 shape
         dz, part = hip.ops().bias_gelu_bwd(dh.contiguous(), z, b, ctx.exact, parts)
+        if ctx.fused_b is not None:
+            from .linear import deposit_grad
+
+            deposit_grad(ctx.fused_b, part)
+            return dz, None, None
         return dz, _sum_rows(part), None
 
 

@@ -41,9 +41,41 @@ def grad_accumulation_fusion(enabled: bool = True):
         _FUSE_ACCUM["on"] = prev
 
 
-def _fuse_target(w: torch.Tensor) -> bool:
+def _fuse_target(w) -> bool:
     return (_FUSE_ACCUM["on"] and isinstance(w, torch.nn.Parameter) and w.is_cuda
             and w.dtype == torch.bfloat16 and w.is_contiguous())
+
+
+def deposit_grad(param: torch.nn.Parameter, part2d: torch.Tensor) -> None:
+    """param.grad (+)= column sums of fp32 partials [S, numel] (row-strided OK),
+    in one kernel: the reduction adds the running gradient in the same pass."""
+    from . import hip
+
+    g = param.grad
+    if g is None or not (g.is_contiguous() and g.dtype == param.dtype):
+        fresh = hip.ops().sum_partials(part2d).view_as(param)
+        param.grad = fresh if g is None else g + fresh
+    else:
+        hip.ops().sum_partials_acc_(part2d, g)
+
+
+def _colsum_parts(rows: int) -> int:
+    return max(1, min(1024, rows // 16))
+
+
+def bias_grad(dy: torch.Tensor, b, fuse: bool):
+    """Bias gradient = column sums of dy [M, N]; deposited into b.grad when fused
+    (returns None then).  One streaming kernel + a tall partial sum instead of
+    ATen's column reduction (~2x slower at [20480, 2304])."""
+    from . import hip
+
+    if dy.is_cuda and dy.dtype == torch.bfloat16 and dy.shape[1] % 8 == 0 and hip.available():
+        part = hip.ops().colsum_partials(dy, _colsum_parts(dy.shape[0]))
+        if fuse:
+            deposit_grad(b, part)
+            return None
+        return hip.ops().sum_partials(part)
+    return dy.sum(0)
 
 
 def split_k_factor(M: int, K: int, N: int) -> int:
@@ -102,6 +134,8 @@ class _LinearKN(torch.autograd.Function):
         ctx.has_b = b is not None
         ctx.fuse = _fuse_target(w)
         ctx.param = w if ctx.fuse else None
+        ctx.fuse_b = b is not None and _fuse_target(b)
+        ctx.bias = b if ctx.fuse_b else None
         return torch.addmm(b, x2d, w) if b is not None else x2d @ w
 
     @staticmethod
@@ -115,7 +149,7 @@ class _LinearKN(torch.autograd.Function):
                 wgrad_into(x2d, dy, ctx.param)
             else:
                 dw = wgrad(x2d, dy)
-        db = dy.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        db = bias_grad(dy, ctx.bias, ctx.fuse_b) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db
 
 
@@ -128,6 +162,8 @@ class _LinearNK(torch.autograd.Function):
         ctx.has_b = b is not None
         ctx.fuse = _fuse_target(w)
         ctx.param = w if ctx.fuse else None
+        ctx.fuse_b = b is not None and _fuse_target(b)
+        ctx.bias = b if ctx.fuse_b else None
         return torch.nn.functional.linear(x2d, w, b)
 
     @staticmethod
@@ -141,7 +177,7 @@ class _LinearNK(torch.autograd.Function):
                 wgrad_into(dy, x2d, ctx.param)
             else:
                 dw = wgrad(dy, x2d)
-        db = dy.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        db = bias_grad(dy, ctx.bias, ctx.fuse_b) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db
 
 

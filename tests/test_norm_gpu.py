@@ -100,3 +100,20 @@ def test_sum_partials(S, shape, cuda):
     assert out.dtype == torch.bfloat16 and out.shape == shape
     ref = part.double().sum(0)
     assert ((out.double() - ref).abs() <= ref.abs() * 2 ** -7 + 1e-3 * S ** 0.5).all()
+
+
+def test_colsum_and_strided_partials(cuda):
+    hip.require()
+    torch.manual_seed(3)
+    x = torch.randn(2000, 2304, device=cuda).bfloat16()
+    part = hip.ops().colsum_partials(x, 125)
+    assert part.shape == (125, 2304)
+    assert _rel(hip.ops().sum_partials(part), x.float().sum(0)) < 1e-2
+    # row-strided slice of a [S, 3, C] norm partial stack, with in-place accumulation
+    stack = torch.randn(64, 3, 768, device=cuda)
+    sl = stack.view(64, 3 * 768)[:, 768:1536]
+    assert _rel(hip.ops().sum_partials(sl), stack[:, 1].sum(0)) < 1e-2
+    acc = torch.randn(768, device=cuda).bfloat16()
+    ref = acc.float() + stack[:, 2].sum(0)
+    hip.ops().sum_partials_acc_(stack.view(64, 3 * 768)[:, 1536:], acc)
+    assert _rel(acc, ref) < 1e-2
