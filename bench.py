@@ -18,7 +18,10 @@ exchange over RCCL, Lion update).  Rank 0 prints one JSON line.
 GPT2LMHeadModel + per-tensor int64 all_gather Lion) for an A/B comparison.
 `--task sft` measures BASELINE config #3 instead: Llama-2-7B, LoRA r=8 on
 q_proj/v_proj (bf16 base instead of the reference's 4-bit NF4), per-device
-batch 4 x seq 1024, grad-accum 2, Lion lr 1e-4 / wd 0.05.
+batch 4 x seq 1024, grad-accum 2, Lion lr 1e-4 / wd 0.05; `--task dpo`
+BASELINE config #4: Llama-2-7B LoRA DPO, policy fwd+bwd plus frozen
+reference fwd on 4 chosen/rejected pairs x 1024 tokens, grad-accum 4,
+gradient checkpointing (dpo_llama2.py defaults).
 """
 from __future__ import annotations
 
@@ -47,6 +50,13 @@ PRESETS = {
     "sft": dict(model="llama-2-7b", micro_batch=4, seq_len=1024, grad_accum=2, lr=1e-4, weight_decay=0.05,
                 lora=dict(r=8, lora_alpha=16, lora_dropout=0.05, target_modules=["q_proj", "v_proj"]),
                 metric="tokens/sec + all-reduce bytes/step, Llama-2-7B LoRA SFT (sft_llama2 config)"),
+    # dpo_llama2.py:25-52 defaults: batch 4 pairs, grad-accum 4, max_length 1024 (prompt 512), beta 0.1,
+    # lr 5e-4, wd 0.05, gradient checkpointing on, LoRA r=8 (its target list's Llama names: q/k/v_proj);
+    # frozen reference model = a copy of the base weights.  Tokens counted = chosen + rejected sequences.
+    "dpo": dict(model="llama-2-7b", micro_batch=4, seq_len=1024, grad_accum=4, lr=5e-4, weight_decay=0.05,
+                lora=dict(r=8, lora_alpha=16, lora_dropout=0.05, target_modules=["q_proj", "v_proj", "k_proj"]),
+                grad_ckpt=True, dpo_beta=0.1,
+                metric="tokens/sec + all-reduce bytes/step, Llama-2-7B LoRA DPO (dpo_llama2 config)"),
 }
 
 
@@ -77,6 +87,7 @@ def parse():
     for k, v in PRESETS[a.task].items():
         if getattr(a, k, None) is None:
             setattr(a, k, v)
+    a.gradient_checkpointing = a.gradient_checkpointing or bool(getattr(a, "grad_ckpt", False))
     return a
 
 
@@ -105,6 +116,13 @@ def build_native(args, dev):
     torch.manual_seed(0)
     with torch.device(dev):  # materialise weights on the GPU directly (7B: no host round trip)
         model = build_model(cfg, native=True).to(dtype=torch.bfloat16)
+    ref_model = None
+    if args.task == "dpo":
+        import copy
+
+        ref_model = copy.deepcopy(model).eval()
+        for p in ref_model.parameters():
+            p.requires_grad_(False)
     if args.lora:
         from distributed_lion_pytorch_amd.models.lora import LoraConfig, inject_lora
 
@@ -115,6 +133,7 @@ def build_native(args, dev):
     broadcast_parameters(model)
     opt = Lion([p for p in model.parameters() if p.requires_grad], lr=args.lr, weight_decay=args.weight_decay,
                exchange=args.exchange, bucket_mb=args.bucket_mb)
+    args.ref_model = ref_model  # not a submodule: stays out of the parameter counts
     return model, opt, cfg
 
 
@@ -164,7 +183,19 @@ def main():
     n_params = sum({p.data_ptr(): p.numel() for p in model.parameters()}.values())
     n_train = sum({p.data_ptr(): p.numel() for p in model.parameters() if p.requires_grad}.values())
 
-    if args.impl == "native":
+    if args.task == "dpo":
+        from distributed_lion_pytorch_amd.trainer.dpo import dpo_loss, sequence_logps
+
+        ref = args.ref_model
+
+        def loss_fn(m, b):
+            ids, labels = b["input_ids"], b["labels"]
+            n = ids.shape[0] // 2
+            logp = sequence_logps(m, ids, labels)
+            with torch.no_grad():
+                ref_logp = sequence_logps(ref, ids, labels)
+            return dpo_loss(logp[:n], logp[n:], ref_logp[:n], ref_logp[n:], args.dpo_beta)[0]
+    elif args.impl == "native":
         loss_fn = None
     else:
         def loss_fn(m, b):
@@ -175,10 +206,16 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
 
+    seqs_per_mb = args.micro_batch * (2 if args.task == "dpo" else 1)  # DPO: chosen + rejected
+
     def batches():
         for _ in range(args.grad_accum):
-            ids = torch.randint(0, cfg.vocab_size, (args.micro_batch, args.seq_len), device=dev, generator=gen)
-            yield {"input_ids": ids, "labels": ids}
+            ids = torch.randint(0, cfg.vocab_size, (seqs_per_mb, args.seq_len), device=dev, generator=gen)
+            labels = ids
+            if args.task == "dpo":  # prompt half masked out of the log-likelihood, as the DPO collator does
+                labels = ids.clone()
+                labels[:, : args.seq_len // 2] = -100
+            yield {"input_ids": ids, "labels": labels}
 
     for _ in range(args.warmup):
         step(batches())
@@ -201,7 +238,7 @@ def main():
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
-    tokens = world * args.grad_accum * args.micro_batch * args.seq_len * args.steps
+    tokens = world * args.grad_accum * seqs_per_mb * args.seq_len * args.steps
     tps = tokens / elapsed
     ms = 1000.0 * elapsed / args.steps
     stats = opt.stats() if hasattr(opt, "stats") else {}
@@ -226,6 +263,7 @@ def main():
                 "trainable_params": n_train,
                 "lora": args.lora,
                 "global_batch": world * args.grad_accum * args.micro_batch,
+                "task": args.task,
                 "micro_batch": args.micro_batch,
                 "grad_accum": args.grad_accum,
                 "seq_len": args.seq_len,

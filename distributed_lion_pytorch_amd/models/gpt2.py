@@ -221,6 +221,11 @@ class GPT2LMHeadModel(PreTrainedModel):
             logits = F.linear(h, self.lm_head.weight)
         return CausalLMOutputWithCrossAttentions(loss=loss, logits=logits)
 
+    def sequence_logps(self, input_ids: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        """Sum of log p(label_t | <t) per sequence (DPO); labels -100 ignored."""
+        h = self.transformer(input_ids)[:, :-1]
+        return fused.token_logps(h, self.lm_head.weight, labels[:, 1:]).sum(-1)
+
     def flops_per_token(self, seq_len: int) -> float:
         """Training FLOPs per token (6N + attention), for MFU reporting."""
         c = self.config

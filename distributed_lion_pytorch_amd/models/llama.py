@@ -251,8 +251,5 @@ def sequence_logps(model, input_ids: torch.Tensor, labels: torch.Tensor) -> torc
     causal LMs): used by the DPO loss (policy and frozen reference)."""
     base = model.model if hasattr(model, "model") and isinstance(model.model, LlamaModel) else model.transformer
     h = base(input_ids)[:, :-1]
-    logits = F.linear(h, model.lm_head.weight).float()
-    tgt = labels[:, 1:]
-    mask = tgt != -100
-    lp = torch.log_softmax(logits, dim=-1).gather(-1, tgt.clamp_min(0).unsqueeze(-1)).squeeze(-1)
-    return (lp * mask).sum(-1)
+    # fused LM head + log-softmax gather (no fp32 [B, T, V] logits)
+    return fused.token_logps(h, model.lm_head.weight, labels[:, 1:]).sum(-1)

@@ -503,6 +503,52 @@ def _softmax_xent_torch_(logits: torch.Tensor, labels: torch.Tensor, v: int) -> 
     return row_loss
 
 
+class _TokenLogp(torch.autograd.Function):
+    """Per-token log p(label) of ``h @ W^T`` (0 for labels == -100) through the
+    same fused softmax-xent kernel: the [N, V] logits are turned into
+    softmax - onehot in place; forward-only callers (the frozen DPO reference
+    model) keep nothing, training callers keep that bf16 matrix for the two
+    backward GEMMs (the row weights differ per sequence, so the gradients
+    cannot be pre-contracted in the forward as in _LMHeadCE)."""
+
+    @staticmethod
+    def forward(ctx, h2d, weight, labels1d):
+        v = weight.shape[0]
+        wp = _pad_rows(weight)
+        logits = h2d @ wp.t()
+        if _use_hip(logits):
+            row_loss = hip.ops().softmax_xent_(logits, labels1d, v)
+        else:
+            row_loss = _softmax_xent_torch_(logits, labels1d, v)
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            ctx.save_for_backward(h2d, wp, logits)
+            ctx.v = v
+        return -row_loss
+
+    @staticmethod
+    def backward(ctx, g):
+        h2d, wp, pm = ctx.saved_tensors  # pm = softmax - onehot
+        d = pm * (-g).to(pm.dtype)[:, None]  # d logp / d logits = -(softmax - onehot)
+        dh = d @ wp if ctx.needs_input_grad[0] else None
+        dw = (d.t() @ h2d)[: ctx.v] if ctx.needs_input_grad[1] else None
+        return dh, dw, None
+
+
+def token_logps(h: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """log p(labels) per position of h [..., C] under the LM head (0 where -100)."""
+    h2d = h.reshape(-1, h.shape[-1])
+    lab = labels.reshape(-1)
+    if h2d.is_cuda:
+        from .linear import autocast_inputs
+
+        h2d, weight = autocast_inputs(h2d.contiguous(), weight)
+        with torch.autocast("cuda", enabled=False):
+            return _TokenLogp.apply(h2d, weight, lab).view(labels.shape)
+    if h2d.dtype != weight.dtype:
+        h2d = h2d.to(weight.dtype)
+    return _TokenLogp.apply(h2d.contiguous(), weight, lab).view(labels.shape)
+
+
 def lm_head_cross_entropy(h: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor,
                           normalizer=None) -> torch.Tensor:
     """Token cross-entropy of ``h @ weight.T`` against ``labels`` (-100 ignored):

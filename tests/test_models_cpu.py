@@ -110,3 +110,24 @@ def test_attention_fallback_matches_reference(T, H, Hkv, D):
     out = fused.causal_attention_gqa(q, k, v, 0.0)
     ref = fused.reference_attention(q, k, v, 0.0)
     assert torch.allclose(out, ref, atol=1e-5)
+
+
+def test_token_logps_matches_log_softmax_cpu():
+    import torch
+
+    from distributed_lion_pytorch_amd.ops import fused
+
+    torch.manual_seed(0)
+    h = torch.randn(3, 7, 16, requires_grad=True)
+    w = torch.randn(50, 16, requires_grad=True)
+    labels = torch.randint(0, 50, (3, 7))
+    labels[0, :3] = -100
+    lp = fused.token_logps(h, w, labels)
+    ref = torch.log_softmax(h @ w.t(), -1).gather(-1, labels.clamp_min(0)[..., None])[..., 0] * (labels != -100)
+    assert torch.allclose(lp, ref, atol=1e-4)
+    g = torch.randn(3)
+    lp.sum(-1).mul(g).sum().backward()
+    gh, gw = h.grad.clone(), w.grad.clone()
+    h.grad = w.grad = None
+    ref.sum(-1).mul(g).sum().backward()
+    assert torch.allclose(gh, h.grad, atol=1e-4) and torch.allclose(gw, w.grad, atol=1e-4)
