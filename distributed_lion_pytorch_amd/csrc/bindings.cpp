@@ -409,9 +409,68 @@ Tensor rope(const Tensor& x, const Tensor& cos, const Tensor& sin, bool inverse)
   return y;
 }
 
+// ---------------------------------------------------------------- GEMM (NT)
+// a [M, K], b [N, K] (rows may be strided, unit column stride) -> c [M, N] bf16
+void check_gemm_operand(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2 && t.stride(1) == 1,
+              "dlion gemm: ", name, " must be a 2-D bf16 GPU tensor with unit column stride");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              "dlion gemm: ", name, " rows must be 16-byte aligned");
+}
+
+bool gemm_nt_supported(const Tensor& a, const Tensor& b) {
+  return a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1) && a.size(1) % 128 == 0 && b.size(0) % 8 == 0 &&
+         a.size(0) * a.stride(0) < (1ll << 31) && b.size(0) * b.stride(0) < (1ll << 31);
+}
+
+void gemm_nt_launch(const Tensor& a, const Tensor& b, const Tensor& c, const Tensor* bias, const Tensor* aux,
+                    int64_t epi) {
+  check_gemm_operand(a, "a");
+  check_gemm_operand(b, "b");
+  check_gemm_operand(c, "out");
+  TORCH_CHECK(gemm_nt_supported(a, b), "dlion gemm: unsupported shape a=", a.sizes(), " b=", b.sizes(),
+              " (needs K % 128 == 0, N % 8 == 0)");
+  TORCH_CHECK(c.size(0) == a.size(0) && c.size(1) == b.size(0), "dlion gemm: output shape mismatch");
+  if (bias) {
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() &&
+                    bias->numel() == b.size(0),
+                "dlion gemm: bias must be a contiguous bf16 [N] tensor");
+  }
+  if (aux) check_gemm_operand(*aux, "aux");
+  const c10::DeviceGuard g(a.device());
+  check_hip(dlion::launch_gemm_nt(a.data_ptr(), static_cast<int>(a.stride(0)), b.data_ptr(),
+                                  static_cast<int>(b.stride(0)), c.data_ptr(), static_cast<int>(c.stride(0)),
+                                  bias ? bias->data_ptr() : nullptr, aux ? aux->data_ptr() : nullptr,
+                                  aux ? static_cast<int>(aux->stride(0)) : 0, static_cast<int>(a.size(0)),
+                                  static_cast<int>(b.size(0)), static_cast<int>(a.size(1)), static_cast<int>(epi),
+                                  cur_stream()),
+            "gemm_nt");
+}
+
+Tensor gemm_nt(const Tensor& a, const Tensor& b, const std::optional<Tensor>& bias) {
+  auto c = at::empty({a.size(0), b.size(0)}, a.options());
+  gemm_nt_launch(a, b, c, bias.has_value() ? &*bias : nullptr, nullptr, bias.has_value() ? 1 : 0);
+  return c;
+}
+
+void gemm_nt_out(const Tensor& a, const Tensor& b, const std::optional<Tensor>& bias, const Tensor& out) {
+  gemm_nt_launch(a, b, out, bias.has_value() ? &*bias : nullptr, nullptr, bias.has_value() ? 1 : 0);
+}
+
+// h = gelu(z + bias), z = a . b^T (bf16): returns (h, z) -- z is what the bias+GELU backward reads
+std::tuple<Tensor, Tensor> gemm_nt_gelu(const Tensor& a, const Tensor& b, const Tensor& bias, bool exact) {
+  auto h = at::empty({a.size(0), b.size(0)}, a.options());
+  auto z = at::empty_like(h);
+  gemm_nt_launch(a, b, h, &bias, &z, exact ? 3 : 2);
+  return {h, z};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dlion, m) {
+  m.def("gemm_nt(Tensor a, Tensor b, Tensor? bias) -> Tensor");
+  m.def("gemm_nt_out(Tensor a, Tensor b, Tensor? bias, Tensor(a!) out) -> ()");
+  m.def("gemm_nt_gelu(Tensor a, Tensor b, Tensor bias, bool exact) -> (Tensor, Tensor)");
   m.def("swiglu_fwd(Tensor g, Tensor u) -> Tensor");
   m.def("swiglu_bwd(Tensor dh, Tensor g, Tensor u) -> (Tensor, Tensor)");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, bool inverse) -> Tensor");
@@ -462,4 +521,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("rope", &rope);
+  m.impl("gemm_nt", &gemm_nt);
+  m.impl("gemm_nt_out", &gemm_nt_out);
+  m.impl("gemm_nt_gelu", &gemm_nt_gelu);
 }

@@ -135,6 +135,22 @@ __device__ __forceinline__ void store8g(typename Elem<DT>::S* base, int64_t e, i
   }
 }
 
+// ------------------------------------------------------------------- GELU
+// tanh via one v_exp_f32 + one v_rcp_f32 (libm tanhf is a ~30-instruction
+// polynomial path and made the memory-bound bias+GELU kernels VALU-bound);
+// |err| ~1e-7, far below the bf16 output rounding.  Saturates correctly.
+__device__ __forceinline__ float fast_tanh(float a) {
+  const float e = __builtin_amdgcn_exp2f(a * 2.8853900817779268f);  // exp(2a)
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
+// GELU: exact = erf form (nn.GELU()), else the tanh approximation (gelu_new).
+// Shared by the bias+GELU kernels and the GEMM epilogue (bitwise-identical).
+__device__ __forceinline__ float gelu_f(float u, bool exact) {
+  if (exact) return 0.5f * u * (1.f + erff(u * 0.7071067811865476f));
+  const float t = fast_tanh(0.7978845608028654f * (u + 0.044715f * u * u * u));
+  return 0.5f * u * (1.f + t);
+}
+
 // ------------------------------------------------------------ vote counting
 // Spread the 8 bits of a byte into the 8 bytes of a u64 (bit j -> bit 8j), so
 // that summing spread bytes over W <= 255 ranks counts 8 votes in parallel.

@@ -17,18 +17,6 @@ constexpr float kKappa = 0.044715f;
 constexpr float kInvSqrt2 = 0.7071067811865476f;
 constexpr float kInvSqrt2Pi = 0.3989422804014327f;
 
-// tanh via one v_exp_f32 + one v_rcp_f32 (libm tanhf is a ~30-instruction
-// polynomial path and made this memory-bound kernel VALU-bound); |err| ~1e-7,
-// far below the bf16 output rounding.  Saturates correctly for |a| large.
-__device__ __forceinline__ float fast_tanh(float a) {
-  const float e = __builtin_amdgcn_exp2f(a * 2.8853900817779268f);  // exp(2a)
-  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
-}
-__device__ __forceinline__ float gelu_f(float u, bool exact) {
-  if (exact) return 0.5f * u * (1.f + erff(u * kInvSqrt2));
-  const float t = fast_tanh(kSqrt2OverPi * (u + kKappa * u * u * u));
-  return 0.5f * u * (1.f + t);
-}
 __device__ __forceinline__ float gelu_grad(float u, bool exact) {
   if (exact) return 0.5f * (1.f + erff(u * kInvSqrt2)) + u * kInvSqrt2Pi * __expf(-0.5f * u * u);
   const float u2 = u * u;

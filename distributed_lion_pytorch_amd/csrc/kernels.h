@@ -48,6 +48,12 @@ hipError_t launch_sum_partials(const float* part, int S, int64_t n, int64_t ld, 
                                hipStream_t st);
 hipError_t launch_colsum(const void* x, float* part, int parts, int64_t rows, int N, hipStream_t st);
 
+// ---- bf16 GEMM C[M,N] = A[M,K] . B[N,K]^T with fused epilogue (gemm.hip)
+// epi: 0 plain, 1 + bias, 2 aux = z, C = gelu_tanh(z + bias), 3 the same with erf GELU.
+// Needs K % 128 == 0, N % 8 == 0, leading dims % 8 == 0.
+hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
+                          void* aux, int ldaux, int M, int N, int K, int epi, hipStream_t st);
+
 // ---- LM head cross-entropy (xent_kernels.hip)
 hipError_t launch_softmax_xent(int dt, void* logits, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,
                                hipStream_t st);

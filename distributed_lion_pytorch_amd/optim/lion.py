@@ -38,6 +38,7 @@ import torch.distributed as dist
 from torch.optim.optimizer import Optimizer
 
 from ..ops import reference as ref
+from ..ops.linear import bump_weight_generation
 from ..parallel.exchange import canonical_strategy, make_exchange, wire_bytes_per_step
 from .executors import HParams, make_executor
 from .plan import FlatPlan
@@ -236,6 +237,9 @@ class Lion(Optimizer):
                 ex.local(meta, b, hps[b.group], grads=grads, moms=moms)
         else:
             self._distributed_step(plan, ex, meta, hps, grads, moms, world, rank)
+        # the kernels wrote the weights through raw pointers (no autograd
+        # version bump): invalidate derived per-step weight copies
+        bump_weight_generation()
         self._n_steps += 1
         return loss
 
