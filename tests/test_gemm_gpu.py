@@ -50,9 +50,8 @@ def test_gemm_nt_asymmetric_exact():
     a = torch.randint(-3, 4, (M, K), device="cuda").to(torch.bfloat16)
     b = torch.randint(-3, 4, (N, K), device="cuda").to(torch.bfloat16)
     b[:, 0] += torch.arange(N, device="cuda").to(torch.bfloat16) % 7  # asymmetric in (row, col)
-    got = ops.gemm_nt(a, b, None).float()
     ref = _ref(a, b).to(torch.bfloat16).float()  # exact sums, one RNE rounding either way
-    assert torch.equal(got, ref)
+    assert torch.equal(ops.gemm_nt(a, b, None).float(), ref)
 
 
 def test_gemm_nt_strided_rows_and_out():
