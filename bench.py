@@ -21,7 +21,9 @@ q_proj/v_proj (bf16 base instead of the reference's 4-bit NF4), per-device
 batch 4 x seq 1024, grad-accum 2, Lion lr 1e-4 / wd 0.05; `--task dpo`
 BASELINE config #4: Llama-2-7B LoRA DPO, policy fwd+bwd plus frozen
 reference fwd on 4 chosen/rejected pairs x 1024 tokens, grad-accum 4,
-gradient checkpointing (dpo_llama2.py defaults).
+gradient checkpointing (dpo_llama2.py defaults); `--task llama3` BASELINE
+config #5's model: Llama-3-8B full-parameter bf16 Lion, 4 x 2048 tokens per
+step (the worker-dropout stress itself is dropout_stress.py).
 """
 from __future__ import annotations
 
@@ -57,6 +59,13 @@ PRESETS = {
                 lora=dict(r=8, lora_alpha=16, lora_dropout=0.05, target_modules=["q_proj", "v_proj", "k_proj"]),
                 grad_ckpt=True, dpo_beta=0.1,
                 metric="tokens/sec + all-reduce bytes/step, Llama-2-7B LoRA DPO (dpo_llama2 config)"),
+    # BASELINE config #5's model: Llama-3-8B, FULL-parameter bf16 Distributed Lion
+    # (8.03B trainable: the optimizer hot path at scale -- 1-bit vote planes of
+    # 1 GB per rank, encode/apply over 48 GB of weights+grads+momentum), the
+    # dropout_stress.py shape (seq 2048) with 4 sequences per micro-batch.
+    "llama3": dict(model="llama-3-8b", micro_batch=4, seq_len=2048, grad_accum=1, lr=1e-5, weight_decay=0.0,
+                   lora=None,
+                   metric="tokens/sec + all-reduce bytes/step, Llama-3-8B full-parameter bf16 Distributed Lion"),
 }
 
 

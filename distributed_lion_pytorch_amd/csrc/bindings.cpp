@@ -27,8 +27,16 @@ void check_hip(hipError_t e, const char* what) {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+const float* gscale_ptr(const std::optional<Tensor>& gscale) {
+  if (!gscale.has_value()) return nullptr;
+  check_dev(*gscale, "gscale");
+  TORCH_CHECK(gscale->scalar_type() == at::kFloat && gscale->numel() >= 2, "dlion: gscale must be float32[2]");
+  return gscale->data_ptr<float>();
+}
+
 void lion_local(const Tensor& meta, int64_t seg_off, int64_t chunk_off, int64_t n_chunks, int64_t dtype,
-                double decay, double neg_lr, double b1, double omb1, double b2, double omb2) {
+                double decay, double neg_lr, double b1, double omb1, double b2, double omb2,
+                const std::optional<Tensor>& gscale) {
   check_dev(meta, "meta");
   TORCH_CHECK(meta.scalar_type() == at::kLong, "dlion: meta must be int64");
   const c10::DeviceGuard g(meta.device());
@@ -36,13 +44,13 @@ void lion_local(const Tensor& meta, int64_t seg_off, int64_t chunk_off, int64_t 
   check_hip(dlion::launch_lion_local(static_cast<int>(dtype), base + seg_off, base + chunk_off, n_chunks,
                                      static_cast<float>(decay), static_cast<float>(neg_lr), static_cast<float>(b1),
                                      static_cast<float>(omb1), static_cast<float>(b2), static_cast<float>(omb2),
-                                     cur_stream()),
+                                     gscale_ptr(gscale), cur_stream()),
             "lion_local");
 }
 
 void lion_encode(const Tensor& meta, int64_t seg_off, int64_t chunk_off, int64_t n_chunks, int64_t dtype,
                  const Tensor& bits, double b1, double omb1, double b2, double omb2, bool update_m,
-                 bool stochastic, double rr, int64_t seed, int64_t step) {
+                 bool stochastic, double rr, int64_t seed, int64_t step, const std::optional<Tensor>& gscale) {
   check_dev(meta, "meta");
   check_dev(bits, "bits");
   TORCH_CHECK(bits.scalar_type() == at::kByte, "dlion: bits must be uint8");
@@ -52,8 +60,35 @@ void lion_encode(const Tensor& meta, int64_t seg_off, int64_t chunk_off, int64_t
                                       bits.data_ptr<uint8_t>(), static_cast<float>(b1), static_cast<float>(omb1),
                                       static_cast<float>(b2), static_cast<float>(omb2), update_m ? 1 : 0,
                                       stochastic ? 1 : 0, static_cast<float>(rr), static_cast<uint64_t>(seed),
-                                      static_cast<uint32_t>(step), cur_stream()),
+                                      static_cast<uint32_t>(step), gscale_ptr(gscale), cur_stream()),
             "lion_encode");
+}
+
+// partial[chunk_base + i] = sum of g^2 over chunk i of the bucket
+void grad_sumsq(const Tensor& meta, int64_t seg_off, int64_t chunk_off, int64_t n_chunks, int64_t dtype,
+                const Tensor& partial, int64_t part_off) {
+  check_dev(meta, "meta");
+  check_dev(partial, "partial");
+  TORCH_CHECK(partial.scalar_type() == at::kFloat && part_off + n_chunks <= partial.numel(),
+              "dlion: grad_sumsq partial buffer too small");
+  const c10::DeviceGuard g(meta.device());
+  const int64_t* base = meta.data_ptr<int64_t>();
+  check_hip(dlion::launch_grad_sumsq(static_cast<int>(dtype), base + seg_off, base + chunk_off, n_chunks,
+                                     partial.data_ptr<float>() + part_off, cur_stream()),
+            "grad_sumsq");
+}
+
+// out[0] = sqrt(sum partial), out[1] = min(1, max_norm / (out[0] + 1e-6))
+void clip_coef(const Tensor& partial, int64_t n, double max_norm, const Tensor& out) {
+  check_dev(partial, "partial");
+  check_dev(out, "out");
+  TORCH_CHECK(partial.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat && out.numel() >= 2 &&
+                  n <= partial.numel(),
+              "dlion: clip_coef needs float32 partials and a float32[2] output");
+  const c10::DeviceGuard g(partial.device());
+  check_hip(dlion::launch_clip_coef(partial.data_ptr<float>(), n, static_cast<float>(max_norm), out.data_ptr<float>(),
+                                    cur_stream()),
+            "clip_coef");
 }
 
 void lion_vote_apply(const Tensor& meta, int64_t seg_off, int64_t chunk_off, int64_t n_chunks, int64_t dtype,
@@ -492,10 +527,14 @@ TORCH_LIBRARY(dlion, m) {
   m.def("softmax_xent_(Tensor(a!) logits, Tensor labels, int v) -> Tensor");
   m.def(
       "lion_local(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, float decay, float neg_lr,"
-      " float b1, float omb1, float b2, float omb2) -> ()");
+      " float b1, float omb1, float b2, float omb2, Tensor? gscale=None) -> ()");
   m.def(
       "lion_encode(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, Tensor(a!) bits, float b1,"
-      " float omb1, float b2, float omb2, bool update_m, bool stochastic, float rr, int seed, int step) -> ()");
+      " float omb1, float b2, float omb2, bool update_m, bool stochastic, float rr, int seed, int step,"
+      " Tensor? gscale=None) -> ()");
+  m.def("grad_sumsq(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, Tensor(a!) partial,"
+        " int part_off) -> ()");
+  m.def("clip_coef(Tensor partial, int n, float max_norm, Tensor(a!) out) -> ()");
   m.def(
       "lion_vote_apply(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, Tensor planes,"
       " int plane_stride, Tensor alive, int mode, int tie, Tensor? neg, float decay, float neg_lr,"
@@ -508,6 +547,8 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("lion_encode", &lion_encode);
   m.impl("lion_vote_apply", &lion_vote_apply);
   m.impl("vote_reduce", &vote_reduce);
+  m.impl("grad_sumsq", &grad_sumsq);
+  m.impl("clip_coef", &clip_coef);
   m.impl("softmax_xent_", &softmax_xent_);
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);

@@ -9,10 +9,15 @@ namespace dlion {
 
 // ---- optimizer (lion_kernels.hip)
 hipError_t launch_lion_local(int dt, const int64_t* seg, const int64_t* chunks, int64_t n_chunks, float decay,
-                             float neg_lr, float b1, float omb1, float b2, float omb2, hipStream_t st);
+                             float neg_lr, float b1, float omb1, float b2, float omb2, const float* gscale,
+                             hipStream_t st);
 hipError_t launch_lion_encode(int dt, const int64_t* seg, const int64_t* chunks, int64_t n_chunks, uint8_t* bits,
                               float b1, float omb1, float b2, float omb2, int update_m, int stochastic, float rr,
-                              uint64_t seed, uint32_t step, hipStream_t st);
+                              uint64_t seed, uint32_t step, const float* gscale, hipStream_t st);
+// fused clip_grad_norm_: per-chunk sum of squares, then norm + clip coefficient on device
+hipError_t launch_grad_sumsq(int dt, const int64_t* seg, const int64_t* chunks, int64_t n_chunks, float* partial,
+                             hipStream_t st);
+hipError_t launch_clip_coef(const float* partial, int64_t n, float max_norm, float* out, hipStream_t st);
 hipError_t launch_lion_vote_apply(int dt, const int64_t* seg, const int64_t* chunks, int64_t n_chunks,
                                   const uint8_t* planes, int64_t plane_stride, const uint8_t* alive, int world,
                                   int mode, int tie, const uint8_t* neg, float decay, float neg_lr, const uint8_t* own,

@@ -56,14 +56,25 @@ __device__ __forceinline__ float sgn(float x) {  // ATen sign: NaN -> 0, +-0 -> 
   return static_cast<float>((x > 0.f) - (x < 0.f));
 }
 
+// Fused gradient clipping: g <- round(g * coef) in the parameter dtype, i.e.
+// what clip_grad_norm_'s in-place _foreach_mul_ would have stored, applied on
+// load instead of as a separate read+write pass over every gradient.
+template <int DT>
+__device__ __forceinline__ void clip8(float (&gv)[8], float cs) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) gv[j] = Elem<DT>::rnd(gv[j] * cs);
+}
+
 // ----------------------------------------------------------------------- K0
 template <int DT>
 __global__ void __launch_bounds__(kThreads)
 lion_local_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ chunks,
-                  float decay, float neg_lr, float b1, float omb1, float b2, float omb2) {
+                  float decay, float neg_lr, float b1, float omb1, float b2, float omb2,
+                  const float* __restrict__ gscale) {
   using E = Elem<DT>;
   using S = typename E::S;
   const int64_t s = chunks[2 * blockIdx.x], start = chunks[2 * blockIdx.x + 1];
+  const float cs = gscale != nullptr ? gscale[1] : 1.f;
   const SegRow r = load_seg(seg, s);
   S* p = const_cast<S*>(static_cast<const S*>(r.p));
   const S* g = static_cast<const S*>(r.g);
@@ -76,6 +87,7 @@ lion_local_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ c
     load8g<DT>(p, e, r.n, r.vec, pv);
     load8g<DT>(g, e, r.n, r.vec, gv);
     load8g<DT>(m, e, r.n, r.vec, mv);
+    if (gscale != nullptr) clip8<DT>(gv, cs);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float pw = E::rnd(pv[j] * decay);                       // p *= 1 - lr*wd
@@ -96,10 +108,12 @@ template <int DT, bool STOC>
 __global__ void __launch_bounds__(kThreads)
 lion_encode_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ chunks,
                    uint8_t* __restrict__ bits, float b1, float omb1, float b2, float omb2,
-                   int update_m, float rr, uint32_t seed_lo, uint32_t seed_hi, uint32_t step) {
+                   int update_m, float rr, uint32_t seed_lo, uint32_t seed_hi, uint32_t step,
+                   const float* __restrict__ gscale) {
   using E = Elem<DT>;
   using S = typename E::S;
   const int64_t s = chunks[2 * blockIdx.x], start = chunks[2 * blockIdx.x + 1];
+  const float cs = gscale != nullptr ? gscale[1] : 1.f;
   const SegRow r = load_seg(seg, s);
   const S* g = static_cast<const S*>(r.g);
   S* m = const_cast<S*>(static_cast<const S*>(r.m));
@@ -113,6 +127,7 @@ lion_encode_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ 
       float gv[8], mv[8];
       load8g<DT>(g, e, r.n, r.vec, gv);
       load8g<DT>(m, e, r.n, r.vec, mv);
+      if (gscale != nullptr) clip8<DT>(gv, cs);
       float u[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) u[j] = E::rnd(__fmaf_rn(gv[j], omb1, E::rnd(mv[j] * b1)));
@@ -269,6 +284,61 @@ vote_reduce_kernel(const uint8_t* __restrict__ recv, int64_t nbytes, const uint8
   }
 }
 
+// ------------------------------------------------------------ gradient norm
+// partial[chunk] = sum of g^2 (fp32) over the chunk's elements, one block per
+// chunk of the same pointer table the update kernels walk; clip_coef_kernel
+// then reduces the partials in a fixed order (deterministic) and stores
+// out[0] = ||g||_2, out[1] = min(1, max_norm / (||g|| + 1e-6)) (NaN -> NaN,
+// as clip_grad_norm_ without error_if_nonfinite).  No host sync: the update
+// kernels read out[1] on the device.
+template <int DT>
+__global__ void __launch_bounds__(kThreads)
+grad_sumsq_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ chunks, float* __restrict__ partial) {
+  const int64_t s = chunks[2 * blockIdx.x], start = chunks[2 * blockIdx.x + 1];
+  const SegRow r = load_seg(seg, s);
+  const typename Elem<DT>::S* g = static_cast<const typename Elem<DT>::S*>(r.g);
+  float acc = 0.f;
+#pragma unroll
+  for (int it = 0; it < kIters; ++it) {
+    const int64_t e = start + it * kSpan + threadIdx.x * 8;
+    if (e >= r.n) break;
+    float gv[8];
+    load8g<DT>(g, e, r.n, r.vec, gv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = __fmaf_rn(gv[j], gv[j], acc);
+  }
+  __shared__ float red[kThreads / 64];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < kThreads / 64; ++i) t += red[i];
+    partial[blockIdx.x] = t;
+  }
+}
+
+__global__ void __launch_bounds__(1024) clip_coef_kernel(const float* __restrict__ partial, int64_t n, float max_norm,
+                                                         float* __restrict__ out) {
+  double acc = 0.0;  // fp64 across up to ~10^6 chunk partials
+  for (int64_t i = threadIdx.x; i < n; i += 1024) acc += partial[i];
+  __shared__ double red[1024 / 64];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < 1024 / 64; ++i) t += red[i];
+    const float norm = static_cast<float>(sqrt(t));
+    const float coef = max_norm / (norm + 1e-6f);
+    out[0] = norm;
+    out[1] = (coef != coef) ? coef : fminf(coef, 1.f);
+  }
+}
+
 // ------------------------------------------------------------ host launchers
 #define DLION_DISPATCH(dt, ...)                         \
   switch (dt) {                                         \
@@ -280,24 +350,25 @@ vote_reduce_kernel(const uint8_t* __restrict__ recv, int64_t nbytes, const uint8
 
 hipError_t launch_lion_local(int dt, const int64_t* seg, const int64_t* chunks, int64_t n_chunks,
                              float decay, float neg_lr, float b1, float omb1, float b2, float omb2,
-                             hipStream_t st) {
+                             const float* gscale, hipStream_t st) {
   if (n_chunks == 0) return hipSuccess;
   DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_local_kernel<DT>), dim3(n_chunks), dim3(kThreads), 0, st,
-                                        seg, chunks, decay, neg_lr, b1, omb1, b2, omb2));
+                                        seg, chunks, decay, neg_lr, b1, omb1, b2, omb2, gscale));
   return hipGetLastError();
 }
 
 hipError_t launch_lion_encode(int dt, const int64_t* seg, const int64_t* chunks, int64_t n_chunks,
                               uint8_t* bits, float b1, float omb1, float b2, float omb2, int update_m,
-                              int stochastic, float rr, uint64_t seed, uint32_t step, hipStream_t st) {
+                              int stochastic, float rr, uint64_t seed, uint32_t step, const float* gscale,
+                              hipStream_t st) {
   if (n_chunks == 0) return hipSuccess;
   const uint32_t lo = static_cast<uint32_t>(seed), hi = static_cast<uint32_t>(seed >> 32);
   if (stochastic) {
     DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_encode_kernel<DT, true>), dim3(n_chunks), dim3(kThreads), 0,
-                                          st, seg, chunks, bits, b1, omb1, b2, omb2, update_m, rr, lo, hi, step));
+                                          st, seg, chunks, bits, b1, omb1, b2, omb2, update_m, rr, lo, hi, step, gscale));
   } else {
     DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_encode_kernel<DT, false>), dim3(n_chunks), dim3(kThreads), 0,
-                                          st, seg, chunks, bits, b1, omb1, b2, omb2, update_m, rr, lo, hi, step));
+                                          st, seg, chunks, bits, b1, omb1, b2, omb2, update_m, rr, lo, hi, step, gscale));
   }
   return hipGetLastError();
 }
@@ -310,6 +381,19 @@ hipError_t launch_lion_vote_apply(int dt, const int64_t* seg, const int64_t* chu
   DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_vote_apply_kernel<DT>), dim3(n_chunks), dim3(kThreads), 0, st,
                                         seg, chunks, planes, plane_stride, alive, world, mode, tie, neg, decay,
                                         neg_lr, own, agree));
+  return hipGetLastError();
+}
+
+hipError_t launch_grad_sumsq(int dt, const int64_t* seg, const int64_t* chunks, int64_t n_chunks, float* partial,
+                             hipStream_t st) {
+  if (n_chunks == 0) return hipSuccess;
+  DLION_DISPATCH(dt, hipLaunchKernelGGL((grad_sumsq_kernel<DT>), dim3(n_chunks), dim3(kThreads), 0, st, seg, chunks,
+                                        partial));
+  return hipGetLastError();
+}
+
+hipError_t launch_clip_coef(const float* partial, int64_t n, float max_norm, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1024), 0, st, partial, n, max_norm, out);
   return hipGetLastError();
 }
 

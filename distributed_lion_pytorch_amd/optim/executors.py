@@ -43,16 +43,24 @@ class HipExecutor:
     def _chunk_off(self, b: Bucket) -> int:
         return self.plan.chunk_off + 2 * b.chunk_off
 
-    def local(self, meta, b: Bucket, hp: HParams, grads=None, moms=None) -> None:
+    def local(self, meta, b: Bucket, hp: HParams, grads=None, moms=None, gscale=None) -> None:
         self.ops.lion_local(meta, self.plan.seg_off, self._chunk_off(b), b.n_chunks, hip.DTYPE_CODE[b.dtype],
-                            hp.decay, -hp.lr, hp.beta1, 1.0 - hp.beta1, hp.beta2, 1.0 - hp.beta2)
+                            hp.decay, -hp.lr, hp.beta1, 1.0 - hp.beta1, hp.beta2, 1.0 - hp.beta2, gscale)
 
     def encode(self, meta, b: Bucket, bits: torch.Tensor, hp: HParams, update_m: bool = True,
                stochastic: bool = False, rr: float = 0.0, seed: int = 0, step: int = 0,
-               grads=None, moms=None) -> None:
+               grads=None, moms=None, gscale=None) -> None:
         self.ops.lion_encode(meta, self.plan.seg_off, self._chunk_off(b), b.n_chunks, hip.DTYPE_CODE[b.dtype], bits,
                              hp.beta1, 1.0 - hp.beta1, hp.beta2, 1.0 - hp.beta2, update_m, stochastic, rr,
-                             seed & 0x7FFFFFFFFFFFFFFF, step & 0xFFFFFFFF)
+                             seed & 0x7FFFFFFFFFFFFFFF, step & 0xFFFFFFFF, gscale)
+
+    def grad_sumsq(self, meta, b: Bucket, partial: torch.Tensor) -> None:
+        """partial[b.chunk_off + i] = sum of g^2 over chunk i of bucket b."""
+        self.ops.grad_sumsq(meta, self.plan.seg_off, self._chunk_off(b), b.n_chunks, hip.DTYPE_CODE[b.dtype],
+                            partial, b.chunk_off)
+
+    def clip_coef(self, partial: torch.Tensor, n: int, max_norm: float, out: torch.Tensor) -> None:
+        self.ops.clip_coef(partial, n, max_norm, out)
 
     def apply(self, meta, b: Bucket, planes: torch.Tensor, stride: int, alive: torch.Tensor, mode: int, tie: int,
               neg: Optional[torch.Tensor], hp: HParams, own: Optional[torch.Tensor] = None,
@@ -71,13 +79,15 @@ class TorchExecutor:
     def __init__(self, plan: FlatPlan):
         self.plan = plan
 
-    def local(self, meta, b: Bucket, hp: HParams, grads=None, moms=None) -> None:
+    def local(self, meta, b: Bucket, hp: HParams, grads=None, moms=None, gscale=None) -> None:
+        assert gscale is None, "the torch executor clips gradients in place (Lion.clip_grad_norm_)"
         for s in b.segments:
             ref.update_fn(s.param, grads[s.index], moms[s.index], hp.lr, hp.wd, hp.beta1, hp.beta2)
 
     def encode(self, meta, b: Bucket, bits: torch.Tensor, hp: HParams, update_m: bool = True,
                stochastic: bool = False, rr: float = 0.0, seed: int = 0, step: int = 0,
-               grads=None, moms=None) -> None:
+               grads=None, moms=None, gscale=None) -> None:
+        assert gscale is None, "the torch executor clips gradients in place (Lion.clip_grad_norm_)"
         gen = None
         if stochastic:
             gen = torch.Generator(device=bits.device)

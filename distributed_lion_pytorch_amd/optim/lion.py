@@ -199,13 +199,7 @@ class Lion(Optimizer):
                 "the vote collectives would mismatch")
 
     # --------------------------------------------------------------- step
-    @torch.no_grad()
-    def step(self, closure: Optional[Callable] = None):
-        loss = None
-        if closure is not None:
-            with torch.enable_grad():
-                loss = closure()
-
+    def _collect(self):
         entries, grads, moms = [], [], []
         for gi, group in enumerate(self.param_groups):
             for p in group["params"]:
@@ -220,6 +214,50 @@ class Lion(Optimizer):
                 entries.append((p, gi))
                 grads.append(g)
                 moms.append(state["exp_avg"])
+        return entries, grads, moms
+
+    @torch.no_grad()
+    def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
+        """Fused ``torch.nn.utils.clip_grad_norm_(params, max_norm)`` (L2) over
+        this optimizer's gradients.  On the HIP path the norm is one read of
+        every gradient through the update kernels' pointer table, the clip
+        coefficient stays on the device (no host sync) and the NEXT ``step()``
+        applies ``g * coef`` (rounded to the gradient dtype, exactly what the
+        in-place ``_foreach_mul_`` would have stored) inside its kernels --
+        instead of a separate read+write pass over all gradients (measured on
+        Llama-3-8B: 19.5 ms of foreach norm+mul per step).  The coefficient is
+        computed in fp32 (torch computes bf16 gradients' norms in bf16).  The
+        gradients themselves are left unscaled; call ``step()`` next.
+        Returns the total norm (0-dim device tensor)."""
+        entries, grads, moms = self._collect()
+        if not entries:
+            return torch.zeros(())
+        world, rank = self._world()
+        plan = self._get_plan(entries, world, rank)
+        ex = self._executor
+        if ex.name != "hip":
+            self._pending_gscale = None
+            return torch.nn.utils.clip_grad_norm_([p for p, _ in entries], max_norm)
+        meta = plan.meta(grads, moms)
+        n = plan.total_chunks
+        if getattr(self, "_clip_part", None) is None or self._clip_part.numel() < n or \
+                self._clip_part.device != plan.device:
+            self._clip_part = torch.empty(n, dtype=torch.float32, device=plan.device)
+            self._clip_out = torch.empty(2, dtype=torch.float32, device=plan.device)
+        for b in plan.buckets:
+            ex.grad_sumsq(meta, b, self._clip_part)
+        ex.clip_coef(self._clip_part, n, float(max_norm), self._clip_out)
+        self._pending_gscale = self._clip_out
+        return self._clip_out[0]
+
+    @torch.no_grad()
+    def step(self, closure: Optional[Callable] = None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+
+        entries, grads, moms = self._collect()
         if not entries:
             return loss
 
@@ -232,18 +270,19 @@ class Lion(Optimizer):
         hps = [HParams(lr=g["lr"], wd=g["weight_decay"], beta1=g["betas"][0], beta2=g["betas"][1])
                for g in self.param_groups]
 
+        gscale, self._pending_gscale = getattr(self, "_pending_gscale", None), None
         if world == 1:
             for b in plan.buckets:
-                ex.local(meta, b, hps[b.group], grads=grads, moms=moms)
+                ex.local(meta, b, hps[b.group], grads=grads, moms=moms, gscale=gscale)
         else:
-            self._distributed_step(plan, ex, meta, hps, grads, moms, world, rank)
+            self._distributed_step(plan, ex, meta, hps, grads, moms, world, rank, gscale)
         # the kernels wrote the weights through raw pointers (no autograd
         # version bump): invalidate derived per-step weight copies
         bump_weight_generation()
         self._n_steps += 1
         return loss
 
-    def _distributed_step(self, plan, ex, meta, hps, grads, moms, world, rank):
+    def _distributed_step(self, plan, ex, meta, hps, grads, moms, world, rank, gscale=None):
         xch = self._exchange
         alive = self._alive(world, plan.device)
         stochastic = self.max_grad_norm is not None
@@ -255,7 +294,7 @@ class Lion(Optimizer):
             hp = hps[b.group]
             rr = (1.0 + 1.0 / hp.beta1) * self.max_grad_norm if stochastic else 0.0
             ex.encode(meta, b, xch.send_view(b), hp, update_m=True, stochastic=stochastic, rr=rr, seed=seed,
-                      step=self._n_steps, grads=grads, moms=moms)
+                      step=self._n_steps, grads=grads, moms=moms, gscale=gscale)
             states.append(xch.launch(b, alive))
         states = [xch.advance(b, s, alive) for b, s in zip(plan.buckets, states)]
         for b, s in zip(plan.buckets, states):

@@ -106,6 +106,7 @@ class FlatPlan:
         self.seg_off = 0
         self.chunk_off = SEG_COLS * self.n_seg
         self._chunk_rows = chunk_rows
+        self.total_chunks = len(chunk_rows)
         self.meta_numel = self.chunk_off + 2 * len(chunk_rows)
         self._meta_dev: Optional[torch.Tensor] = None
         self._ptr_key = None

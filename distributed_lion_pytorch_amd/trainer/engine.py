@@ -11,6 +11,7 @@ majority vote.
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Callable, Iterable, Optional
 
@@ -62,6 +63,16 @@ class TrainStep:
             fuse_grad_accumulation = not isinstance(model, torch.nn.parallel.DistributedDataParallel)
         self.fuse_grad_accumulation = fuse_grad_accumulation
 
+    def _fused_clip(self) -> bool:
+        """Lion's fused clip covers exactly its own parameters: use it only when
+        those are the parameters being trained (else the norm would differ)."""
+        if not hasattr(self.optimizer, "clip_grad_norm_") or os.environ.get("DLION_FUSED_CLIP", "1") == "0":
+            return False
+        if not hasattr(self, "_fused_ok"):
+            mine = {id(p) for g in self.optimizer.param_groups for p in g["params"]}
+            self._fused_ok = mine == {id(p) for p in self.params}
+        return self._fused_ok
+
     def __call__(self, micro_batches: Iterable[dict]) -> torch.Tensor:
         from ..ops.linear import grad_accumulation_fusion
 
@@ -73,7 +84,11 @@ class TrainStep:
                 loss.backward()
                 total = loss.detach() if total is None else total + loss.detach()
         if self.max_grad_norm is not None and self.max_grad_norm > 0:
-            torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm, foreach=True)
+            if self._fused_clip():
+                # norm on device, scale applied inside the Lion update kernels
+                self.optimizer.clip_grad_norm_(self.max_grad_norm)
+            else:
+                torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm, foreach=True)
         self.optimizer.step()
         if self.scheduler is not None:
             self.scheduler.step()

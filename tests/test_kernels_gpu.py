@@ -212,3 +212,60 @@ def test_lion_optimizer_gpu_single_rank_matches_cpu_oracle(cuda):
     assert type(opt._executor).__name__ == "HipExecutor"
     for a, b in zip(net.parameters(), net_ref.parameters()):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_fused_clip_matches_prescaled_grads(dtype, cuda):
+    """grad_sumsq + clip_coef give the total L2 norm and clip_grad_norm_'s
+    coefficient on the device; the update kernels fed that coefficient equal
+    the same kernels run on gradients scaled in place (round(g * coef))."""
+    ps, gs, ms = _tensors(dtype, cuda, seed=5)
+    plan = FlatPlan([(p, 0) for p in ps], world=1, bucket_bytes=1 << 14, device=cuda)
+    hp = HParams(lr=1e-3, wd=0.1, beta1=0.9, beta2=0.99)
+    hx = HipExecutor(plan)
+    meta = plan.meta(gs, ms)
+    part = torch.empty(plan.total_chunks, dtype=torch.float32, device=cuda)
+    out = torch.empty(2, dtype=torch.float32, device=cuda)
+    for b in plan.buckets:
+        hx.grad_sumsq(meta, b, part)
+    max_norm = 1.0
+    hx.clip_coef(part, plan.total_chunks, max_norm, out)
+    norm = torch.linalg.vector_norm(torch.cat([g.double().reshape(-1) for g in gs]))
+    torch.testing.assert_close(out[0].double(), norm, rtol=1e-5, atol=0)
+    coef = min(1.0, max_norm / (out[0].item() + 1e-6))
+    assert abs(out[1].item() - coef) <= 1e-6 * coef
+    p0, m0 = _clone(ps), _clone(ms)
+    bits_a = torch.zeros(plan.total_bytes, dtype=torch.uint8, device=cuda)
+    bits_b = torch.zeros_like(bits_a)
+
+    # fused: local step + encode read g and scale on load
+    for b in plan.buckets:
+        hx.local(meta, b, hp, gscale=out)
+    pa, ma = _clone(ps), _clone(ms)
+    for t, s in zip(ms, m0):
+        t.copy_(s)
+    for b in plan.buckets:
+        hx.encode(meta, b, bits_a[b.byte_off:b.byte_off + b.nbytes], hp, gscale=out)
+    ma_enc = _clone(ms)
+    # reference: scale the gradients in place first, then the plain kernels
+    for t, s in zip(ps, p0):
+        t.copy_(s)
+    for t, s in zip(ms, m0):
+        t.copy_(s)
+    for g in gs:
+        g.copy_((g.float() * out[1]).to(dtype))
+    for b in plan.buckets:
+        hx.local(meta, b, hp)
+    pb, mb = _clone(ps), _clone(ms)
+    for t, s in zip(ms, m0):
+        t.copy_(s)
+    for b in plan.buckets:
+        hx.encode(meta, b, bits_b[b.byte_off:b.byte_off + b.nbytes], hp)
+    torch.cuda.synchronize()
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
+    for a, b in zip(ma, mb):
+        assert torch.equal(a, b)
+    for a, b in zip(ma_enc, ms):
+        assert torch.equal(a, b)
+    assert torch.equal(bits_a, bits_b)

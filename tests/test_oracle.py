@@ -158,3 +158,22 @@ def test_stochastic_bits_probability_clamped():
     assert bits.all()
     bits = ref.stochastic_bits(-gr, m, 0.9, max_grad_norm=1.0)
     assert not bits.any()
+
+
+def test_lion_clip_grad_norm_cpu_matches_torch():
+    """CPU (torch executor): Lion.clip_grad_norm_ is torch's clip_grad_norm_
+    over the optimizer's gradients (in place), then step() as usual."""
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(n)) for n in (5, 300, 64)]
+    qs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    for p, q in zip(ps, qs):
+        p.grad = torch.randn_like(p) * 3
+        q.grad = p.grad.clone()
+    a, b = Lion(ps, lr=1e-2, weight_decay=0.1), Lion(qs, lr=1e-2, weight_decay=0.1)
+    na = a.clip_grad_norm_(1.0)
+    nb = torch.nn.utils.clip_grad_norm_(qs, 1.0)
+    torch.testing.assert_close(na, nb)
+    a.step()
+    b.step()
+    for p, q in zip(ps, qs):
+        assert torch.equal(p, q)
