@@ -92,6 +92,9 @@ def parse():
     ap.add_argument("--dropout", type=float, default=None, help="override GPT-2 dropout (default 0.1)")
     ap.add_argument("--profile_dir", default=None)
     ap.add_argument("--rocm_fa", default=None, help="PyTorch SDPA flash library on ROCm: ck | aotriton")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend; gloo (with ranks sharing GPUs) only to rehearse the multi-rank "
+                         "path on a 1-GPU box -- RCCL refuses two ranks on one device")
     a = ap.parse_args()
     for k, v in PRESETS[a.task].items():
         if getattr(a, k, None) is None:
@@ -106,11 +109,16 @@ def setup_dist(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
     return world, rank, dev
 
 
