@@ -439,10 +439,16 @@ def reference_attention(q, k, v, dropout_p: float = 0.0, seed: int = 0) -> torch
 
 # ------------------------------------------------- LM head + cross-entropy
 def _pad_rows(w: torch.Tensor, mult: int = 64) -> torch.Tensor:
+    """Vocabulary rows padded to a multiple of 64, cached per optimizer step
+    for parameters (the same padded copy serves every micro-batch)."""
     v = w.shape[0]
     vp = (v + mult - 1) // mult * mult
     if vp == v:
         return w
+    if isinstance(w, torch.nn.Parameter):
+        from .linear import cached_derived
+
+        return cached_derived(w, "pad_rows", lambda t: torch.cat([t, t.new_zeros(vp - v, t.shape[1])], 0))
     return torch.cat([w, w.new_zeros(vp - v, w.shape[1])], 0)
 
 

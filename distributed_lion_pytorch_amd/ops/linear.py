@@ -135,27 +135,34 @@ def wgrad(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 # bump), hence the explicit generation counter bumped by Lion.step; any other
 # in-place update (AdamW, load_state_dict) bumps the tensor's _version.
 _WEIGHT_GEN = [0]
-_WT_CACHE: dict = {}  # id(w) -> (weakref(w), key, w^T); entries die with w
+_WT_CACHE: dict = {}  # (id(w), tag) -> (weakref(w), key, derived tensor); entries die with w
 
 
 def bump_weight_generation() -> None:
     _WEIGHT_GEN[0] += 1
 
 
-def transposed_weight(w: torch.Tensor) -> torch.Tensor:
-    """Contiguous w.t() cached until w changes (next optimizer step)."""
+def cached_derived(w: torch.Tensor, tag: str, fn) -> torch.Tensor:
+    """fn(w.detach()) cached until w changes (in place or via the next Lion
+    step).  Used for per-step weight layouts (transposed, vocab-padded)."""
     import weakref
 
     key = (w._version, _WEIGHT_GEN[0], w.data_ptr())
-    hit = _WT_CACHE.get(id(w))
+    ck = (id(w), tag)
+    hit = _WT_CACHE.get(ck)
     if hit is not None and hit[0]() is w and hit[1] == key:
         return hit[2]
     with torch.no_grad():
-        wt = w.detach().t().contiguous()
+        out = fn(w.detach())
     if hit is None or hit[0]() is not w:
-        weakref.finalize(w, _WT_CACHE.pop, id(w), None)
-    _WT_CACHE[id(w)] = (weakref.ref(w), key, wt)
-    return wt
+        weakref.finalize(w, _WT_CACHE.pop, ck, None)
+    _WT_CACHE[ck] = (weakref.ref(w), key, out)
+    return out
+
+
+def transposed_weight(w: torch.Tensor) -> torch.Tensor:
+    """Contiguous w.t() cached until w changes (next optimizer step)."""
+    return cached_derived(w, "t", lambda t: t.t().contiguous())
 
 
 class _LinearKN(torch.autograd.Function):
