@@ -101,17 +101,31 @@ __device__ __forceinline__ f32x16 zero16() {
 }
 
 // ------------------------------------------------------------- LDS tiles
-// A 32-row x D tile, rows padded by 8 bf16 (D=64: 144-byte rows; the 16-row
-// ds_read_b128 row reads then cover all 64 banks once).
-constexpr int kPad = 8;
+// A 32-row x D tile, unpadded rows, 16-byte chunks XOR-swizzled per row so
+// that all three access patterns are bank-conflict-free (guide T2/T10; model
+// and check: tools/lds_bank_sim.py): the ds_read_b128 row reads of the
+// 32x32x16 operand (16 lanes = 16 rows, one chunk), the ds_read_b64_tr_b16
+// transposed reads (a 32-lane half = 4 rows x 4 chunks) and the ds_write_b128
+// staging stores.  The first layout (rows padded by 8 bf16) left the
+// transposed reads 2-way (D=64) / 4-way (D=128): SQ_LDS_BANK_CONFLICT was 50%
+// of the LDS-active cycles at D=128.
 template <int D>
-using LdsTile = __bf16[32][D + kPad];
+using LdsTile = __bf16[32 * D];
+
+template <int D>
+__device__ __forceinline__ int swz_chunk(int row, int ch) {
+  if constexpr (D == 128) return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
+  else return ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
+}
+// element offset of 16-byte chunk `ch` of row `row`
+template <int D>
+__device__ __forceinline__ int lds_off(int row, int ch) { return row * D + 8 * swz_chunk<D>(row, ch); }
 
 // row fragment: row `r` of the tile, columns 16ks + 8hf .. +7 (an operand whose
 // m / n index is the lane's row, k = the D axis)
 template <int D>
 __device__ __forceinline__ bf16x8 row_frag(const LdsTile<D>& t, int r, int ks, int hf) {
-  return *reinterpret_cast<const bf16x8*>(&t[r][16 * ks + 8 * hf]);
+  return *reinterpret_cast<const bf16x8*>(&t[lds_off<D>(r, 2 * ks + hf)]);
 }
 // transposed fragment: column d = 32tt + (lane & 31) of the tile, rows in the
 // permuted-k order of acc_frag(s2): {0..3, 8..11} + 4hf + 16s2.  Two
@@ -121,10 +135,10 @@ __device__ __forceinline__ bf16x8 row_frag(const LdsTile<D>& t, int r, int ks, i
 template <int D>
 __device__ __forceinline__ bf16x8 tr_frag(const LdsTile<D>& t, int s2, int tt, int lane) {
   const int j = lane & 15, hf = lane >> 5, gh = (lane >> 4) & 1;
-  const __bf16* p0 = &t[16 * s2 + 4 * hf + (j >> 2)][32 * tt + 16 * gh + 4 * (j & 3)];
+  const int row = 16 * s2 + 4 * hf + (j >> 2), ch = 4 * tt + 2 * gh + ((j & 3) >> 1), sub = 4 * (j & 1);
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 8 * (D + kPad)));
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&t[lds_off<D>(row, ch) + sub]));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&t[lds_off<D>(row + 8, ch) + sub]));
   // assemble as whole dwords: per-element bf16 inserts of the builtin's result
   // miscompile (only dword 0 of each read survived, replicated by v_perm)
   const i32x2 l2 = __builtin_bit_cast(i32x2, lo), h2 = __builtin_bit_cast(i32x2, hi);
@@ -132,24 +146,56 @@ __device__ __forceinline__ bf16x8 tr_frag(const LdsTile<D>& t, int s2, int tt, i
   return __builtin_bit_cast(bf16x8, r);
 }
 
-// cooperative global -> registers -> LDS staging of one 32 x D tile
+// LDS-DMA staging of one 32 x D tile (global_load_lds_dwordx4, guide §5 /
+// T3): each wave moves 1 KiB pieces (64 lanes x 16 B) straight into LDS, so
+// the tile costs no staging VGPRs, no ds_write and -- the point -- the fetch
+// is issued where it is written, a whole tile ahead of its use.  (The
+// register-staged version had its global loads sunk past the branchy compute
+// block to just before their ds_write, and for D=128 the staging registers
+// were even kept in scratch: every tile paid the full fetch latency.)  A
+// piece lands lane-linear at base + 16*lane, so the swizzle of lds_off goes on
+// the SOURCE side: LDS chunk slot p = row*CPR + pos holds source chunk
+// swz_chunk(row, pos) (the XOR is an involution).
+//
+// Issued through inline asm, not __builtin_amdgcn_global_load_lds: for the
+// builtin hipcc cannot tell the DMA's LDS buffer (buf^1) from the one the
+// math reads (buf) and puts an s_waitcnt vmcnt(0) before the first ds_read,
+// serialising the prefetch again.  The asm is invisible to its waitcnt pass,
+// so every consumer goes through vm_wait0() + barrier; the compiler's own
+// counted vmcnt waits stay correct (ops issued later only make a vmcnt(N)
+// stricter).  M0 = the wave-uniform LDS destination.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p)));
+}
+__device__ __forceinline__ void glds16(const __bf16* src, const void* dst) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr(dst)));
+}
+__device__ __forceinline__ void glds4(const float* src, const void* dst) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(lds_addr(dst)));
+}
+// vmcnt(0) through the builtin (gfx9 encoding: lgkmcnt 15, expcnt 7, vmcnt 0),
+// not asm: the waitcnt pass then knows the Q/K/V register loads issued
+// before it are complete, instead of re-waiting for them with counted vmcnt
+// inside the loop -- which, counting the asm DMAs too, drained the prefetch
+__device__ __forceinline__ void vm_wait0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 template <int D>
-struct RowTile {
-  static constexpr int CH = 32 * D / 8, PT = (CH + 255) / 256;  // 16-byte chunks
-  uint4 reg[PT];
-  __device__ __forceinline__ void load(const __bf16* base, int64_t stride) {
-#pragma unroll
-    for (int i = 0; i < PT; ++i) {
-      const int c = threadIdx.x + 256 * i, row = c / (D / 8), col = (c % (D / 8)) * 8;
-      if (c < CH) reg[i] = *reinterpret_cast<const uint4*>(base + static_cast<int64_t>(row) * stride + col);
-    }
+struct DmaTile {
+  static constexpr int CPR = D / 8, PPW = D / 64;  // 16-byte chunks per row, 1 KiB pieces per wave
+  static_assert(D == 64 || D == 128, "head dim");
+  int off0, off1, lds;  // source element offsets (tile-relative) of the lane's chunks; wave's LDS byte offset
+  __device__ __forceinline__ DmaTile(int64_t stride) {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int p0 = 64 * PPW * w + lane, p1 = p0 + 64;
+    off0 = static_cast<int>((p0 / CPR) * stride) + 8 * swz_chunk<D>(p0 / CPR, p0 % CPR);
+    off1 = static_cast<int>((p1 / CPR) * stride) + 8 * swz_chunk<D>(p1 / CPR, p1 % CPR);
+    lds = 1024 * PPW * w;
   }
-  __device__ __forceinline__ void store(LdsTile<D>& t) const {
-#pragma unroll
-    for (int i = 0; i < PT; ++i) {
-      const int c = threadIdx.x + 256 * i, row = c / (D / 8), col = (c % (D / 8)) * 8;
-      if (c < CH) *reinterpret_cast<uint4*>(&t[row][col]) = reg[i];
-    }
+  __device__ __forceinline__ void issue(const __bf16* tile, LdsTile<D>& t) const {
+    char* dst = reinterpret_cast<char*>(&t[0]) + lds;
+    glds16(tile + off0, dst);
+    if constexpr (PPW == 2) glds16(tile + off1, dst + 1024);
   }
 };
 
@@ -191,19 +237,19 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 
   const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
   const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
-  RowTile<D> kr, vr;
   const uint32_t arow = drop_row(a.seed, bh, q);
   const uint32_t thr_hi = a.thresh16 << 16;
-  kr.load(kg, a.k_st);
-  vr.load(vg, a.v_st);
-  kr.store(ks_[0]);
-  vr.store(vs_[0]);
+  const DmaTile<D> kd(a.k_st), vd(a.v_st);
+  kd.issue(kg, ks_[0]);
+  vd.issue(vg, vs_[0]);
+  vm_wait0();
   __syncthreads();
   for (int kt = 0; kt <= last; ++kt) {
     const int buf = kt & 1;
-    if (kt < last) {
-      kr.load(kg + static_cast<int64_t>((kt + 1) * 32) * a.k_st, a.k_st);
-      vr.load(vg + static_cast<int64_t>((kt + 1) * 32) * a.v_st, a.v_st);
+    if (kt < last) {  // next tile into the other buffer (last read before the previous barrier)
+      const int64_t nxt = static_cast<int64_t>((kt + 1) * 32);
+      kd.issue(kg + nxt * a.k_st, ks_[buf ^ 1]);
+      vd.issue(vg + nxt * a.v_st, vs_[buf ^ 1]);
     }
     if (blk.active && kt <= qtile) {  // wave-uniform
       const int kb = kt * 32;
@@ -258,10 +304,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
         for (int t = 0; t < D / 32; ++t) oacc[t] = mfma32(tr_frag<D>(vs_[buf], s2, t, lane), pf, oacc[t]);
       }
     }
-    if (kt < last) {
-      kr.store(ks_[buf ^ 1]);
-      vr.store(vs_[buf ^ 1]);
-    }
+    vm_wait0();  // this wave's pieces of the next tile have landed
     __syncthreads();
   }
   if (!blk.active) return;
@@ -310,17 +353,17 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   for (int t = 0; t < D / 32; ++t) dq[t] = zero16();
   const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
   const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
-  RowTile<D> kr, vr;
-  kr.load(kg, a.k_st);
-  vr.load(vg, a.v_st);
-  kr.store(ks_[0]);
-  vr.store(vs_[0]);
+  const DmaTile<D> kd(a.k_st), vd(a.v_st);
+  kd.issue(kg, ks_[0]);
+  vd.issue(vg, vs_[0]);
+  vm_wait0();
   __syncthreads();
   for (int kt = 0; kt <= last; ++kt) {
     const int buf = kt & 1;
-    if (kt < last) {
-      kr.load(kg + static_cast<int64_t>((kt + 1) * 32) * a.k_st, a.k_st);
-      vr.load(vg + static_cast<int64_t>((kt + 1) * 32) * a.v_st, a.v_st);
+    if (kt < last) {  // next tile into the other buffer (last read before the previous barrier)
+      const int64_t nxt = static_cast<int64_t>((kt + 1) * 32);
+      kd.issue(kg + nxt * a.k_st, ks_[buf ^ 1]);
+      vd.issue(vg + nxt * a.v_st, vs_[buf ^ 1]);
     }
     if (blk.active && kt <= qtile) {
       const int kb = kt * 32;
@@ -353,10 +396,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
         for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tr_frag<D>(ks_[buf], s2, t, lane), dq[t]);  // dQ += dS K
       }
     }
-    if (kt < last) {
-      kr.store(ks_[buf ^ 1]);
-      vr.store(vs_[buf ^ 1]);
-    }
+    vm_wait0();  // this wave's pieces of the next tile have landed
     __syncthreads();
   }
   if (!blk.active) return;
@@ -407,35 +447,32 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
     dv[t] = zero16();
   }
   const uint32_t thr_hi = a.thresh16 << 16, kshift = (key & 1) ? 0u : 16u;
-  RowTile<D> qr, dr;
-  float lsr = 0.f;                 // threads 0..95 stage lse (0..31) / delta (32..63) / drop_row (64..95)
+  const DmaTile<D> qd(a.q_st), dd(a.o_st);
   const int nq = ntiles - first;   // query tiles per head
   const int total = group * nq;    // (head, query tile) steps, head-major
-  auto gload = [&](int i) {
+  // step i -> buffer i&1: Q and dO tiles by LDS-DMA; wave 0 also DMAs the 32
+  // lse (lanes 0..31) and delta (lanes 32..63) values into ls_[buf][0..1];
+  // with dropout, wave 1 writes the 32 per-row hash keys into ls_[buf][2]
+  auto stage = [&](int i, int buf) {
     const int gh = i / nq, qt = first + i % nq;
     const int h = hk * group + gh, bh = b * a.H + h;
     const int64_t qrow = static_cast<int64_t>(qt * 32);
-    qr.load(a.q + b * a.q_sb + h * a.q_sh + qrow * a.q_st, a.q_st);
-    dr.load(a.dout + b * a.o_sb + h * a.o_sh + qrow * a.o_st, a.o_st);
-    if (threadIdx.x < 64) {
-      const float* src = (threadIdx.x < 32 ? a.lse : a.delta) + static_cast<int64_t>(bh) * a.T + qt * 32;
-      lsr = src[threadIdx.x & 31];
-    } else if (DROP && threadIdx.x < 96) {
-      lsr = __uint_as_float(drop_row(a.seed, bh, qt * 32 + (threadIdx.x & 31)));
+    qd.issue(a.q + b * a.q_sb + h * a.q_sh + qrow * a.q_st, qs_[buf]);
+    dd.issue(a.dout + b * a.o_sb + h * a.o_sh + qrow * a.o_st, ds_[buf]);
+    if (w == 0) {
+      const float* src = (lane < 32 ? a.lse : a.delta) + static_cast<int64_t>(bh) * a.T + qt * 32 + (lane & 31);
+      glds4(src, &ls_[buf][0][0]);
+    } else if (DROP && w == 1 && lane < 32) {
+      ls_[buf][2][lane] = __uint_as_float(drop_row(a.seed, bh, qt * 32 + lane));
     }
   };
-  auto swrite = [&](int buf) {
-    qr.store(qs_[buf]);
-    dr.store(ds_[buf]);
-    if (threadIdx.x < (DROP ? 96 : 64)) ls_[buf][threadIdx.x >> 5][threadIdx.x & 31] = lsr;
-  };
   const uint32_t kmix = (static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u;
-  gload(0);
-  swrite(0);
+  stage(0, 0);
+  vm_wait0();
   __syncthreads();
   for (int i = 0; i < total; ++i) {
     const int buf = i & 1;
-    if (i + 1 < total) gload(i + 1);
+    if (i + 1 < total) stage(i + 1, buf ^ 1);
     const int qt = first + i % nq;
     if (active && qt >= ktile) {  // wave-uniform
       const int qb = qt * 32;
@@ -488,7 +525,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
         }
       }
     }
-    if (i + 1 < total) swrite(buf ^ 1);
+    vm_wait0();
     __syncthreads();
   }
   if (!active) return;
