@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--lr", type=float, default=1e-5)
     ap.add_argument("--weight_decay", type=float, default=0.0)
     ap.add_argument("--gradient_checkpointing", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo on cuda: rehearse N ranks on fewer GPUs (ranks share cuda:local%%ngpu)")
     return ap.parse_args()
 
 
@@ -59,9 +61,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.device == "cuda":
+        if a.backend == "gloo":
+            local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
         dtype = torch.bfloat16
     else:
         dev = torch.device("cpu")
@@ -71,7 +78,8 @@ def main():
         raise SystemExit("--drop_rank 0: rank 0 may host the rendezvous store; drop another rank")
     cfg = load_config(a.model)
     torch.manual_seed(0)
-    model = build_model(cfg, native=True).to(device=dev, dtype=dtype)
+    with torch.device(dev):  # materialise on the device (8B: no 32 GB host copy per rank)
+        model = build_model(cfg, native=True).to(dtype=dtype)
     if a.gradient_checkpointing:
         model.gradient_checkpointing_enable()
     broadcast_parameters(model)
@@ -98,6 +106,8 @@ def main():
         w = opt.last_world
         log.append({"step": s, "world": w, "loss": float(loss), "s": dt,
                     "tokens_per_s": w * a.grad_accum * a.micro_batch * a.seq_len / dt})
+        if rank == 0:
+            print(json.dumps({"progress": log[-1]}), file=sys.stderr, flush=True)
     # survivors: compare replicas inside the shrunken group
     h = hashlib.sha256()
     for p in model.parameters():
