@@ -48,11 +48,13 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   return x;
 }
 // drop hash: 32 random bits shared by keys (2i, 2i+1) of query q, in two
-// stages so the per-element cost is one 32-bit multiply (v_mul_lo_u32 is a
-// slow multi-cycle op; the first version's two per pair cost ~20% of the
-// backward):
+// stages so the per-pair cost is one full-rate 24-bit multiply (v_mul_lo_u32
+// is a quarter-rate op and the attention kernels are VALU-bound at D=64: ~22
+// VALU instructions per MFMA; the first version's two per pair cost ~20% of
+// the backward):
 //   arow(bh, q)  = lowbias32(seed ^ bh*0x9E3779B9 ^ q*0x85EBCA6B)   (per row)
-//   hash(q, key) = mix1(arow ^ (key>>1)*0xC2B2AE35),  mix1(x) = y ^ (y >> 16), y = x*0x7FEB352D
+//   hash(q, key) = mix1(arow ^ (key>>1)*0xC2B2AE35),
+//   mix1(x) = y ^ (y >> 16),  y = (x mod 2^24) * 0x9E3779  (v_mul_u32_u24)
 // low 16 bits for the even key.  Keep tests run in the high half (one shift
 // for the low half, none for the high one): with thr_hi = thresh16 << 16,
 //   keep(even) = (hash << 16) >= thr_hi,  keep(odd) = hash >= thr_hi.
@@ -60,7 +62,7 @@ __device__ __forceinline__ uint32_t drop_row(uint32_t seed, uint32_t bh, uint32_
   return lowbias32(seed ^ (bh * 0x9E3779B9u) ^ (q * 0x85EBCA6Bu));
 }
 __device__ __forceinline__ uint32_t mix1(uint32_t x) {
-  x *= 0x7feb352du;
+  x = __umul24(x, 0x9E3779u);
   return x ^ (x >> 16);
 }
 
@@ -204,7 +206,7 @@ struct QBlock {
   int bh, qtile, last;
   bool active;
   __device__ __forceinline__ QBlock(int nbh, int ntiles) {
-    const int ngroups = (ntiles + 3) >> 2, w = threadIdx.x >> 6;
+    const int ngroups = (ntiles + 3) >> 2, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches
     bh = static_cast<int>(blockIdx.x % nbh);
     const int grp = ngroups - 1 - static_cast<int>(blockIdx.x / nbh);
     qtile = grp * 4 + w;
@@ -319,7 +321,11 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
       for (int i = 0; i < 4; ++i) wv[i] = static_cast<__bf16>(oacc[t][4 * g + i] * inv_l);
       *reinterpret_cast<bf16x4*>(op + 32 * t + 8 * g + 4 * hf) = wv;
     }
-  if (hf == 0) a.lse[static_cast<int64_t>(bh) * a.T + q] = m + log2f(l);
+  // under dropout the stored row constant is lse + log2(1-p): the backward's
+  // exp2(s*scale - lse') is then P/(1-p) directly, and with delta' = delta*(1-p)
+  // (attn_delta_kernel) both backward kernels drop their per-element 1/(1-p)
+  // multiplies: dS = P'*(keep ? dP : 0) - P'*delta', Pd = keep ? P' : 0
+  if (hf == 0) a.lse[static_cast<int64_t>(bh) * a.T + q] = m + log2f(l) + (DROP ? -log2f(a.inv_keep) : 0.f);
 }
 
 // --------------------------------------------------------------- backward dQ
@@ -373,6 +379,11 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
         s = mfma32(row_frag<D>(ks_[buf], r, ks, hf), qf[ks], s);    // S^T  = K Q^T
         dp = mfma32(row_frag<D>(vs_[buf], r, ks, hf), dof[ks], dp);  // dP^T = V dO^T
       }
+      if (kt == qtile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+          if (kb + acc_row(reg, hf) > q) s[reg] = -INFINITY;
+      }
 #pragma unroll
       for (int reg = 0; reg < 16; reg += 2) {
         const int key = kb + acc_row(reg, hf);  // even: regs (reg, reg+1) = keys (key, key+1)
@@ -381,11 +392,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const int kk = key + e;
-          const float p = (kt == qtile && kk > q)
-                              ? 0.f
-                              : __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg + e], a.scale_log2, -lse2));
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg + e], a.scale_log2, -lse2));
           float dpv = dp[reg + e];
-          if constexpr (DROP) dpv = ((e == 0 ? hsh << 16 : hsh) >= thr_hi) ? dpv * a.inv_keep : 0.f;
+          if constexpr (DROP) dpv = ((e == 0 ? hsh << 16 : hsh) >= thr_hi) ? dpv : 0.f;  // p, dlt carry 1/(1-p)
           s[reg + e] = p * (dpv - dlt);  // dS^T
         }
       }
@@ -420,7 +429,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) LdsTile<D> qs_[2];
   __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[2];
   __shared__ __attribute__((aligned(16))) float ls_[2][3][32];  // [buf][lse | delta | drop row key][row]
-  const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntiles = a.T >> 5, nbhk = a.B * a.Hkv;
   const int bhk = static_cast<int>(blockIdx.x % nbhk);
   const int grp = static_cast<int>(blockIdx.x / nbhk);
@@ -497,19 +506,22 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
           ar_r[4 * g] = av.x; ar_r[4 * g + 1] = av.y; ar_r[4 * g + 2] = av.z; ar_r[4 * g + 3] = av.w;
         }
       }
+      if (qt == ktile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+          if (key > qb + acc_row(reg, hf)) s[reg] = -INFINITY;
+      }
       f32x16 pd;
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
-        const int qq = qb + acc_row(reg, hf);
-        const float p = (qt == ktile && key > qq)
-                            ? 0.f
-                            : __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -lse_r[reg]));
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -lse_r[reg]));
         float dpv = dp[reg];
         float pdv = p;
-        if constexpr (DROP) {  // the lane is the key here: one (cheap) hash per element
+        if constexpr (DROP) {  // the lane is the key here: one (cheap) hash per element;
+                               // p and the delta row values already carry 1/(1-p)
           const bool kp_ = (mix1(ar_r[reg] ^ kmix) << kshift) >= thr_hi;
-          dpv = kp_ ? dpv * a.inv_keep : 0.f;
-          pdv = kp_ ? p * a.inv_keep : 0.f;
+          dpv = kp_ ? dpv : 0.f;
+          pdv = kp_ ? p : 0.f;
         }
         pd[reg] = pdv;
         s[reg] = p * (dpv - dl_r[reg]);  // dS
@@ -560,7 +572,7 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(AttnArgs a) {
   for (int j = 0; j < 8; ++j) acc += static_cast<float>(o[j]) * static_cast<float>(d[j]);
 #pragma unroll
   for (int s = LPR / 2; s > 0; s >>= 1) acc += __shfl_xor(acc, s, LPR);
-  if (sub == 0) const_cast<float*>(a.delta)[row] = acc;
+  if (sub == 0) const_cast<float*>(a.delta)[row] = a.thresh16 ? acc / a.inv_keep : acc;  // delta * (1-p), see fwd
 }
 
 // ------------------------------------------------------------------ launchers

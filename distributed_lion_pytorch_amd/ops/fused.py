@@ -413,8 +413,8 @@ def attention_dropout_keep(B: int, H: int, T: int, p: float, seed: int, device=N
     key = torch.arange(T, device=device, dtype=torch.int64).view(1, 1, T)
     # per-(head, query) row key: full hash; per key pair: one multiply round
     arow = _lowbias32(((bh * 0x9E3779B9) & _M32) ^ ((q * 0x85EBCA6B) & _M32) ^ (seed & _M32))
-    x = ((arow ^ (((key >> 1) * 0xC2B2AE35) & _M32)) * 0x7FEB352D) & _M32
-    x = x ^ (x >> 16)
+    x = ((arow ^ (((key >> 1) * 0xC2B2AE35) & _M32)) & 0xFFFFFF) * 0x9E3779  # v_mul_u32_u24
+    x = (x & _M32) ^ ((x & _M32) >> 16)
     u16 = (x >> ((key & 1) * 16)) & 0xFFFF
     return (u16 >= th).view(B, H, T, T)
 

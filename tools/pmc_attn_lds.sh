@@ -2,7 +2,7 @@
 # and GPT-2 (D=64) shapes.  One counter pass per run (rocprofv3 --pmc, kernel trace only).
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp
 out=gpurun_out/pmc_attn_lds; rm -rf $out; mkdir -p $out
-C="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA"
+C="${PMC_COUNTERS:-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA}"
 timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d $out -o llama --pmc $C \
   -- python3 tools/bench_attention.py 4 2048 32 128 0.0 > $out/llama.txt 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d $out -o gpt2 --pmc $C \
