@@ -241,6 +241,121 @@ lion_vote_apply_kernel(const int64_t* __restrict__ seg, const int64_t* __restric
   }
 }
 
+// K2, word-sliced: one dword per live plane per 32 coordinates, the vote as
+// bit-sliced counters.  The byte version above is latency-bound at W > 1 (a runtime loop
+// of dependent byte loads per plane, 64-bit spreads): 2.0 TB/s effective at
+// W = 8.  Here every plane word is loaded up front, each plane costs 7 bitwise
+// ops per 32 coordinates (a 4-bit vertical counter), and the majority is a
+// bit-sliced compare with floor(n_live / 2).  Majority (mode 0) for W <= 15
+// and pre-voted bitmaps (mode 2); mode 1 and wider worlds use the byte kernel.
+constexpr int kMaxSliced = 15;
+
+// Majority over up to 15 planes for 32 coordinates at once: a 4-bit vertical
+// counter per bit position (7 bitwise ops per plane), then count vs
+// K = floor(n_live / 2) compared bit-sliced from the MSB.  pos / neg follow the
+// byte kernels' rules (ties by `tie`, nobody alive -> neither).
+__device__ __forceinline__ void sliced_vote(const uint32_t (&w)[kMaxSliced], int world, int n_live, int tie,
+                                            uint32_t& pos, uint32_t& neg) {
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#pragma unroll
+  for (int k = 0; k < kMaxSliced; ++k) {
+    if (k >= world) break;  // uniform
+    const uint32_t x = w[k];
+    const uint32_t t0 = c0 & x;
+    c0 ^= x;
+    const uint32_t t1 = c1 & t0;
+    c1 ^= t0;
+    const uint32_t t2 = c2 & t1;
+    c2 ^= t1;
+    c3 ^= t2;
+  }
+  const int K = n_live >> 1;
+  uint32_t gt = 0, eq = 0xffffffffu;
+  const uint32_t cb[4] = {c0, c1, c2, c3};
+#pragma unroll
+  for (int b = 3; b >= 0; --b) {
+    if ((K >> b) & 1) {
+      eq &= cb[b];
+    } else {
+      gt |= eq & cb[b];
+      eq &= ~cb[b];
+    }
+  }
+  if (n_live == 0) {
+    pos = neg = 0;  // nobody voted: weight decay only
+  } else if (n_live & 1) {
+    pos = gt;  // count > K  <=>  2*count > n_live
+    neg = ~gt;
+  } else {
+    const uint32_t lt = ~(gt | eq);
+    pos = gt | (tie == 2 ? eq : 0u);
+    neg = lt | (tie == 0 ? eq : 0u);
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(kThreads)
+lion_vote_apply32_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ chunks,
+                         const uint8_t* __restrict__ planes, int64_t plane_stride,
+                         const uint8_t* __restrict__ alive, int world, int mode, int tie,
+                         const uint8_t* __restrict__ neg_plane, float decay, float neg_lr,
+                         const uint8_t* __restrict__ own, unsigned long long* __restrict__ agree) {
+  using E = Elem<DT>;
+  using S = typename E::S;
+  const int64_t s = chunks[2 * blockIdx.x], start = chunks[2 * blockIdx.x + 1];
+  const SegRow r = load_seg(seg, s);
+  S* p = const_cast<S*>(static_cast<const S*>(r.p));
+  int n_live = 0;
+  uint32_t live_mask = 0;
+  for (int k = 0; k < world && k < kMaxSliced; ++k)
+    if (alive[k]) {
+      live_mask |= 1u << k;
+      ++n_live;
+    }
+  uint32_t n_agree = 0;
+  // Each lane owns 8 consecutive coordinates (coalesced 16-byte p accesses,
+  // as in K0); the 4 lanes of a 32-coordinate group load the same plane dword
+  // and vote on all of it, then keep their byte.
+  const int sub = threadIdx.x & 3;  // bit_off % 2048 == 0, start % 8192 == 0
+#pragma unroll
+  for (int it = 0; it < kIters; ++it) {
+    const int64_t e = start + it * kSpan + threadIdx.x * 8;
+    if (e >= r.n) break;
+    const int64_t word = (r.bit_off + e) >> 5;
+    uint32_t pos, neg;
+    if (mode == 2) {
+      pos = reinterpret_cast<const uint32_t*>(planes)[word];
+      neg = neg_plane ? reinterpret_cast<const uint32_t*>(neg_plane)[word] : ~pos;
+    } else {
+      uint32_t w[kMaxSliced];
+#pragma unroll
+      for (int k = 0; k < kMaxSliced; ++k)  // every live plane's load first
+        w[k] = (live_mask >> k) & 1 ? reinterpret_cast<const uint32_t*>(planes + k * plane_stride)[word] : 0u;
+      sliced_vote(w, world, n_live, tie, pos, neg);
+    }
+    pos = (pos >> (8 * sub)) & 0xffu;
+    neg = (neg >> (8 * sub)) & 0xffu;
+    if (agree != nullptr) {
+      const uint32_t mine = own[(r.bit_off + e) >> 3];
+      const int64_t left = r.n - e;
+      const uint32_t valid = left >= 8 ? 0xffu : ((1u << left) - 1u);
+      n_agree += __popc(((mine & pos) | (~mine & neg)) & valid);
+    }
+    float pv[8];
+    load8g<DT>(p, e, r.n, r.vec, pv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float delta = static_cast<float>(static_cast<int>((pos >> j) & 1) - static_cast<int>((neg >> j) & 1));
+      pv[j] = __fmaf_rn(neg_lr, delta, E::rnd(pv[j] * decay));
+    }
+    store8g<DT>(p, e, r.n, r.vec, pv);
+  }
+  if (agree != nullptr) {
+    for (int off = 32; off > 0; off >>= 1) n_agree += __shfl_xor(n_agree, off);
+    if ((threadIdx.x & 63) == 0) atomicAdd(agree, static_cast<unsigned long long>(n_agree));
+  }
+}
+
 // ----------------------------------------------------------------------- K4
 // recv: [W][nbytes] shards gathered by all_to_all; out: voted positive bits;
 // neg_out (optional): voted negative bits (only needed when ties map to 0).
@@ -251,6 +366,22 @@ vote_reduce_kernel(const uint8_t* __restrict__ recv, int64_t nbytes, const uint8
   const int64_t nwords = nbytes >> 2;  // nbytes % 4 == 0 guaranteed by the planner
   int n_live = 0;
   for (int k = 0; k < world; ++k) n_live += alive[k] != 0;
+  if (world <= kMaxSliced) {  // bit-sliced counters, every plane word loaded up front
+    uint32_t live_mask = 0;
+    for (int k = 0; k < world; ++k) live_mask |= static_cast<uint32_t>(alive[k] != 0) << k;
+    for (int64_t w = blockIdx.x * (int64_t)kThreads + threadIdx.x; w < nwords;
+         w += (int64_t)gridDim.x * kThreads) {
+      uint32_t v[kMaxSliced];
+#pragma unroll
+      for (int k = 0; k < kMaxSliced; ++k)
+        v[k] = (live_mask >> k) & 1 ? reinterpret_cast<const uint32_t*>(recv + k * nbytes)[w] : 0u;
+      uint32_t pos, ng;
+      sliced_vote(v, world, n_live, tie, pos, ng);
+      reinterpret_cast<uint32_t*>(out)[w] = pos;
+      if (neg_out != nullptr) reinterpret_cast<uint32_t*>(neg_out)[w] = ng;
+    }
+    return;
+  }
   for (int64_t w = blockIdx.x * (int64_t)kThreads + threadIdx.x; w < nwords;
        w += (int64_t)gridDim.x * kThreads) {
     uint32_t cnt[32];
@@ -378,6 +509,12 @@ hipError_t launch_lion_vote_apply(int dt, const int64_t* seg, const int64_t* chu
                                   int mode, int tie, const uint8_t* neg, float decay, float neg_lr,
                                   const uint8_t* own, unsigned long long* agree, hipStream_t st) {
   if (n_chunks == 0) return hipSuccess;
+  if (mode == 2 || (mode == 0 && world <= kMaxSliced)) {
+    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_vote_apply32_kernel<DT>), dim3(n_chunks), dim3(kThreads), 0, st,
+                                          seg, chunks, planes, plane_stride, alive, world, mode, tie, neg, decay,
+                                          neg_lr, own, agree));
+    return hipGetLastError();
+  }
   DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_vote_apply_kernel<DT>), dim3(n_chunks), dim3(kThreads), 0, st,
                                         seg, chunks, planes, plane_stride, alive, world, mode, tie, neg, decay,
                                         neg_lr, own, agree));
