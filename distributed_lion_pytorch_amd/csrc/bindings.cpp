@@ -399,47 +399,91 @@ Tensor colsum_partials(const Tensor& x, int64_t parts) {
 }
 
 // ---------------------------------------------------------------- SwiGLU / RoPE
-void check_same(const Tensor& a, const Tensor& b, const char* what) {
-  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.is_contiguous(), "dlion ", what,
-              ": inputs must be contiguous bf16 GPU tensors");
-  TORCH_CHECK(b.is_cuda() && b.scalar_type() == at::kBFloat16 && b.is_contiguous() && b.sizes() == a.sizes(),
-              "dlion ", what, ": operand shapes / dtypes differ");
-  TORCH_CHECK(a.numel() % 8 == 0, "dlion ", what, ": numel must be a multiple of 8");
+// [..., F] bf16 GPU tensor whose leading dims collapse to `rows` rows at a
+// uniform row stride `ld` (unit column stride): contiguous tensors and column
+// slices of a fused [..., 2F] projection output both qualify.
+void rows_of(const Tensor& t, const char* what, int64_t& rows, int64_t& ld) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() >= 2 && t.stride(-1) == 1, "dlion ", what,
+              ": operands must be bf16 GPU tensors [..., F] with unit column stride");
+  ld = t.stride(-2);
+  rows = 1;
+  for (int64_t i = 0; i < t.dim() - 1; ++i) rows *= t.size(i);
+  for (int64_t i = 0; i + 2 < t.dim(); ++i)
+    TORCH_CHECK(t.size(i) == 1 || t.stride(i) == t.stride(i + 1) * t.size(i + 1), "dlion ", what,
+                ": leading dims must collapse to rows of one stride");
+  TORCH_CHECK(t.size(-1) % 8 == 0 && ld % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "dlion ",
+              what, ": F, the row stride and the base must be 16-byte aligned");
+}
+
+void check_pair(const Tensor& g, const Tensor& u, int64_t& rows, int64_t& ld) {
+  rows_of(g, "swiglu", rows, ld);
+  int64_t r2, ld2;
+  rows_of(u, "swiglu", r2, ld2);
+  TORCH_CHECK(g.sizes() == u.sizes() && ld == ld2, "dlion swiglu: gate / up shapes or strides differ");
 }
 
 Tensor swiglu_fwd(const Tensor& g, const Tensor& u) {
-  check_same(g, u, "swiglu");
+  int64_t rows, ld;
+  check_pair(g, u, rows, ld);
   const c10::DeviceGuard dg(g.device());
-  auto h = at::empty_like(g);
-  check_hip(dlion::launch_swiglu_fwd(g.data_ptr(), u.data_ptr(), h.data_ptr(), g.numel(), cur_stream()), "swiglu_fwd");
+  auto h = at::empty(g.sizes(), g.options());
+  check_hip(dlion::launch_swiglu_fwd(g.data_ptr(), u.data_ptr(), h.data_ptr(), rows, g.size(-1), ld, cur_stream()),
+            "swiglu_fwd");
   return h;
 }
 
 std::tuple<Tensor, Tensor> swiglu_bwd(const Tensor& dh, const Tensor& g, const Tensor& u) {
-  check_same(g, u, "swiglu");
-  check_same(g, dh, "swiglu");
+  int64_t rows, ld;
+  check_pair(g, u, rows, ld);
+  TORCH_CHECK(dh.is_contiguous() && dh.sizes() == g.sizes() && dh.scalar_type() == at::kBFloat16,
+              "dlion swiglu: dh must be contiguous bf16 of the gate's shape");
   const c10::DeviceGuard dg(g.device());
-  auto dgate = at::empty_like(g), dup = at::empty_like(u);
+  const int64_t F = g.size(-1);
+  auto dgate = at::empty(g.sizes(), g.options()), dup = at::empty(g.sizes(), g.options());
   check_hip(dlion::launch_swiglu_bwd(dh.data_ptr(), g.data_ptr(), u.data_ptr(), dgate.data_ptr(), dup.data_ptr(),
-                                     g.numel(), cur_stream()),
+                                     rows, F, ld, F, cur_stream()),
             "swiglu_bwd");
   return {dgate, dup};
 }
 
-// x [B, T, H, D] contiguous, cos / sin [>= T, D] bf16 (row t = position t)
+// gradient of a fused [gate | up] projection output: one [..., 2F] tensor
+// (dgate in the first F columns, dup in the last F)
+Tensor swiglu_bwd_fused(const Tensor& dh, const Tensor& g, const Tensor& u) {
+  int64_t rows, ld;
+  check_pair(g, u, rows, ld);
+  TORCH_CHECK(dh.is_contiguous() && dh.sizes() == g.sizes() && dh.scalar_type() == at::kBFloat16,
+              "dlion swiglu: dh must be contiguous bf16 of the gate's shape");
+  const c10::DeviceGuard dg(g.device());
+  const int64_t F = g.size(-1);
+  auto shape = g.sizes().vec();
+  shape.back() = 2 * F;
+  auto dgu = at::empty(shape, g.options());
+  auto* base = static_cast<uint16_t*>(dgu.data_ptr());
+  check_hip(dlion::launch_swiglu_bwd(dh.data_ptr(), g.data_ptr(), u.data_ptr(), base, base + F, rows, F, ld, 2 * F,
+                                     cur_stream()),
+            "swiglu_bwd_fused");
+  return dgu;
+}
+
+// x [B, T, H, D] with unit-stride heads (stride(2) == D) and any token stride
+// (a q or k slice of a fused projection output), cos / sin [>= T, D] bf16
+// (row t = position t); y contiguous.
 Tensor rope(const Tensor& x, const Tensor& cos, const Tensor& sin, bool inverse) {
-  TORCH_CHECK(x.dim() == 4 && x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(),
-              "dlion rope: x must be a contiguous bf16 [B, T, H, D] GPU tensor");
+  TORCH_CHECK(x.dim() == 4 && x.is_cuda() && x.scalar_type() == at::kBFloat16, "dlion rope: x must be bf16 [B, T, H, D]");
   const int64_t B = x.size(0), T = x.size(1), H = x.size(2), D = x.size(3);
+  TORCH_CHECK(x.stride(3) == 1 && x.stride(2) == D && (B == 1 || x.stride(0) == T * x.stride(1)) &&
+                  x.stride(1) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "dlion rope: x must have contiguous heads and a uniform, 16-byte aligned token stride");
   TORCH_CHECK(D % 8 == 0, "dlion rope: head_dim must be a multiple of 8");
   for (const Tensor* t : {&cos, &sin})
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->dim() == 2 &&
                     t->size(0) >= T && t->size(1) == D,
                 "dlion rope: cos/sin must be contiguous bf16 [>=T, D]");
   const c10::DeviceGuard dg(x.device());
-  auto y = at::empty_like(x);
+  auto y = at::empty(x.sizes(), x.options());
   check_hip(dlion::launch_rope(x.data_ptr(), cos.data_ptr(), sin.data_ptr(), y.data_ptr(), B * T,
-                               static_cast<int>(T), static_cast<int>(H), static_cast<int>(D), inverse, cur_stream()),
+                               static_cast<int>(T), static_cast<int>(H), static_cast<int>(D), inverse, x.stride(1),
+                               H * D, cur_stream()),
             "rope");
   return y;
 }
@@ -508,6 +552,7 @@ TORCH_LIBRARY(dlion, m) {
   m.def("gemm_nt_gelu(Tensor a, Tensor b, Tensor bias, bool exact) -> (Tensor, Tensor)");
   m.def("swiglu_fwd(Tensor g, Tensor u) -> Tensor");
   m.def("swiglu_bwd(Tensor dh, Tensor g, Tensor u) -> (Tensor, Tensor)");
+  m.def("swiglu_bwd_fused(Tensor dh, Tensor g, Tensor u) -> Tensor");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, bool inverse) -> Tensor");
   m.def(
       "add_norm_fwd(Tensor x, Tensor? y, Tensor? bias, Tensor gamma, Tensor? beta, float eps, bool rms, float p,"
@@ -561,6 +606,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("colsum_partials", &colsum_partials);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
+  m.impl("swiglu_bwd_fused", &swiglu_bwd_fused);
   m.impl("rope", &rope);
   m.impl("gemm_nt", &gemm_nt);
   m.impl("gemm_nt_out", &gemm_nt_out);

@@ -157,13 +157,19 @@ __device__ __forceinline__ float sigmoid_f(float a) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-a * 1.4426950408889634f));
 }
 
+// Row geometry: rows x F, inputs g / u at row stride ld_in (the two halves of a
+// fused [gate | up] projection output, ld_in = 2F, need no copy), h / dh
+// contiguous, dg / du at row stride ld_out (2F: straight into the fused
+// projection's input-gradient buffer).
 __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ u,
-                                                        uint16_t* __restrict__ h, int64_t n8) {
+                                                        uint16_t* __restrict__ h, int64_t n8, int64_t f8,
+                                                        int64_t ld_in) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n8;
        i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t src = (i / f8) * ld_in + (i % f8) * 8;
     float gv[8], uv[8], o[8];
-    Elem<kBF16>::load8(g + i * 8, gv);
-    Elem<kBF16>::load8(u + i * 8, uv);
+    Elem<kBF16>::load8(g + src, gv);
+    Elem<kBF16>::load8(u + src, uv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = gv[j] * sigmoid_f(gv[j]) * uv[j];
     Elem<kBF16>::store8(h + i * 8, o);
@@ -173,21 +179,24 @@ __global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restr
 __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restrict__ dh,
                                                         const uint16_t* __restrict__ g,
                                                         const uint16_t* __restrict__ u, uint16_t* __restrict__ dg,
-                                                        uint16_t* __restrict__ du, int64_t n8) {
+                                                        uint16_t* __restrict__ du, int64_t n8, int64_t f8,
+                                                        int64_t ld_in, int64_t ld_out) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n8;
        i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t row = i / f8, c = (i % f8) * 8;
+    const int64_t src = row * ld_in + c, dst = row * ld_out + c;
     float dv[8], gv[8], uv[8], og[8], ou[8];
     Elem<kBF16>::load8(dh + i * 8, dv);
-    Elem<kBF16>::load8(g + i * 8, gv);
-    Elem<kBF16>::load8(u + i * 8, uv);
+    Elem<kBF16>::load8(g + src, gv);
+    Elem<kBF16>::load8(u + src, uv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float sg = sigmoid_f(gv[j]);
       ou[j] = dv[j] * gv[j] * sg;
       og[j] = dv[j] * uv[j] * sg * (1.f + gv[j] * (1.f - sg));
     }
-    Elem<kBF16>::store8(dg + i * 8, og);
-    Elem<kBF16>::store8(du + i * 8, ou);
+    Elem<kBF16>::store8(dg + dst, og);
+    Elem<kBF16>::store8(du + dst, ou);
   }
 }
 
@@ -214,15 +223,18 @@ __device__ __forceinline__ void store4(uint16_t* p, const float (&o)[4]) {
 // their partners in the second half.
 __global__ void __launch_bounds__(256) rope_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ cs,
                                                   const uint16_t* __restrict__ sn, uint16_t* __restrict__ y,
-                                                  int64_t rows, int T, int H, int D, bool inverse) {
+                                                  int64_t rows, int T, int H, int D, bool inverse, int64_t x_ld,
+                                                  int64_t y_ld) {
   const int hd = D / 2, q = hd / 4;  // quads per half
   const int64_t n = rows * H * q;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * 256) {
     const int d0 = static_cast<int>(i % q) * 4;
     const int64_t rh = i / q;  // row * H + head
-    const int t = static_cast<int>((rh / H) % T);
-    const int64_t o = rh * D;
+    const int64_t row = rh / H;
+    const int t = static_cast<int>(row % T);
+    const int64_t o = row * x_ld + (rh % H) * D;   // token rows may be strided (slices of a fused
+    const int64_t oy = row * y_ld + (rh % H) * D;  // q|k|v projection output / input gradient)
     float a[4], b[4], ca[4], cb[4], sa[4], sb[4], oa[4], ob[4];
     load4(x + o + d0, a);
     load4(x + o + hd + d0, b);
@@ -240,8 +252,8 @@ __global__ void __launch_bounds__(256) rope_kernel(const uint16_t* __restrict__ 
         ob[j] = b[j] * cb[j] - a[j] * sa[j];
       }
     }
-    store4(y + o + d0, oa);
-    store4(y + o + hd + d0, ob);
+    store4(y + oy + d0, oa);
+    store4(y + oy + hd + d0, ob);
   }
 }
 
@@ -346,28 +358,31 @@ hipError_t launch_colsum(const void* x, float* part, int parts, int64_t rows, in
   return hipGetLastError();
 }
 
-hipError_t launch_swiglu_fwd(const void* g, const void* u, void* h, int64_t n, hipStream_t st) {
-  if (n % 8 != 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, st, static_cast<const uint16_t*>(g),
-                     static_cast<const uint16_t*>(u), static_cast<uint16_t*>(h), n / 8);
+hipError_t launch_swiglu_fwd(const void* g, const void* u, void* h, int64_t rows, int64_t F, int64_t ld_in,
+                             hipStream_t st) {
+  if (F % 8 != 0 || ld_in % 8 != 0) return hipErrorInvalidValue;
+  const int64_t n8 = rows * F / 8;
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(n8, 256)), dim3(256), 0, st, static_cast<const uint16_t*>(g),
+                     static_cast<const uint16_t*>(u), static_cast<uint16_t*>(h), n8, F / 8, ld_in);
   return hipGetLastError();
 }
 
-hipError_t launch_swiglu_bwd(const void* dh, const void* g, const void* u, void* dg, void* du, int64_t n,
-                             hipStream_t st) {
-  if (n % 8 != 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, st, static_cast<const uint16_t*>(dh),
+hipError_t launch_swiglu_bwd(const void* dh, const void* g, const void* u, void* dg, void* du, int64_t rows,
+                             int64_t F, int64_t ld_in, int64_t ld_out, hipStream_t st) {
+  if (F % 8 != 0 || ld_in % 8 != 0 || ld_out % 8 != 0) return hipErrorInvalidValue;
+  const int64_t n8 = rows * F / 8;
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(n8, 256)), dim3(256), 0, st, static_cast<const uint16_t*>(dh),
                      static_cast<const uint16_t*>(g), static_cast<const uint16_t*>(u), static_cast<uint16_t*>(dg),
-                     static_cast<uint16_t*>(du), n / 8);
+                     static_cast<uint16_t*>(du), n8, F / 8, ld_in, ld_out);
   return hipGetLastError();
 }
 
 hipError_t launch_rope(const void* x, const void* cos, const void* sin, void* y, int64_t rows, int T, int H, int D,
-                       bool inverse, hipStream_t st) {
-  if (D % 8 != 0 || T <= 0) return hipErrorInvalidValue;
+                       bool inverse, int64_t x_ld, int64_t y_ld, hipStream_t st) {
+  if (D % 8 != 0 || T <= 0 || x_ld % 4 != 0 || y_ld % 4 != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(rope_kernel, dim3(grid_for(rows * H * (D / 8), 256)), dim3(256), 0, st,
                      static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(cos),
-                     static_cast<const uint16_t*>(sin), static_cast<uint16_t*>(y), rows, T, H, D, inverse);
+                     static_cast<const uint16_t*>(sin), static_cast<uint16_t*>(y), rows, T, H, D, inverse, x_ld, y_ld);
   return hipGetLastError();
 }
 

@@ -44,11 +44,12 @@ hipError_t launch_bias_gelu_fwd(const void* z, const void* b, void* h, int64_t r
                                 hipStream_t st);
 hipError_t launch_bias_gelu_bwd(const void* dh, const void* z, const void* b, void* dz, float* dbpart, int parts,
                                 int64_t rows, int N, bool exact, hipStream_t st);
-hipError_t launch_swiglu_fwd(const void* g, const void* u, void* h, int64_t n, hipStream_t st);
-hipError_t launch_swiglu_bwd(const void* dh, const void* g, const void* u, void* dg, void* du, int64_t n,
+hipError_t launch_swiglu_fwd(const void* g, const void* u, void* h, int64_t rows, int64_t F, int64_t ld_in,
                              hipStream_t st);
+hipError_t launch_swiglu_bwd(const void* dh, const void* g, const void* u, void* dg, void* du, int64_t rows,
+                             int64_t F, int64_t ld_in, int64_t ld_out, hipStream_t st);
 hipError_t launch_rope(const void* x, const void* cos, const void* sin, void* y, int64_t rows, int T, int H, int D,
-                       bool inverse, hipStream_t st);
+                       bool inverse, int64_t x_ld, int64_t y_ld, hipStream_t st);
 hipError_t launch_sum_partials(const float* part, int S, int64_t n, int64_t ld, void* out, bool accumulate,
                                hipStream_t st);
 hipError_t launch_colsum(const void* x, float* part, int parts, int64_t rows, int N, hipStream_t st);

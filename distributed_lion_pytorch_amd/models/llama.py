@@ -20,7 +20,7 @@ from transformers import LlamaConfig, PreTrainedModel
 from transformers.modeling_outputs import CausalLMOutputWithPast
 
 from ..ops import fused
-from ..ops.linear import linear_nk
+from ..ops.linear import linear_multi_nk, linear_nk
 
 LLAMA_SIZES = {
     "llama-2-7b": dict(hidden_size=4096, intermediate_size=11008, num_hidden_layers=32, num_attention_heads=32,
@@ -106,9 +106,10 @@ class LlamaAttention(nn.Module):
 
     def forward(self, x, cos, sin):
         B, T, _ = x.shape
-        q = _lin(self.q_proj, x).view(B, T, self.n_head, self.head_dim)
-        k = _lin(self.k_proj, x).view(B, T, self.n_kv, self.head_dim)
-        v = _lin(self.v_proj, x).view(B, T, self.n_kv, self.head_dim)
+        q, k, v = _proj(x, (self.q_proj, self.k_proj, self.v_proj))
+        q = q.view(B, T, self.n_head, self.head_dim)
+        k = k.view(B, T, self.n_kv, self.head_dim)
+        v = v.view(B, T, self.n_kv, self.head_dim)
         q, k = apply_rope(q, cos, sin), apply_rope(k, cos, sin)
         y = fused.causal_attention_gqa(q, k, v, self.attn_dropout if self.training else 0.0)
         return _lin(self.o_proj, y)
@@ -121,6 +122,29 @@ def _lin(layer: nn.Module, x):
     return layer(x)
 
 
+def _proj(x, layers):
+    """Projections sharing the input x (q/k/v, gate/up) as ONE GEMM on the
+    concatenated weights (ops/linear.py linear_multi_nk); LoRA-wrapped layers
+    contribute their frozen base weight to the fused GEMM and add their
+    adapter path to their own output.  Falls back to one GEMM per layer off the
+    GPU, with biases, or for unknown wrappers."""
+    from .lora import LoraLinear
+
+    bases = []
+    for layer in layers:
+        if type(layer) is nn.Linear and layer.bias is None:
+            bases.append(layer.weight)
+        elif isinstance(layer, LoraLinear) and layer.base_layer.bias is None:
+            bases.append(layer.base_layer.weight)
+        else:
+            return tuple(_lin(layer, x) for layer in layers)
+    if not x.is_cuda or len({w.dtype for w in bases}) != 1:
+        return tuple(_lin(layer, x) for layer in layers)
+    outs = linear_multi_nk(x, bases)
+    return tuple(layer.lora_delta(x) + o if isinstance(layer, LoraLinear) and not layer.merged else o
+                 for layer, o in zip(layers, outs))
+
+
 class LlamaMLP(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
@@ -129,7 +153,8 @@ class LlamaMLP(nn.Module):
         self.down_proj = nn.Linear(cfg.intermediate_size, cfg.hidden_size, bias=False)
 
     def forward(self, x):
-        return _lin(self.down_proj, fused.swiglu(_lin(self.gate_proj, x), _lin(self.up_proj, x)))
+        g, u = _proj(x, (self.gate_proj, self.up_proj))
+        return _lin(self.down_proj, fused.swiglu(g, u))
 
 
 class LlamaDecoderLayer(nn.Module):

@@ -60,11 +60,15 @@ class LoraLinear(nn.Module):
     def weight(self):
         return self.base_layer.weight
 
+    def lora_delta(self, x):
+        """The adapter path alone: dropout(x) A^T B^T * (alpha / r)."""
+        return self.lora_B(self.lora_A(self.dropout(x))) * self.scaling
+
     def forward(self, x):
         y = linear_nk(x, self.base_layer.weight, self.base_layer.bias)
         if self.merged:
             return y
-        return y + self.lora_B(self.lora_A(self.dropout(x))) * self.scaling
+        return y + self.lora_delta(x)
 
     @torch.no_grad()
     def merge(self):

@@ -80,16 +80,31 @@ class _Rope(torch.autograd.Function):
         return hip.ops().rope(dy.contiguous(), cos, sin, True), None, None
 
 
+def _token_strided_ok(x: torch.Tensor) -> bool:
+    """[B, T, H, D] with contiguous heads and one 16-byte aligned token stride
+    (a q / k column slice of a fused projection output): the kernel reads it
+    in place."""
+    B, T, H, D = x.shape
+    return (x.stride(3) == 1 and x.stride(2) == D and (B == 1 or x.stride(0) == T * x.stride(1))
+            and x.stride(1) % 8 == 0 and x.data_ptr() % 16 == 0)
+
+
 def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
     """x [B, T, H, D]; cos/sin [>=T, D]; HF rotate-half convention."""
     if (x.dtype == torch.bfloat16 and cos.dtype == torch.bfloat16 and sin.dtype == torch.bfloat16
             and x.shape[-1] % 8 == 0 and _use_hip(x)):
+        if not _token_strided_ok(x):
+            x = x.contiguous()
         with torch.autocast("cuda", enabled=False):
-            return _Rope.apply(x.contiguous(), cos.contiguous(), sin.contiguous())
+            return _Rope.apply(x, cos.contiguous(), sin.contiguous())
     return rope_reference(x, cos, sin)
 
 
 class _SwiGLU(torch.autograd.Function):
+    """gate / up may be the two column halves of one fused projection output
+    (row stride 2F): read in place, and the backward then writes [dgate | dup]
+    as one buffer, which the fused projection's backward takes without a copy."""
+
     @staticmethod
     def forward(ctx, gate, up):
         ctx.save_for_backward(gate, up)
@@ -98,6 +113,11 @@ class _SwiGLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh):
         gate, up = ctx.saved_tensors
+        F_ = gate.shape[-1]
+        if (gate.stride(-2) == 2 * F_ and up.data_ptr() == gate.data_ptr() + F_ * gate.element_size()
+                and up.stride() == gate.stride()):
+            dgu = hip.ops().swiglu_bwd_fused(dh.contiguous(), gate, up)
+            return dgu[..., :F_], dgu[..., F_:]
         dg, du = hip.ops().swiglu_bwd(dh.contiguous(), gate, up)
         return dg, du
 
@@ -109,10 +129,19 @@ def swiglu(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
 
         gate, up = autocast_inputs(gate, up)
     if (gate.dtype == torch.bfloat16 and up.dtype == torch.bfloat16 and gate.shape == up.shape
-            and gate.numel() % 8 == 0 and _use_hip(gate)):
+            and gate.shape[-1] % 8 == 0 and _use_hip(gate)):
+        if not (_rows_ok(gate) and up.stride() == gate.stride()):
+            gate, up = gate.contiguous(), up.contiguous()
         with torch.autocast("cuda", enabled=False):
-            return _SwiGLU.apply(gate.contiguous(), up.contiguous())
+            return _SwiGLU.apply(gate, up)
     return F.silu(gate) * up
+
+
+def _rows_ok(t: torch.Tensor) -> bool:
+    """[..., F] whose leading dims collapse to rows of one 16-byte aligned stride."""
+    if t.dim() < 2 or t.stride(-1) != 1 or t.stride(-2) % 8 or t.data_ptr() % 16:
+        return False
+    return all(t.shape[i] == 1 or t.stride(i) == t.stride(i + 1) * t.shape[i + 1] for i in range(t.dim() - 2))
 
 
 # ------------------------------------------------------------- dropout + add

@@ -223,6 +223,154 @@ class _LinearNK(torch.autograd.Function):
         return dx, dw, db
 
 
+# ------------------------------------------------- fused projections (one GEMM)
+_CAT_CACHE: dict = {}  # tuple(id(w)) -> (weakrefs, key, concatenated weight)
+
+
+def cat_weights(ws) -> torch.Tensor:
+    """[W1; W2; ...] along the output dim, cached until any of them changes
+    (in place, or via the next Lion step: see bump_weight_generation)."""
+    import weakref
+
+    if len(ws) == 1:
+        return ws[0]
+    ck = tuple(id(w) for w in ws)
+    key = (_WEIGHT_GEN[0],) + tuple((w._version, w.data_ptr()) for w in ws)
+    hit = _CAT_CACHE.get(ck)
+    if hit is not None and all(r() is w for r, w in zip(hit[0], ws)) and hit[1] == key:
+        return hit[2]
+    with torch.no_grad():
+        out = torch.cat([w.detach() for w in ws], 0)
+    if hit is None:
+        weakref.finalize(ws[0], _CAT_CACHE.pop, ck, None)
+    _CAT_CACHE[ck] = ([weakref.ref(w) for w in ws], key, out)
+    return out
+
+
+def _adjacent_views(ts):
+    """If ts are consecutive column blocks of one row-major buffer (e.g. the
+    fused SwiGLU backward's [dgate | dup]), return that [..., sum n] view."""
+    t0 = ts[0]
+    if any(t is None for t in ts) or t0.dim() < 2 or t0.stride(-1) != 1:
+        return None
+    n = sum(t.shape[-1] for t in ts)
+    off = 0
+    for t in ts:
+        if (t.shape[:-1] != t0.shape[:-1] or t.stride() != t0.stride() or t.dtype != t0.dtype
+                or t.data_ptr() != t0.data_ptr() + off * t0.element_size()
+                or t.untyped_storage().data_ptr() != t0.untyped_storage().data_ptr()):
+            return None
+        off += t.shape[-1]
+    if t0.stride(-2) != n:
+        return None
+    return t0.as_strided(t0.shape[:-1] + (n,), t0.stride())
+
+
+class _LinearMultiNK(torch.autograd.Function):
+    """[y1 | y2 | ...] = x @ [W1; W2; ...]^T as ONE GEMM for projections that
+    share their input (Llama q/k/v, gate/up); the outputs are column views of
+    the fused result.  Backward: one input-gradient GEMM on the concatenated
+    output gradient (zero-copy when the consumers wrote it as one buffer) and
+    one weight-gradient GEMM whose row blocks are the per-weight gradients.
+    Measured at Llama-3-8B shapes (tools/bench_fused_proj.py): q/k/v fwd+dgrad+
+    wgrad 1155 -> 958 us, gate/up 4590 -> 4242 us per layer -- the k/v
+    projections alone (1024 outputs) fill only half of the 256 CUs."""
+
+    @staticmethod
+    def forward(ctx, x2d, *ws):
+        sizes = [w.shape[0] for w in ws]
+        y = torch.nn.functional.linear(x2d, cat_weights(ws))
+        ctx.save_for_backward(x2d, *ws)
+        ctx.sizes = sizes
+        ctx.fuse = [_fuse_target(w) for w in ws]
+        ctx.params = [w if f else None for w, f in zip(ws, ctx.fuse)]
+        return tuple(y.split(sizes, dim=-1))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        x2d, *ws = ctx.saved_tensors
+        grads = [torch.zeros(x2d.shape[0], n, dtype=x2d.dtype, device=x2d.device) if g is None else g
+                 for g, n in zip(grads, ctx.sizes)]
+        dy = _adjacent_views(grads)
+        if dy is None:
+            dy = torch.cat([g.reshape(-1, g.shape[-1]) for g in grads], -1)
+        dy = dy.reshape(-1, dy.shape[-1])
+        dx = dy @ cat_weights(ws) if ctx.needs_input_grad[0] else None
+        dws = [None] * len(ws)
+        want = [ctx.needs_input_grad[1 + i] for i in range(len(ws))]
+        if any(want):
+            if all(ctx.fuse) and all(want):
+                _multi_wgrad_into(dy, x2d, ctx.params, ctx.sizes)
+            else:
+                dwc = wgrad(dy, x2d)  # [sum n, K]; its row blocks are contiguous
+                off = 0
+                for i, n in enumerate(ctx.sizes):
+                    if want[i]:
+                        blk = dwc[off:off + n]
+                        if ctx.fuse[i]:
+                            p = ctx.params[i]
+                            p.grad = blk if p.grad is None else p.grad.add_(blk)
+                        else:
+                            dws[i] = blk
+                    off += n
+        return (dx, *dws)
+
+
+def _multi_wgrad_into(dy, x2d, params, sizes) -> None:
+    """params[i].grad (+)= (dy[:, block i])^T x2d for every block, one GEMM."""
+    M, N = dy.shape
+    K = x2d.shape[1]
+    s = split_k_factor(M, N, K)
+    if s > 1 and (N * K) % 4 == 0 and M % s == 0:
+        from . import hip
+
+        if hip.available():
+            part = torch.bmm(dy.view(s, M // s, N).transpose(1, 2), x2d.view(s, M // s, K), out_dtype=torch.float32)
+            flat = part.view(s, N * K)
+            off = 0
+            for p, n in zip(params, sizes):
+                deposit_grad(p, flat[:, off * K:(off + n) * K])
+                off += n
+            return
+    gs = [p.grad for p in params]
+    base = _adjacent_rows(gs) if all(g is not None for g in gs) else None
+    if base is not None:  # every grad is a row block of one buffer (the first micro-batch made it)
+        base.addmm_(dy.t(), x2d)
+        return
+    dwc = dy.t() @ x2d
+    off = 0
+    for p, n in zip(params, sizes):
+        blk = dwc[off:off + n]
+        p.grad = blk if p.grad is None else p.grad.add_(blk)
+        off += n
+
+
+def _adjacent_rows(ts):
+    t0 = ts[0]
+    if not all(t.is_contiguous() and t.dtype == t0.dtype and t.shape[1:] == t0.shape[1:] for t in ts):
+        return None
+    off = 0
+    for t in ts:
+        if (t.data_ptr() != t0.data_ptr() + off * t0.stride(0) * t0.element_size()
+                or t.untyped_storage().data_ptr() != t0.untyped_storage().data_ptr()):
+            return None
+        off += t.shape[0]
+    return t0.as_strided((off,) + tuple(t0.shape[1:]), t0.stride())
+
+
+def linear_multi_nk(x: torch.Tensor, ws) -> tuple:
+    """(x @ W1^T, x @ W2^T, ...) for nn.Linear-layout weights sharing the input
+    x, as one fused GEMM (CUDA) -- outputs are column views of one buffer."""
+    x2d = x.reshape(-1, x.shape[-1])
+    lead = x.shape[:-1]
+    if not x.is_cuda:
+        return tuple(torch.nn.functional.linear(x2d, w).view(lead + (w.shape[0],)) for w in ws)
+    x2d, *ws = autocast_inputs(x2d, *ws)
+    with torch.autocast("cuda", enabled=False):
+        outs = _LinearMultiNK.apply(x2d, *ws)
+    return tuple(o.view(lead + (o.shape[-1],)) for o in outs)
+
+
 def autocast_inputs(*ts):
     """Under autocast (HF ``--bf16``/``--fp16``), cast the floating inputs of a
     custom op to the autocast dtype with differentiable casts, so the op itself

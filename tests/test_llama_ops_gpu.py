@@ -90,3 +90,66 @@ def test_rope(D, cuda):
     y.backward(dy)
     yr.backward(dy.float())
     assert _rel(x.grad, xr.grad) < 1e-2
+
+
+def test_swiglu_on_fused_halves_and_fused_grad(cuda):
+    """gate/up as the two column halves of one [.., 2F] buffer: read in place,
+    backward returns [dgate | dup] as views of one buffer; matches fp32."""
+    hip.require()
+    torch.manual_seed(3)
+    B, T, F = 2, 16, 96
+    gu = torch.randn(B, T, 2 * F, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    g, u = gu[..., :F], gu[..., F:]
+    h = fused.swiglu(g, u)
+    dh = torch.randn_like(h)
+    h.backward(dh)
+    ref = gu.detach().float().requires_grad_(True)
+    hr = torch.nn.functional.silu(ref[..., :F]) * ref[..., F:]
+    hr.backward(dh.float())
+    torch.testing.assert_close(h.float(), hr, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(gu.grad.float(), ref.grad, rtol=3e-2, atol=3e-2)
+
+
+def test_rope_strided_token_rows(cuda):
+    """q / k column slices of a fused projection output (token stride > H*D)."""
+    hip.require()
+    torch.manual_seed(4)
+    B, T, H, D, extra = 2, 32, 4, 64, 128
+    buf = torch.randn(B, T, H * D + extra, device=cuda, dtype=torch.bfloat16)
+    x = buf[..., : H * D].view(B, T, H, D)
+    cos = torch.randn(T, D, device=cuda, dtype=torch.bfloat16)
+    sin = torch.randn(T, D, device=cuda, dtype=torch.bfloat16)
+    assert fused._token_strided_ok(x)
+    y = fused.rope(x, cos, sin)
+    torch.testing.assert_close(y.float(), fused.rope_reference(x.float(), cos.float(), sin.float()),
+                               rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("fuse", [False, True])
+def test_linear_multi_matches_separate(fuse, cuda):
+    """One GEMM on [Wq; Wk; Wv] == three linears: outputs, dx and every dW,
+    accumulated over two micro-batches (gradient-accumulation fusion on/off)."""
+    from distributed_lion_pytorch_amd.ops.linear import grad_accumulation_fusion, linear_multi_nk
+
+    hip.require()
+    torch.manual_seed(5)
+    C, sizes = 256, (256, 64, 64)
+    ws = [torch.nn.Parameter((torch.randn(n, C, device=cuda) * 0.05).to(torch.bfloat16)) for n in sizes]
+    refs = [w.detach().float().clone().requires_grad_(True) for w in ws]
+    xs = [torch.randn(2, 64, C, device=cuda, dtype=torch.bfloat16) for _ in range(2)]
+    dxs = []
+    with grad_accumulation_fusion(fuse):
+        for x in xs:
+            xx = x.clone().requires_grad_(True)
+            outs = linear_multi_nk(xx, ws)
+            loss = sum((o.float() * (i + 1)).sum() for i, o in enumerate(outs))
+            loss.backward()
+            dxs.append(xx.grad)
+    for x, dx in zip(xs, dxs):
+        xr = x.float().requires_grad_(True)
+        outs = [xr @ w.t() for w in refs]
+        sum((o * (i + 1)).sum() for i, o in enumerate(outs)).backward()
+        torch.testing.assert_close(dx.float(), xr.grad, rtol=2e-2, atol=5e-2)
+    for w, r in zip(ws, refs):
+        err = (w.grad.float() - r.grad).abs().max().item() / r.grad.abs().max().item()
+        assert err < 2e-2, err
