@@ -154,6 +154,7 @@ def dropout_add(y: torch.Tensor, residual: torch.Tensor, p: float) -> torch.Tens
 # --------------------------------------- fused residual + dropout + LN / RMSNorm
 _NORM_BWD_ROWS = 4  # rows per backward block-iteration for C <= 1024 (csrc/norm_kernels.hip RowGroup)
 _NORM_PARTS_CAP = int(os.environ.get("DLION_NORM_PARTS", "512"))
+_JOINT = os.environ.get("DLION_JOINT_DEPOSIT", "1") != "0"  # A/B switch for _deposit_joint
 
 
 def _norm_parts(rows: int, C: int) -> int:
@@ -193,10 +194,35 @@ def _param_grads(part2d, C, fused, present):
     else:
         for i in need:
             out[i] = _sum_rows(part2d[:, i * C:(i + 1) * C])
-    for i in range(3):
-        if present[i] and fused[i] is not None:
-            deposit_grad(fused[i], part2d[:, i * C:(i + 1) * C])
+    dep = [i for i in range(3) if present[i] and fused[i] is not None]
+    if len(dep) > 1 and _JOINT and dep == list(range(dep[0], dep[0] + len(dep))) and _deposit_joint(
+            [fused[i] for i in dep], part2d[:, dep[0] * C:(dep[-1] + 1) * C], C):
+        return tuple(out)
+    for i in dep:
+        deposit_grad(fused[i], part2d[:, i * C:(i + 1) * C])
     return tuple(out)
+
+
+def _deposit_joint(params, part2d, C) -> bool:
+    """(gamma, beta, bias).grad (+)= column sums of their adjacent partial
+    blocks in ONE reduction launch: the gradients live as consecutive views of
+    one buffer (allocated that way on the step's first deposit).  GPT-2 has 25
+    such boundaries per micro-batch: 50 fewer ~9 us launches."""
+    gs = [p.grad for p in params]
+    if all(g is None for g in gs):
+        buf = hip.ops().sum_partials(part2d)  # bf16 [k*C], fresh
+        for j, p in enumerate(params):
+            p.grad = buf[j * C:(j + 1) * C].view_as(p)
+        return True
+    if any(g is None or not g.is_contiguous() or g.dtype != params[0].dtype for g in gs):
+        return False
+    g0 = gs[0]
+    for j, g in enumerate(gs):
+        if (g.data_ptr() != g0.data_ptr() + j * C * g0.element_size()
+                or g.untyped_storage().data_ptr() != g0.untyped_storage().data_ptr()):
+            return False
+    hip.ops().sum_partials_acc_(part2d, g0.as_strided((len(gs) * C,), (1,)))
+    return True
 
 
 class _AddNorm(torch.autograd.Function):
