@@ -155,6 +155,7 @@ def dropout_add(y: torch.Tensor, residual: torch.Tensor, p: float) -> torch.Tens
 _NORM_BWD_ROWS = 4  # rows per backward block-iteration for C <= 1024 (csrc/norm_kernels.hip RowGroup)
 _NORM_PARTS_CAP = int(os.environ.get("DLION_NORM_PARTS", "512"))
 _JOINT = os.environ.get("DLION_JOINT_DEPOSIT", "1") != "0"  # A/B switch for _deposit_joint
+_LM_OWN_DGRAD = os.environ.get("DLION_LM_OWN_DGRAD", "1") != "0"  # A/B switch for _lm_dgrad
 
 
 def _norm_parts(rows: int, C: int) -> int:
@@ -507,6 +508,26 @@ def _pad_rows(w: torch.Tensor, mult: int = 64) -> torch.Tensor:
     return torch.cat([w, w.new_zeros(vp - v, w.shape[1])], 0)
 
 
+def _lm_dgrad(g: torch.Tensor, weight: torch.Tensor, wp: torch.Tensor) -> torch.Tensor:
+    """g [N, Vp] @ wp [Vp, C]: the LM head's input gradient, K = vocab.  When
+    the output has fewer 256x256 tiles than the chip has CUs (GPT-2: 20480 x 768
+    = 240 tiles, each with a 50304-long K loop) the own gfx950 NT GEMM
+    (csrc/gemm.hip) against a per-step cached wp^T beats hipBLASLt: 1589 ->
+    1169 us (tools/bench_lmhead.py), same-box bench A/B 859k -> 880k tok/s.
+    At Llama-3-8B's 8192 x 4096 (512 tiles) hipBLASLt stays ahead (22.6k vs
+    22.1k tok/s with the own kernel), so larger outputs keep it."""
+    vp = wp.shape[0]
+    tiles = -(-g.shape[0] // 256) * -(-wp.shape[1] // 256)
+    if (_LM_OWN_DGRAD and tiles < 256 and isinstance(weight, torch.nn.Parameter) and g.is_cuda
+            and g.dtype == torch.bfloat16 and vp % 128 == 0 and vp >= 8192 and g.is_contiguous()
+            and g.numel() < 2**31 and hip.available()):
+        from .linear import cached_derived
+
+        wpt = cached_derived(weight, "pad_t", lambda t: _pad_rows(t).t().contiguous())
+        return hip.ops().gemm_nt(g, wpt, None)
+    return g @ wp
+
+
 class _LMHeadCE(torch.autograd.Function):
     """loss = mean_{labels != -100} CE(h @ W^T, labels), gradients computed in
     the forward pass (the loss gradient is a scalar multiple of
@@ -530,7 +551,7 @@ class _LMHeadCE(torch.autograd.Function):
             row_loss = _softmax_xent_torch_(logits, labels1d, v)
         loss = row_loss.sum() / n_valid
         if need_grad:
-            dh = logits @ wp  # [N, C]
+            dh = _lm_dgrad(logits, weight, wp)  # [N, C]
             dw = (logits.t() @ h2d)[:v] if ctx.needs_input_grad[1] else None
             ctx.save_for_backward(dh, dw if dw is not None else dh.new_empty(0), n_valid)
             ctx.has_dw = dw is not None
@@ -584,13 +605,14 @@ class _TokenLogp(torch.autograd.Function):
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             ctx.save_for_backward(h2d, wp, logits)
             ctx.v = v
+            ctx.weight = weight
         return -row_loss
 
     @staticmethod
     def backward(ctx, g):
         h2d, wp, pm = ctx.saved_tensors  # pm = softmax - onehot
         d = pm * (-g).to(pm.dtype)[:, None]  # d logp / d logits = -(softmax - onehot)
-        dh = d @ wp if ctx.needs_input_grad[0] else None
+        dh = _lm_dgrad(d, ctx.weight, wp) if ctx.needs_input_grad[0] else None
         dw = (d.t() @ h2d)[: ctx.v] if ctx.needs_input_grad[1] else None
         return dh, dw, None
 

@@ -44,3 +44,25 @@ def test_lm_head_ce_wide_vocab_matches_reference(cuda):
     loss.backward()
     ref.backward()
     assert (h.grad.float() - hr.grad).abs().max().item() < 2e-2 * hr.grad.abs().max().item() + 1e-4
+
+
+def test_lm_head_ce_parameter_uses_own_dgrad_gemm(cuda):
+    """Parameter weight, GPT-2 vocab (padded 50304 = 393 x 128): the input
+    gradient runs on the own NT GEMM against the cached padded W^T."""
+    hip.require()
+    torch.manual_seed(1)
+    V, C = 50257, 128
+    h = torch.randn(3, 40, C, device=cuda).bfloat16().requires_grad_()
+    w = torch.nn.Parameter((0.05 * torch.randn(V, C, device=cuda)).bfloat16())
+    labels = torch.randint(0, V, (3, 40), device=cuda)
+    loss = fused.lm_head_cross_entropy(h, w, labels)
+    loss.backward()
+    hr, wr = h.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    ref = torch.nn.functional.cross_entropy((hr @ wr.t()).view(-1, V), labels.view(-1))
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-2
+    assert (h.grad.float() - hr.grad).abs().max().item() < 2e-2 * hr.grad.abs().max().item() + 1e-4
+    assert (w.grad.float() - wr.grad).abs().max().item() < 2e-2 * wr.grad.abs().max().item() + 1e-4
+    from distributed_lion_pytorch_amd.ops.linear import _WT_CACHE
+
+    assert (id(w), "pad_t") in _WT_CACHE

@@ -2,7 +2,12 @@
 V padded to 50304), random data, interleaved rounds in one process."""
 import statistics
 
+import sys
+
 import torch
+
+sys.path.insert(0, ".")
+from distributed_lion_pytorch_amd.ops import hip  # noqa: E402
 
 
 def timed(fn, reps=10):
@@ -16,6 +21,7 @@ def timed(fn, reps=10):
 
 
 def main():
+    ops = hip.ops()
     N, C, V = 20480, 768, 50304
     dt = torch.bfloat16
     h = torch.randn(N, C, device="cuda", dtype=dt)
@@ -31,6 +37,7 @@ def main():
         "wgrad lg.T@h (current)": lambda: lg.t() @ h,
         "wgrad (h.T@lg).T": lambda: (h.t() @ lg),
         "pad cat": lambda: torch.cat([w[:50257], w.new_zeros(47, C)], 0),
+        "dgrad own gemm_nt(lg, wt)": lambda: ops.gemm_nt(lg, wt, None),
     }
     for f in variants.values():
         f()
