@@ -216,10 +216,14 @@ struct QBlock {
 };
 
 // ------------------------------------------------------------------ forward
-template <int D, bool DROP>
+// NT key tiles (32 keys each) per barrier: with NT = 2 every wave has two
+// independent QK^T chains and two PV chains per iteration, so hipcc can put one
+// tile's MFMAs beside the other's softmax VALU work; with NT = 1 each step of
+// the QK -> max -> exp -> PV chain waits for the previous one.
+template <int D, bool DROP, int NT>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[2];
-  __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[2];
+  __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[2][NT];
+  __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[2][NT];
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
   const QBlock blk(a.B * a.H, a.T >> 5);
   const int bh = blk.bh, qtile = blk.qtile, last = blk.last;
@@ -242,32 +246,44 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const uint32_t arow = drop_row(a.seed, bh, q);
   const uint32_t thr_hi = a.thresh16 << 16;
   const DmaTile<D> kd(a.k_st), vd(a.v_st);
-  kd.issue(kg, ks_[0]);
-  vd.issue(vg, vs_[0]);
+  // tiles past `last` re-read tile `last` (valid memory); the causal mask
+  // zeroes them, since they lie beyond every query of the block
+  auto stage = [&](int first, int buf) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int64_t row = static_cast<int64_t>(min(first + j, last) * 32);
+      kd.issue(kg + row * a.k_st, ks_[buf][j]);
+      vd.issue(vg + row * a.v_st, vs_[buf][j]);
+    }
+  };
+  stage(0, 0);
   vm_wait0();
   __syncthreads();
-  for (int kt = 0; kt <= last; ++kt) {
-    const int buf = kt & 1;
-    if (kt < last) {  // next tile into the other buffer (last read before the previous barrier)
-      const int64_t nxt = static_cast<int64_t>((kt + 1) * 32);
-      kd.issue(kg + nxt * a.k_st, ks_[buf ^ 1]);
-      vd.issue(vg + nxt * a.v_st, vs_[buf ^ 1]);
-    }
+  for (int kt = 0; kt <= last; kt += NT) {
+    const int buf = (kt / NT) & 1;
+    if (kt + NT <= last) stage(kt + NT, buf ^ 1);  // the other buffer was last read before the previous barrier
     if (blk.active && kt <= qtile) {  // wave-uniform
-      const int kb = kt * 32;
-      f32x16 s = zero16();
+      f32x16 s[NT];
 #pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) s = mfma32(row_frag<D>(ks_[buf], r, ks, hf), qf[ks], s);
-      if (kt == qtile) {  // causal mask only on the diagonal tile
+      for (int j = 0; j < NT; ++j) {
+        s[j] = zero16();
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg)
-          if (kb + acc_row(reg, hf) > q) s[reg] = -INFINITY;
+        for (int ks = 0; ks < D / 16; ++ks) s[j] = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), qf[ks], s[j]);
+      }
+      if (kt + NT - 1 >= qtile) {  // the diagonal (or tiles past it) in this group: causal mask
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg)
+            if ((kt + j) * 32 + acc_row(reg, hf) > q) s[j][reg] = -INFINITY;
       }
       // row max on the raw scores (scale > 0); the scale is folded into the
       // exponent's FMA instead of a separate multiply pass
-      float tmax = s[0];
+      float tmax = s[0][0];
 #pragma unroll
-      for (int reg = 1; reg < 16; ++reg) tmax = fmaxf(tmax, s[reg]);
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) tmax = fmaxf(tmax, s[j][reg]);
       tmax = xmax32(tmax) * a.scale_log2;
       // deferred rescale (guide T13): keep the running max while no row of the
       // wave grew by more than kDeferLog2 -- P stays <= 2^kDeferLog2, exact in
@@ -284,29 +300,36 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
       }
       float rs = 0.f;
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -m));
-        rs += p;
-        s[reg] = p;
-      }
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][reg], a.scale_log2, -m));
+          rs += p;
+          s[j][reg] = p;
+        }
       l = l * alpha + xsum32(rs);
       if constexpr (DROP) {  // 1/(1-p) is applied once to O at the end
 #pragma unroll
-        for (int reg = 0; reg < 16; reg += 2) {  // regs (2i, 2i+1) hold keys (2j, 2j+1)
-          const uint32_t key = kb + acc_row(reg, hf);
-          const uint32_t hsh = mix1(arow ^ ((key >> 1) * 0xC2B2AE35u));
-          if ((hsh << 16) < thr_hi) s[reg] = 0.f;
-          if (hsh < thr_hi) s[reg + 1] = 0.f;
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int reg = 0; reg < 16; reg += 2) {  // regs (2i, 2i+1) hold keys (2j, 2j+1)
+            const uint32_t key = (kt + j) * 32 + acc_row(reg, hf);
+            const uint32_t hsh = mix1(arow ^ ((key >> 1) * 0xC2B2AE35u));
+            if ((hsh << 16) < thr_hi) s[j][reg] = 0.f;
+            if (hsh < thr_hi) s[j][reg + 1] = 0.f;
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 pf = acc_frag(s[j], s2);
+#pragma unroll
+          for (int t = 0; t < D / 32; ++t)
+            oacc[t] = mfma32(tr_frag<D>(vs_[buf][j], s2, t, lane), pf, oacc[t]);
         }
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pf = acc_frag(s, s2);
-#pragma unroll
-        for (int t = 0; t < D / 32; ++t) oacc[t] = mfma32(tr_frag<D>(vs_[buf], s2, t, lane), pf, oacc[t]);
-      }
     }
-    vm_wait0();  // this wave's pieces of the next tile have landed
+    vm_wait0();  // this wave's pieces of the next tiles have landed
     __syncthreads();
   }
   if (!blk.active) return;
@@ -581,13 +604,15 @@ static inline int64_t tile_blocks(int64_t nbh, int T) { return nbh * (((T >> 5) 
 
 hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) {
   const dim3 grid(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T))), block(256);
-#define FWD(DD)                                                                    \
-  if (drop) hipLaunchKernelGGL((attn_fwd_kernel<DD, true>), grid, block, 0, st, a); \
-  else hipLaunchKernelGGL((attn_fwd_kernel<DD, false>), grid, block, 0, st, a);
+  // NT = 2 key tiles per barrier at D=64 (GPT-2 shape fwd 0.067 -> 0.065 ms);
+  // at D=128 the extra 64 VGPRs cost a wave of occupancy and it was neutral
+#define FWD(DD, NT)                                                                        \
+  if (drop) hipLaunchKernelGGL((attn_fwd_kernel<DD, true, NT>), grid, block, 0, st, a); \
+  else hipLaunchKernelGGL((attn_fwd_kernel<DD, false, NT>), grid, block, 0, st, a);
   if (D == 64) {
-    FWD(64)
+    FWD(64, 2)
   } else if (D == 128) {
-    FWD(128)
+    FWD(128, 1)
   } else {
     return hipErrorInvalidValue;
   }
