@@ -54,7 +54,10 @@ class ApplyArgs:
 
 
 class WireCounter:
-    """Bytes this rank puts on / takes off the wire (payload only)."""
+    """Bytes this rank puts on / takes off the wire (payload only).  An
+    all-gather delivers this rank's contribution to each of the W-1 peers, so
+    it counts (W-1) x contribution sent -- ring or direct, the same bytes leave
+    the rank -- and sent == recv for every collective used here."""
 
     def __init__(self):
         self.sent = 0
@@ -108,7 +111,7 @@ class AllGatherExchange(VoteExchange):
     def launch(self, b, alive):
         out = self.recv_view(b)
         work = dist.all_gather_into_tensor(out, self.send_view(b), group=self.group, async_op=True)
-        self.wire.add(b.nbytes, (self.world - 1) * b.nbytes)
+        self.wire.add((self.world - 1) * b.nbytes, (self.world - 1) * b.nbytes)
         return work
 
     def finish(self, b, work, alive):
@@ -154,7 +157,7 @@ class AllToAllExchange(VoteExchange):
             works.append(dist.all_gather_into_tensor(self._v(self.voted_neg, b), neg, group=self.group,
                                                      async_op=True))
         n = len(works)
-        self.wire.add(n * shard, n * (self.world - 1) * shard, calls=n)
+        self.wire.add(n * (self.world - 1) * shard, n * (self.world - 1) * shard, calls=n)
         return works
 
     def finish(self, b, works, alive):
@@ -178,7 +181,7 @@ class RefInt64Exchange(AllGatherExchange):
             dist.all_gather(bufs, wide, group=self.group)
             for r, t in enumerate(bufs):
                 out[r, o:o + nb] = t.view(-1).to(torch.uint8)
-            self.wire.add(8 * nb, 8 * nb * (self.world - 1))
+            self.wire.add(8 * nb * (self.world - 1), 8 * nb * (self.world - 1))
         return None
 
     def finish(self, b, _, alive):
