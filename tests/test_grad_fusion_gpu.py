@@ -38,3 +38,35 @@ def test_fused_accumulation_matches_autograd(family, cuda):
     for n in ref:
         err = (ref[n] - fused[n]).abs().max().item() / (ref[n].abs().max().item() + 1e-8)
         assert err < 2e-2, (n, err)
+
+
+def test_split_k_accumulator_window(cuda):
+    """Split-K weight gradients stay in fp32 [S, K, N] buffers across the
+    micro-batches of one window (GEMM epilogue accumulation) and reach
+    param.grad once, when the window closes; the sum is fp32-exact to bf16
+    rounding of the final gradient."""
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    torch.manual_seed(3)
+    K, N, M = 256, 768, 2048
+    assert L.split_k_factor(M, K, N) > 1
+    w = torch.nn.Parameter((torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16))
+    xs = [torch.randn(M, K, device=cuda, dtype=torch.bfloat16) for _ in range(4)]
+    dys = [torch.randn(M, N, device=cuda, dtype=torch.bfloat16) for _ in range(4)]
+    with L.grad_accumulation_fusion(True):
+        for i, (x, dy) in enumerate(zip(xs, dys)):
+            y = L.linear_nk(x, w)
+            y.backward(dy)
+            assert w.grad is None, "deposit must wait for the end of the window"
+            assert len(L._PENDING) == 1
+    assert not L._PENDING
+    ref = sum(dy.float().t() @ x.float() for x, dy in zip(xs, dys))
+    err = (w.grad.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 8e-3, err
+    # a second window accumulates on top of the existing gradient
+    with L.grad_accumulation_fusion(True):
+        L.linear_nk(xs[0], w).backward(dys[0])
+    ref2 = ref + dys[0].float().t() @ xs[0].float()
+    err2 = (w.grad.float() - ref2).abs().max().item() / ref2.abs().max().item()
+    assert err2 < 8e-3, err2
