@@ -30,6 +30,15 @@ into ``param.grad`` once.  Measured at the GPT-2 shapes with GA = 8
 (tools/bench_wgrad_acc.py): 3-8 us less per weight gradient per micro-batch,
 and the micro-batch sum is fp32 instead of a bf16 running gradient.  Buffers
 are capped by ``_ACC_BUDGET`` bytes (large models have S = 1 and never use it).
+
+Memory cost: the buffers hold S x (weight numel) fp32 per split-K weight (about
+2 GB at GPT-2-124M) and stay allocated between steps so that the next window
+reuses them.  They are only used when the window is known to span more than
+one micro-batch (``grad_accumulation_fusion(micro_batches=n)`` with n > 1, or
+n unknown); ``release_split_k_accumulators()`` frees them, and
+``DLION_SPLITK_ACC=0`` disables them.  A change of split factor inside a window
+(micro-batches with different token counts) first flushes the running
+partials into ``param.grad``, then starts a fresh buffer.
 """
 from __future__ import annotations
 
@@ -40,27 +49,40 @@ import weakref
 
 import torch
 
-_FUSE_ACCUM = {"on": False}
+_FUSE_ACCUM = {"on": False, "multi": True}
 _ACC_BUDGET = (8 << 30) if os.environ.get("DLION_SPLITK_ACC", "1") != "0" else 0  # bytes of fp32 accumulators
 _ACC: dict = {}  # key -> [weakrefs of params, fp32 buffer [S, ...], [(param ref, col0, ncols)]]
 _PENDING: list = []  # keys written in the current window, in order
 
 
 @contextlib.contextmanager
-def grad_accumulation_fusion(enabled: bool = True):
-    prev = _FUSE_ACCUM["on"]
-    outer = bool(enabled) and not prev
+def grad_accumulation_fusion(enabled: bool = True, micro_batches: int | None = None):
+    """Fusion window = the micro-batches of one optimizer step.  ``micro_batches``
+    (if known) gates the split-K accumulators: with one micro-batch they save
+    nothing, so the weight gradient is reduced straight into ``param.grad``."""
+    prev = (_FUSE_ACCUM["on"], _FUSE_ACCUM["multi"])
+    outer = bool(enabled) and not prev[0]
     _FUSE_ACCUM["on"] = bool(enabled)
+    if outer:
+        _FUSE_ACCUM["multi"] = micro_batches is None or int(micro_batches) > 1
     ok = False
     try:
         yield
         ok = True
     finally:
-        _FUSE_ACCUM["on"] = prev
+        _FUSE_ACCUM["on"], _FUSE_ACCUM["multi"] = prev
         if outer:
             if ok:
                 flush_split_k_accumulators()
             _PENDING.clear()
+
+
+def _flush_entry(ent) -> None:
+    flat = ent[1].view(ent[1].shape[0], -1)
+    for ref, c0, n in ent[2]:
+        p = ref()
+        if p is not None:
+            deposit_grad(p, flat[:, c0:c0 + n])
 
 
 def flush_split_k_accumulators() -> None:
@@ -68,28 +90,41 @@ def flush_split_k_accumulators() -> None:
     parameters' ``.grad`` (one fused sum + deposit per weight)."""
     for key in _PENDING:
         ent = _ACC.get(key)
-        if ent is None:
-            continue
-        flat = ent[1].view(ent[1].shape[0], -1)
-        for ref, c0, n in ent[2]:
-            p = ref()
-            if p is not None:
-                deposit_grad(p, flat[:, c0:c0 + n])
+        if ent is not None:
+            _flush_entry(ent)
     _PENDING.clear()
+
+
+def release_split_k_accumulators() -> None:
+    """Free every split-K accumulator (flushing the open window's partials
+    into ``param.grad`` first).  Call after training to return the memory."""
+    flush_split_k_accumulators()
+    _ACC.clear()
 
 
 def _acc_gemm(params, cols, a3, b3) -> bool:
     """Accumulate bmm(a3, b3) (fp32, [S, R, C]) into the window's buffer for
-    `params` (column blocks `cols` of the flattened R*C).  False if over budget."""
+    `params` (column blocks `cols` of the flattened R*C).  False if the buffer
+    cannot be used (over budget, single-micro-batch window): the caller then
+    deposits into ``param.grad`` directly, on top of any flushed partials."""
+    if not _FUSE_ACCUM["multi"]:
+        return False
     key = tuple(id(p) for p in params)
     ent = _ACC.get(key)
     shape = (a3.shape[0], a3.shape[1], b3.shape[2])
     if ent is None or any(r() is not p for r, p in zip(ent[0], params)) or tuple(ent[1].shape) != shape:
         if ent is not None:
+            if key in _PENDING:
+                # split factor / token count changed inside the window: the
+                # partials so far go into param.grad before the buffer is replaced
+                _flush_entry(ent)
+                _PENDING.remove(key)
             _ACC.pop(key)
         used = sum(e[1].numel() * 4 for e in _ACC.values() if all(r() is not None for r in e[0]))
         for k in [k for k, e in _ACC.items() if any(r() is None for r in e[0])]:
             _ACC.pop(k)  # parameters gone: drop their buffers
+            if k in _PENDING:
+                _PENDING.remove(k)
         if used + math.prod(shape) * 4 > _ACC_BUDGET:
             return False
         buf = torch.empty(shape, device=a3.device, dtype=torch.float32)
@@ -165,7 +200,9 @@ def wgrad_into(a: torch.Tensor, b: torch.Tensor, w: torch.nn.Parameter) -> None:
             a3, b3 = a.view(s, M // s, K).transpose(1, 2), b.view(s, M // s, N)
             if _FUSE_ACCUM["on"] and _acc_gemm([w], [(0, K * N)], a3, b3):
                 return  # reduced into w.grad when the accumulation window closes
-            if g is not None:
+            g = w.grad  # _acc_gemm may have flushed earlier partials into it
+            grad_ok = g is None or (g.is_contiguous() and g.dtype == w.dtype)
+            if g is not None and grad_ok:
                 hip.ops().sum_partials_acc_(torch.bmm(a3, b3, out_dtype=torch.float32), g)
                 return
     if not grad_ok or g is None:

@@ -140,6 +140,11 @@ class Lion(Optimizer):
         if self._n_steps in self._dropout_schedule:
             self.drop_workers(self._dropout_schedule[self._n_steps])
         host = tuple(r not in self._dropped for r in range(world))
+        if not any(host):
+            # with no live voter the exchanges would disagree (allgather: delta 0,
+            # a2a without a negative plane: delta -1), so this is refused outright
+            raise ValueError(f"every worker of the {world}-rank vote is dropped ({sorted(self._dropped)}); "
+                             "at least one rank must keep voting")
         if self._alive_dev is None or host != self._alive_host or self._alive_dev.device != device:
             t = torch.tensor([1 if a else 0 for a in host], dtype=torch.uint8)
             self._alive_dev = t.to(device)

@@ -78,7 +78,7 @@ class TrainStep:
 
         self.model.train()
         total = None
-        with grad_accumulation_fusion(self.fuse_grad_accumulation):
+        with grad_accumulation_fusion(self.fuse_grad_accumulation, micro_batches=self.grad_accum):
             for batch in micro_batches:
                 loss = self.loss_fn(self.model, batch) / self.grad_accum
                 loss.backward()

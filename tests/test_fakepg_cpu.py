@@ -104,3 +104,43 @@ def test_allgather_family_wire_bytes_w8(exchange):
         assert s["wire_bytes_recv"] >= (world - 1) * out["numel"]
         assert s["collectives"] > len(out["bucket_bytes"])
     assert out["finite"]
+
+
+def _fake_all_dropped(q, world):
+    try:
+        import torch.distributed as dist
+        from torch.testing._internal.distributed.fake_pg import FakeStore
+
+        from distributed_lion_pytorch_amd import Lion
+
+        torch.set_num_threads(1)
+        dist.init_process_group("fake", store=FakeStore(), rank=0, world_size=world)
+        p = torch.nn.Parameter(torch.randn(64, 64))
+        opt = Lion([p], lr=1e-3, exchange="a2a", backend="torch", verify_consistency=False)
+        p.grad = torch.randn_like(p)
+        opt.drop_workers(range(world))
+        try:
+            opt.step()
+            q.put(("err", "step with every worker dropped did not raise"))
+        except ValueError as e:
+            q.put(("ok", str(e)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        q.put(("err", traceback.format_exc()))
+
+
+def test_dropping_every_worker_is_refused():
+    """With no live voter the allgather and a2a exchanges would disagree (0 vs
+    -1 delta), so the optimizer refuses the configuration instead."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    proc = ctx.Process(target=_fake_all_dropped, args=(q, 4))
+    proc.start()
+    try:
+        status, out = q.get(timeout=240)
+    finally:
+        proc.join(timeout=30)
+        if proc.is_alive():
+            proc.kill()
+    assert status == "ok", out
+    assert "dropped" in out

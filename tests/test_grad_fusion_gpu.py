@@ -70,3 +70,55 @@ def test_split_k_accumulator_window(cuda):
     ref2 = ref + dys[0].float().t() @ xs[0].float()
     err2 = (w.grad.float() - ref2).abs().max().item() / ref2.abs().max().item()
     assert err2 < 8e-3, err2
+
+
+def _window_ref(steps):
+    """fp32 autograd-free reference: sum of dy^T x over the window."""
+    return sum(dy.float().t() @ x.float() for x, dy in steps)
+
+
+@pytest.mark.parametrize("case", ["varying_m", "tiny_budget", "shared_weight", "single_micro_batch"])
+def test_split_k_window_edge_cases(case, cuda, monkeypatch):
+    """The branches where the accumulators could lose or corrupt partials:
+    a split factor that changes inside a window (different token counts), an
+    over-budget buffer, one weight used by two layers (two keys deposit into
+    one .grad), and a window declared as one micro-batch (no buffers)."""
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    torch.manual_seed(7)
+    K, N = 256, 768
+    if case == "tiny_budget":
+        monkeypatch.setattr(L, "_ACC_BUDGET", 1 << 20)
+    w = torch.nn.Parameter((torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16))
+    w2 = torch.nn.Parameter((torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16))
+    Ms = [2048, 1032, 2048, 1032] if case in ("varying_m", "tiny_budget") else [2048, 2048, 2048]
+    if case == "single_micro_batch":
+        Ms = [2048]
+    if case == "varying_m":
+        assert L.split_k_factor(2048, K, N) != L.split_k_factor(1032, K, N)
+    steps = [(torch.randn(m, K, device=cuda, dtype=torch.bfloat16),
+              torch.randn(m, N, device=cuda, dtype=torch.bfloat16)) for m in Ms]
+    L.release_split_k_accumulators()
+    with L.grad_accumulation_fusion(True, micro_batches=len(Ms)):
+        for x, dy in steps:
+            if case == "shared_weight":
+                # w alone (single key) and w fused with w2 (multi key)
+                L.linear_nk(x, w).backward(dy)
+                ya, yb = L.linear_multi_nk(x, [w, w2])
+                torch.autograd.backward([ya, yb], [dy, dy])
+            else:
+                L.linear_nk(x, w).backward(dy)
+        if case == "single_micro_batch":
+            assert not L._PENDING and w.grad is not None
+    assert not L._PENDING
+    ref = _window_ref(steps)
+    if case == "shared_weight":
+        ref2 = ref.clone()
+        ref = 2 * ref
+        err2 = (w2.grad.float() - ref2).abs().max().item() / ref2.abs().max().item()
+        assert err2 < 8e-3, err2
+    err = (w.grad.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 8e-3, (case, err)
+    L.release_split_k_accumulators()
+    assert not L._ACC
