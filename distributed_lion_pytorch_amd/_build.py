@@ -122,7 +122,7 @@ def build(verbose: bool = False, force: bool = False) -> Path:
     cmd = (
         [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}"]
         + [str(o) for o in objs]
-        + [f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", f"-Wl,-rpath,{lib}", "-o", str(tmp)]
+        + [f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lhipblaslt", f"-Wl,-rpath,{lib}", "-o", str(tmp)]
     )
     if verbose:
         print(" ".join(cmd), flush=True)

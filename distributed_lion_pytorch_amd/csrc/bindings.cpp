@@ -12,6 +12,11 @@
 
 #include "kernels.h"
 
+namespace dlion {
+bool lt_gemm_nt(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, const void* bias,
+                int64_t M, int64_t N, int64_t K, int epi, int device, hipStream_t s);
+}
+
 namespace {
 
 using at::Tensor;
@@ -544,9 +549,32 @@ std::tuple<Tensor, Tensor> gemm_nt_gelu(const Tensor& a, const Tensor& b, const 
   return {h, z};
 }
 
+// ------------------------------------------- hipBLASLt GEMM + epilogue (lt_gemm.cpp)
+// out [M, N] = epi(a [M, K] . b [N, K]^T); epi 0 plain, 1 + bias, 2 gelu_tanh(z + bias).
+// Returns false when hipBLASLt has no kernel for the case (caller falls back).
+bool lt_gemm_nt(const Tensor& a, const Tensor& b, const std::optional<Tensor>& bias, int64_t epi, const Tensor& out) {
+  check_gemm_operand(a, "a");
+  check_gemm_operand(b, "b");
+  check_gemm_operand(out, "out");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "dlion lt_gemm: bad epilogue ", epi);
+  TORCH_CHECK(a.size(1) == b.size(1) && out.size(0) == a.size(0) && out.size(1) == b.size(0),
+              "dlion lt_gemm: shape mismatch a=", a.sizes(), " b=", b.sizes(), " out=", out.sizes());
+  TORCH_CHECK(bias.has_value() == (epi != 0), "dlion lt_gemm: epilogue ", epi, epi ? " needs" : " takes no", " bias");
+  if (bias.has_value()) {
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() &&
+                    bias->numel() == b.size(0),
+                "dlion lt_gemm: bias must be a contiguous bf16 [N] tensor");
+  }
+  const c10::DeviceGuard g(a.device());
+  return dlion::lt_gemm_nt(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
+                           bias.has_value() ? bias->data_ptr() : nullptr, a.size(0), b.size(0), a.size(1),
+                           static_cast<int>(epi), a.device().index(), cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dlion, m) {
+  m.def("lt_gemm_nt(Tensor a, Tensor b, Tensor? bias, int epi, Tensor(a!) out) -> bool");
   m.def("gemm_nt(Tensor a, Tensor b, Tensor? bias) -> Tensor");
   m.def("gemm_nt_out(Tensor a, Tensor b, Tensor? bias, Tensor(a!) out) -> ()");
   m.def("gemm_nt_gelu(Tensor a, Tensor b, Tensor bias, bool exact) -> (Tensor, Tensor)");
@@ -611,4 +639,5 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("gemm_nt", &gemm_nt);
   m.impl("gemm_nt_out", &gemm_nt_out);
   m.impl("gemm_nt_gelu", &gemm_nt_gelu);
+  m.impl("lt_gemm_nt", &lt_gemm_nt);
 }

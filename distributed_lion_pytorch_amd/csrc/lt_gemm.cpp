@@ -1,0 +1,199 @@
+// hipBLASLt GEMMs with fused epilogues (the library's MFMA kernels, our
+// epilogue choice):  out[M,N] = epi(a[M,K] . b[N,K]^T)
+//
+//   epi 0  plain      1  + bias[N]      2  gelu_tanh(z + bias[N])
+//
+// Row-major operands map onto hipBLASLt's column-major convention as
+// D^T[N,M] = op_T(b)[N,K] . a^T[K,M] (transA = T, transB = N).  Epilogue 2 is
+// the GPT-2 MLP up-projection when no backward follows (evaluation, frozen
+// reference models): one GEMM instead of GEMM + a bias+GELU pass over the
+// [tokens, 4C] activation.  Training keeps the separate kernel because the
+// backward needs the pre-activation, and this hipBLASLt build has no kernels
+// for the AUX / DGELU / BGRAD epilogues on gfx950 bf16 (probed with
+// tools/probes/lt_probe.cpp: GELU_AUX, GELU_AUX_BIAS, DGELU, DGELU_BGRAD,
+// BGRADA, BGRADB all return 0 heuristic candidates).
+//
+// The algorithm per (shape, strides, epilogue) is chosen once: hipBLASLt's
+// heuristic returns up to kCand candidates, each is timed on the caller's
+// stream (skipped under stream capture) and the fastest is cached, so a call
+// costs ~11 us of host time against ~19 us for ATen's per-call heuristic
+// query (tools/bench_host_overhead.py).  The library is torch's own bundled
+// libhipblaslt (linked by SONAME, so the copy libtorch_hip already loaded is
+// reused -- no second hipBLASLt in the process).
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt.h>
+
+#include <array>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+
+namespace dlion {
+namespace {
+
+constexpr int kCand = 12;
+constexpr size_t kWorkspace = 64ull << 20;
+
+void lt_check(hipblasStatus_t s, const char* what) {
+  TORCH_CHECK(s == HIPBLAS_STATUS_SUCCESS, "dlion lt_gemm: ", what, " failed (hipblas status ", static_cast<int>(s),
+              ")");
+}
+
+struct DevState {
+  hipblasLtHandle_t handle = nullptr;
+  at::Tensor workspace;
+};
+
+using Key = std::array<int64_t, 8>;  // m, n, k, lda, ldb, ldc, epi, device
+
+struct Plan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+  hipblasLtMatmulAlgo_t algo{};
+  size_t ws = 0;
+  bool ok = false;
+  bool tuned = false;
+  int n_cand = 0;
+  hipblasLtMatmulHeuristicResult_t cand[kCand];
+};
+
+std::mutex g_mu;
+std::map<int, DevState> g_dev;
+std::map<Key, Plan> g_plans;
+
+DevState& dev_state(const at::Device& d) {
+  auto& st = g_dev[d.index()];
+  if (st.handle == nullptr) {
+    lt_check(hipblasLtCreate(&st.handle), "hipblasLtCreate");
+    st.workspace = at::empty({static_cast<int64_t>(kWorkspace)}, at::TensorOptions().dtype(at::kByte).device(d));
+  }
+  return st;
+}
+
+hipblasLtEpilogue_t epilogue_of(int epi) {
+  switch (epi) {
+    case 0: return HIPBLASLT_EPILOGUE_DEFAULT;
+    case 1: return HIPBLASLT_EPILOGUE_BIAS;
+    case 2: return HIPBLASLT_EPILOGUE_GELU_BIAS;
+    default: TORCH_CHECK(false, "dlion lt_gemm: bad epilogue ", epi);
+  }
+  return HIPBLASLT_EPILOGUE_DEFAULT;
+}
+
+void set_attr(hipblasLtMatmulDesc_t d, hipblasLtMatmulDescAttributes_t a, const void* v, size_t n) {
+  lt_check(hipblasLtMatmulDescSetAttribute(d, a, v, n), "hipblasLtMatmulDescSetAttribute");
+}
+
+void bind_pointers(Plan& p, const void* bias) {
+  if (bias) set_attr(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
+}
+
+hipblasStatus_t run(DevState& st, Plan& p, const hipblasLtMatmulAlgo_t& algo, const void* a, const void* b, void* c,
+                    hipStream_t s) {
+  const float alpha = 1.f, beta = 0.f;
+  // column-major: A_cm = b (op T), B_cm = a (op N), D_cm = out
+  return hipblasLtMatmul(st.handle, p.desc, &alpha, b, p.la, a, p.lb, &beta, c, p.lc, c, p.lc, &algo,
+                         st.workspace.data_ptr(), kWorkspace, s);
+}
+
+Plan& get_plan(DevState& st, const Key& key, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldc,
+               int epi, const void* bias) {
+  auto it = g_plans.find(key);
+  if (it != g_plans.end()) return it->second;
+  Plan& p = g_plans[key];
+  lt_check(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F), "hipblasLtMatmulDescCreate");
+  const int32_t opT = HIPBLAS_OP_T, opN = HIPBLAS_OP_N;
+  set_attr(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opT, sizeof(opT));
+  set_attr(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opN, sizeof(opN));
+  const hipblasLtEpilogue_t e = epilogue_of(epi);
+  set_attr(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e));
+  if (epi == 1 || epi == 2) {
+    const int32_t bt = HIP_R_16BF;
+    set_attr(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
+  }
+  bind_pointers(p, bias);
+  // A_cm: b viewed column-major [K, N] (ld = ldb); B_cm: a as [K, M] (ld = lda); D: [N, M] (ld = ldc)
+  lt_check(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, k, n, ldb), "layout A");
+  lt_check(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, k, m, lda), "layout B");
+  lt_check(hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_16BF, n, m, ldc), "layout D");
+  hipblasLtMatmulPreference_t pref;
+  lt_check(hipblasLtMatmulPreferenceCreate(&pref), "preference");
+  const uint64_t wsb = kWorkspace;
+  lt_check(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)),
+           "preference workspace");
+  int got = 0;
+  const hipblasStatus_t hs =
+      hipblasLtMatmulAlgoGetHeuristic(st.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, kCand, p.cand, &got);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  p.n_cand = 0;
+  if (hs == HIPBLAS_STATUS_SUCCESS) {
+    for (int i = 0; i < got; ++i)
+      if (p.cand[i].state == HIPBLAS_STATUS_SUCCESS && p.cand[i].workspaceSize <= kWorkspace) p.cand[p.n_cand++] = p.cand[i];
+  }
+  p.ok = p.n_cand > 0;
+  if (p.ok) {
+    p.algo = p.cand[0].algo;
+    p.ws = p.cand[0].workspaceSize;
+  }
+  return p;
+}
+
+bool tuning_enabled() {
+  const char* v = std::getenv("DLION_LT_TUNE");
+  return v == nullptr || v[0] != '0';
+}
+
+// time every candidate (2 launches each after a warm-up) and keep the fastest
+void tune(DevState& st, Plan& p, const void* a, const void* b, void* c, hipStream_t s) {
+  p.tuned = true;
+  if (p.n_cand < 2 || !tuning_enabled()) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return;
+  if (hipEventCreate(&e1) != hipSuccess) {
+    hipEventDestroy(e0);
+    return;
+  }
+  float best = 1e30f;
+  int besti = 0;
+  for (int i = 0; i < p.n_cand; ++i) {
+    if (run(st, p, p.cand[i].algo, a, b, c, s) != HIPBLAS_STATUS_SUCCESS) continue;
+    hipEventRecord(e0, s);
+    bool ok = true;
+    for (int r = 0; r < 2 && ok; ++r) ok = run(st, p, p.cand[i].algo, a, b, c, s) == HIPBLAS_STATUS_SUCCESS;
+    hipEventRecord(e1, s);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (ok && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms < best) {
+      best = ms;
+      besti = i;
+    }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  p.algo = p.cand[besti].algo;
+  p.ws = p.cand[besti].workspaceSize;
+}
+
+}  // namespace
+
+// Returns false (and does nothing) when hipBLASLt has no kernel for this
+// shape/epilogue, so the caller can take its unfused path.
+bool lt_gemm_nt(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, const void* bias,
+                int64_t M, int64_t N, int64_t K, int epi, int device, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DevState& st = dev_state(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
+  const Key key{M, N, K, lda, ldb, ldc, epi, device};
+  Plan& p = get_plan(st, key, M, N, K, lda, ldb, ldc, epi, bias);
+  if (!p.ok) return false;
+  bind_pointers(p, bias);
+  if (!p.tuned) tune(st, p, a, b, c, s);
+  lt_check(run(st, p, p.algo, a, b, c, s), "hipblasLtMatmul");
+  return true;
+}
+
+}  // namespace dlion

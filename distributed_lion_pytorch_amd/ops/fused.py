@@ -358,10 +358,20 @@ def norm_dropout_keep(rows: int, C: int, p: float, seed: int, device=None) -> to
 
 # --------------------------------------------------------------- bias + GELU
 def linear_gelu(x2d: torch.Tensor, w_in_out: torch.Tensor, bias: torch.Tensor, exact: bool = False):
-    """gelu(x @ W + b) with HF Conv1D's [in, out] weight layout: GEMM without
-    bias, then one bias+GELU kernel whose backward also yields the bias grad."""
-    from .linear import linear_kn
+    """gelu(x @ W + b) with HF Conv1D's [in, out] weight layout.  Training: GEMM
+    without bias, then one bias+GELU kernel whose backward also yields the
+    bias grad.  Without autograd (evaluation, frozen models): one hipBLASLt
+    GEMM with the bias+GELU epilogue (csrc/lt_gemm.cpp; tanh GELU only)."""
+    from .linear import autocast_inputs, linear_kn, transposed_weight
 
+    if (not exact and not torch.is_grad_enabled() and x2d.is_cuda and _use_hip(x2d)
+            and x2d.dim() == 2 and x2d.stride(1) == 1 and x2d.stride(0) % 8 == 0):
+        xa, wa, ba = autocast_inputs(x2d, w_in_out, bias)
+        if xa.dtype == wa.dtype == ba.dtype == torch.bfloat16 and ba.is_contiguous() and xa.data_ptr() % 16 == 0:
+            wt = transposed_weight(wa)  # [out, in], cached until the next optimizer step
+            out = torch.empty(xa.shape[0], wt.shape[0], dtype=xa.dtype, device=xa.device)
+            if hip.ops().lt_gemm_nt(xa, wt, ba, 2, out):
+                return out
     return bias_gelu(linear_kn(x2d, w_in_out, None), bias, exact)
 
 

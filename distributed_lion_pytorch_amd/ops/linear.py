@@ -77,6 +77,32 @@ def grad_accumulation_fusion(enabled: bool = True, micro_batches: int | None = N
             _PENDING.clear()
 
 
+def begin_fusion_window(micro_batches: int | None = None) -> bool:
+    """Non-context form of :func:`grad_accumulation_fusion` for loops that do
+    not own the micro-batch iteration (the HF Trainer's ``training_step`` runs
+    once per micro-batch).  Returns False if a window is already open."""
+    if _FUSE_ACCUM["on"]:
+        return False
+    _FUSE_ACCUM["on"] = True
+    _FUSE_ACCUM["multi"] = micro_batches is None or int(micro_batches) > 1
+    return True
+
+
+def end_fusion_window(flush: bool = True) -> None:
+    """Close the window opened by :func:`begin_fusion_window`: every weight
+    gradient of the window is in ``param.grad`` afterwards."""
+    if not _FUSE_ACCUM["on"]:
+        return
+    _FUSE_ACCUM["on"], _FUSE_ACCUM["multi"] = False, True
+    if flush:
+        flush_split_k_accumulators()
+    _PENDING.clear()
+
+
+def fusion_window_open() -> bool:
+    return bool(_FUSE_ACCUM["on"])
+
+
 def _flush_entry(ent) -> None:
     flat = ent[1].view(ent[1].shape[0], -1)
     for ref, c0, n in ent[2]:
