@@ -162,7 +162,8 @@ int dtype_code(at::ScalarType t) {
   return -1;
 }
 
-Tensor softmax_xent_(const Tensor& logits, const Tensor& labels, int64_t v) {
+// variant: 0 auto, 1 register-resident fp32 row, 2 streaming, 3/4/5 packed 16-bit row with 256/512/1024 threads
+Tensor softmax_xent_(const Tensor& logits, const Tensor& labels, int64_t v, int64_t variant) {
   check_dev(logits, "logits");
   check_dev(labels, "labels");
   TORCH_CHECK(logits.dim() == 2, "dlion: logits must be [N, Vpad]");
@@ -172,7 +173,7 @@ Tensor softmax_xent_(const Tensor& logits, const Tensor& labels, int64_t v) {
   auto loss = at::empty({logits.size(0)}, logits.options().dtype(at::kFloat));
   check_hip(dlion::launch_softmax_xent(dtype_code(logits.scalar_type()), logits.data_ptr(), labels.data_ptr<int64_t>(),
                                        logits.size(0), logits.size(1), static_cast<int>(v), loss.data_ptr<float>(),
-                                       cur_stream()),
+                                       static_cast<int>(variant), cur_stream()),
             "softmax_xent");
   return loss;
 }
@@ -597,7 +598,7 @@ TORCH_LIBRARY(dlion, m) {
   m.def(
       "attn_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout, Tensor lse, float p, int seed,"
       " Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
-  m.def("softmax_xent_(Tensor(a!) logits, Tensor labels, int v) -> Tensor");
+  m.def("softmax_xent_(Tensor(a!) logits, Tensor labels, int v, int variant=0) -> Tensor");
   m.def(
       "lion_local(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, float decay, float neg_lr,"
       " float b1, float omb1, float b2, float omb2, Tensor? gscale=None) -> ()");

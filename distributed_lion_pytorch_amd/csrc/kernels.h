@@ -61,7 +61,8 @@ hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* 
                           void* aux, int ldaux, int M, int N, int K, int epi, hipStream_t st);
 
 // ---- LM head cross-entropy (xent_kernels.hip)
+// variant 0 = auto (DLION_XENT env override), 1 fp32-row, 2 streaming, 3/4/5 packed 16-bit row (256/512/1024 thr)
 hipError_t launch_softmax_xent(int dt, void* logits, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,
-                               hipStream_t st);
+                               int variant, hipStream_t st);
 
 }  // namespace dlion

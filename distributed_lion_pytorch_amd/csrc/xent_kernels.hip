@@ -8,6 +8,9 @@
 // reference path (HF GPT2LMHeadModel loss, /root/reference/run_clm.py:442).
 #include "common.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace dlion {
 
 constexpr int kXentThreads = 1024;
@@ -159,18 +162,181 @@ softmax_xent_stream_kernel(typename Elem<DT>::S* __restrict__ logits, const int6
   }
 }
 
+
+// an empty asm that "modifies" the packed row: values unpacked before it
+// cannot be reused after it, so hipcc keeps 4 VGPRs per chunk live, not 8 floats
+template <int CH>
+__device__ __forceinline__ void opaque(uint4 (&raw)[CH]) {
+#pragma unroll
+  for (int i = 0; i < CH; ++i) asm volatile("" : "+v"(raw[i].x), "+v"(raw[i].y), "+v"(raw[i].z), "+v"(raw[i].w));
+}
+
+// Packed variant for 16-bit logits: the row stays in registers as raw 16-bit
+// pairs (CH 16-byte chunks per lane, 4 VGPRs each) instead of fp32 (8 VGPRs
+// per chunk), so a row needs half the registers and THREADS-thread blocks run
+// several rows per CU at once: every chunk load is issued up front, and one
+// row's reductions / write-back overlap the next row's loads.  Each pass
+// (max, sum of exp, gradient) unpacks on the fly -- two exps per logit, which
+// is noise next to the memory traffic.
+template <int DT, int THREADS, int CH>
+__global__ void __launch_bounds__(THREADS)
+softmax_xent_packed_kernel(uint16_t* __restrict__ logits, const int64_t* __restrict__ labels, int64_t vp, int v,
+                           float* __restrict__ row_loss) {
+  using E = Elem<DT>;
+  constexpr int W = THREADS / 64;
+  __shared__ float red[2][W];
+  const int64_t row = blockIdx.x;
+  uint16_t* x = logits + row * vp;
+  const int64_t label = labels[row];
+  const int lab = (label >= 0 && label < v) ? static_cast<int>(label) : -1;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+  // the target logit comes straight from memory (one scalar load per row)
+  const float tgt = lab >= 0 ? E::to_f(x[lab]) : 0.f;
+  constexpr uint32_t kNegInf2 = DT == kBF16 ? 0xff80ff80u : 0xfc00fc00u;
+  uint4 raw[CH];
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int e = (i * THREADS + tid) * 8;
+    raw[i] = e < vp ? *reinterpret_cast<const uint4*>(x + e) : make_uint4(kNegInf2, kNegInf2, kNegInf2, kNegInf2);
+  }
+  // padded vocab columns (v <= e+j < vp) become -inf in the packed row itself,
+  // so no pass needs a per-element bound check
+  {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int e = (i * THREADS + tid) * 8;
+      if (e + 8 > v && e < vp) {
+        uint32_t wv[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (e + j >= v) wv[j >> 1] = (j & 1) ? ((wv[j >> 1] & 0xffffu) | (kNegInf2 & 0xffff0000u))
+                                               : ((wv[j >> 1] & 0xffff0000u) | (kNegInf2 & 0xffffu));
+        raw[i] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      }
+    }
+  }
+  auto unpack = [&](const uint4& r4, float (&f)[8]) {
+    const uint32_t wv[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = E::to_f(static_cast<uint16_t>(j & 1 ? wv[j >> 1] >> 16 : wv[j >> 1] & 0xffffu));
+  };
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    float f[8];
+    unpack(raw[i], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mx = fmaxf(mx, f[j]);
+  }
+  opaque(raw);  // keep the row packed: the next pass re-unpacks instead of holding fp32 copies live
+  mx = wave_max(mx);
+  if (lane == 0) red[0][wid] = mx;
+  __syncthreads();
+  mx = red[0][0];
+#pragma unroll
+  for (int w = 1; w < W; ++w) mx = fmaxf(mx, red[0][w]);
+
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    float f[8];
+    unpack(raw[i], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sum += __expf(f[j] - mx);  // exp(-inf) = 0: padding and past-the-row
+  }
+  opaque(raw);
+  sum = wave_sum(sum);
+  if (lane == 0) red[1][wid] = sum;
+  __syncthreads();
+  sum = 0.f;
+#pragma unroll
+  for (int w = 0; w < W; ++w) sum += red[1][w];
+
+  const float inv = lab >= 0 ? 1.f / sum : 0.f;
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int e = (i * THREADS + tid) * 8;
+    if (e < vp) {
+      float f[8], o[8];
+      unpack(raw[i], f);
+      const int rel = lab - e;  // the one-hot column, if it is in this chunk
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = __expf(f[j] - mx) * inv - (rel == j ? 1.f : 0.f);
+      E::store8(x + e, o);
+    }
+  }
+  if (tid == 0) row_loss[row] = lab >= 0 ? (mx + __logf(sum)) - tgt : 0.f;
+}
+
+// xent variant override for A/B runs: DLION_XENT = reg | stream | p256 | p512 | p1024 (default: auto)
+static int xent_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* s = getenv("DLION_XENT");
+    v = 0;
+    if (s) {
+      if (!strcmp(s, "reg")) v = 1;
+      else if (!strcmp(s, "stream")) v = 2;
+      else if (!strcmp(s, "p256")) v = 3;
+      else if (!strcmp(s, "p512")) v = 4;
+      else if (!strcmp(s, "p1024")) v = 5;
+    }
+  }
+  return v;
+}
+
+template <int DT, int THREADS, int CH>
+static void launch_packed(uint16_t* lp, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,
+                          hipStream_t st) {
+  hipLaunchKernelGGL((softmax_xent_packed_kernel<DT, THREADS, CH>), dim3(n), dim3(THREADS), 0, st, lp, labels, vp, v,
+                     loss);
+}
+
+// packed 16-bit row kernel when the row fits: returns false otherwise
+template <int DT>
+static bool launch_packed_dt(int threads, void* logits, const int64_t* labels, int64_t n, int64_t vp, int v,
+                             float* loss, hipStream_t st) {
+  uint16_t* lp = static_cast<uint16_t*>(logits);
+  const int64_t ch = (vp + threads * 8 - 1) / (threads * 8);
+  if (threads == 1024) {
+    if (ch <= 4) launch_packed<DT, 1024, 4>(lp, labels, n, vp, v, loss, st);
+    else if (ch <= 7) launch_packed<DT, 1024, 7>(lp, labels, n, vp, v, loss, st);
+    else return false;
+  } else if (threads == 256) {
+    if (ch <= 16) launch_packed<DT, 256, 16>(lp, labels, n, vp, v, loss, st);
+    else if (ch <= 25) launch_packed<DT, 256, 25>(lp, labels, n, vp, v, loss, st);
+    else return false;
+  } else {
+    if (ch <= 8) launch_packed<DT, 512, 8>(lp, labels, n, vp, v, loss, st);
+    else if (ch <= 13) launch_packed<DT, 512, 13>(lp, labels, n, vp, v, loss, st);
+    else if (ch <= 16) launch_packed<DT, 512, 16>(lp, labels, n, vp, v, loss, st);
+    else return false;
+  }
+  return true;
+}
+
+// Measured at the GPT-2 shape (20480 x 50304 bf16, tools/bench_xent.py): fp32-row
+// 1194 us, streaming 1224 us, packed 512 thr 966 us, packed 1024 thr 874 us
+// (4.7 TB/s); Llama-2 vocab (8192 x 32000): 280 / - / 204 / 210 us.
 template <int DT>
 static hipError_t launch_xent_dt(void* logits, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,
-                                 hipStream_t st) {
+                                 int var, hipStream_t st) {
   using S = typename Elem<DT>::S;
   const int64_t per = kXentThreads * 8;
   const int vpt = static_cast<int>((vp + per - 1) / per);
   S* lp = static_cast<S*>(logits);
+  if (var == 0) var = xent_variant();
+  if constexpr (DT != kF32) {
+    if (var == 0) var = (vp + 8191) / 8192 <= 7 ? 5 : (vp + 4095) / 4096 <= 16 ? 4 : 0;
+    if (var >= 3 && launch_packed_dt<DT>(var == 3 ? 256 : var == 4 ? 512 : 1024, logits, labels, n, vp, v, loss, st))
+      return hipGetLastError();
+  }
 #define XENT_CASE(K)                                                                                   \
   case K:                                                                                              \
     hipLaunchKernelGGL((softmax_xent_kernel<DT, K>), dim3(n), dim3(kXentThreads), 0, st, lp, labels, vp, v, loss); \
     break;
-  if (vpt > 8) {
+  if (vpt > 8 || var == 2) {
     const int64_t grid = n < 1024 ? n : 1024;  // persistent
     hipLaunchKernelGGL((softmax_xent_stream_kernel<DT>), dim3(grid), dim3(kStreamThreads), 0, st, lp, labels, n, vp,
                        v, loss);
@@ -191,12 +357,13 @@ static hipError_t launch_xent_dt(void* logits, const int64_t* labels, int64_t n,
 }
 
 hipError_t launch_softmax_xent(int dt, void* logits, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,
-                               hipStream_t st) {
+                               int variant, hipStream_t st) {
   if (n == 0) return hipSuccess;
+  if (reinterpret_cast<uintptr_t>(logits) % 16 != 0) return hipErrorInvalidValue;
   switch (dt) {
-    case kF32: return launch_xent_dt<kF32>(logits, labels, n, vp, v, loss, st);
-    case kBF16: return launch_xent_dt<kBF16>(logits, labels, n, vp, v, loss, st);
-    case kF16: return launch_xent_dt<kF16>(logits, labels, n, vp, v, loss, st);
+    case kF32: return launch_xent_dt<kF32>(logits, labels, n, vp, v, loss, variant, st);
+    case kBF16: return launch_xent_dt<kBF16>(logits, labels, n, vp, v, loss, variant, st);
+    case kF16: return launch_xent_dt<kF16>(logits, labels, n, vp, v, loss, variant, st);
     default: return hipErrorInvalidValue;
   }
 }

@@ -1,5 +1,6 @@
-"""Fused softmax cross-entropy kernel (register-resident and streaming variants)
-vs an fp32 PyTorch reference: per-row loss and the in-place softmax - onehot."""
+"""Fused softmax cross-entropy kernel (fp32-row, streaming and packed 16-bit
+row variants) vs an fp32 PyTorch reference: per-row loss and the in-place
+softmax - onehot."""
 import pytest
 import torch
 
@@ -8,8 +9,12 @@ from distributed_lion_pytorch_amd.ops import fused, hip
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("V", [512, 32000, 50257, 128256])
-def test_softmax_xent_kernel(V, cuda):
+# variant: 0 auto, 1 fp32 row in registers, 2 streaming, 4 / 5 packed row (512 / 1024 threads)
+CASES = [(V, var) for V in (512, 32000, 50257) for var in (0, 1, 2, 4, 5)] + [(128256, 0), (128256, 2)]
+
+
+@pytest.mark.parametrize("V,variant", CASES)
+def test_softmax_xent_kernel(V, variant, cuda):
     hip.require()
     torch.manual_seed(V)
     N = 67
@@ -19,7 +24,7 @@ def test_softmax_xent_kernel(V, cuda):
     labels[::7] = -100
     ref_in = x[:, :V].float()
     y = x.clone()
-    loss = hip.ops().softmax_xent_(y, labels, V)
+    loss = hip.ops().softmax_xent_(y, labels, V, variant)
     valid = labels != -100
     ref_loss = torch.nn.functional.cross_entropy(ref_in, labels.clamp_min(0), reduction="none") * valid
     assert (loss - ref_loss).abs().max().item() < 1e-3

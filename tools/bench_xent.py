@@ -25,4 +25,4 @@ for _ in range(3):
     e.record()
     torch.cuda.synchronize()
     ms = s.elapsed_time(e)
-print(f"xent {ms*1e3:8.1f} us  {2 * N * Vp * 2 / ms / 1e9:7.1f} GB/s (2 passes of the row)")
+print(f"xent {ms*1e3:8.1f} us  {2 * N * Vp * 2 / ms / 1e9:7.2f} TB/s (read + write of the row)")
