@@ -509,7 +509,7 @@ bool gemm_nt_supported(const Tensor& a, const Tensor& b) {
 }
 
 void gemm_nt_launch(const Tensor& a, const Tensor& b, const Tensor& c, const Tensor* bias, const Tensor* aux,
-                    int64_t epi) {
+                    int64_t epi, const Tensor* part = nullptr) {
   check_gemm_operand(a, "a");
   check_gemm_operand(b, "b");
   check_gemm_operand(c, "out");
@@ -521,14 +521,22 @@ void gemm_nt_launch(const Tensor& a, const Tensor& b, const Tensor& c, const Ten
                     bias->numel() == b.size(0),
                 "dlion gemm: bias must be a contiguous bf16 [N] tensor");
   }
-  if (aux) check_gemm_operand(*aux, "aux");
+  if (aux) {
+    check_gemm_operand(*aux, "aux");
+    TORCH_CHECK(aux->size(0) == c.size(0) && aux->size(1) == c.size(1), "dlion gemm: aux must match the output shape");
+  }
+  if (part) {
+    TORCH_CHECK(part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                    part->size(0) == 2 * ((a.size(0) + 255) / 256) && part->size(1) == b.size(0),
+                "dlion gemm: part must be fp32 [2 * ceil(M / 256), N]");
+  }
   const c10::DeviceGuard g(a.device());
   check_hip(dlion::launch_gemm_nt(a.data_ptr(), static_cast<int>(a.stride(0)), b.data_ptr(),
                                   static_cast<int>(b.stride(0)), c.data_ptr(), static_cast<int>(c.stride(0)),
                                   bias ? bias->data_ptr() : nullptr, aux ? aux->data_ptr() : nullptr,
                                   aux ? static_cast<int>(aux->stride(0)) : 0, static_cast<int>(a.size(0)),
                                   static_cast<int>(b.size(0)), static_cast<int>(a.size(1)), static_cast<int>(epi),
-                                  cur_stream()),
+                                  part ? part->data_ptr<float>() : nullptr, cur_stream()),
             "gemm_nt");
 }
 
@@ -572,9 +580,20 @@ bool lt_gemm_nt(const Tensor& a, const Tensor& b, const std::optional<Tensor>& b
                            static_cast<int>(epi), a.device().index(), cur_stream());
 }
 
+// dz = (a . b^T) * gelu'(z + bias) -> (dz [M, N] bf16, part [2 * ceil(M/256), N] fp32 bias-grad partials):
+// the MLP down-projection's input gradient fused with the bias+GELU backward
+std::tuple<Tensor, Tensor> gemm_nt_dgelu(const Tensor& a, const Tensor& b, const Tensor& bias, const Tensor& z,
+                                         bool exact) {
+  auto dz = at::empty({a.size(0), b.size(0)}, a.options());
+  auto part = at::empty({2 * ((a.size(0) + 255) / 256), b.size(0)}, a.options().dtype(at::kFloat));
+  gemm_nt_launch(a, b, dz, &bias, &z, exact ? 5 : 4, &part);
+  return {dz, part};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dlion, m) {
+  m.def("gemm_nt_dgelu(Tensor a, Tensor b, Tensor bias, Tensor z, bool exact) -> (Tensor, Tensor)");
   m.def("lt_gemm_nt(Tensor a, Tensor b, Tensor? bias, int epi, Tensor(a!) out) -> bool");
   m.def("gemm_nt(Tensor a, Tensor b, Tensor? bias) -> Tensor");
   m.def("gemm_nt_out(Tensor a, Tensor b, Tensor? bias, Tensor(a!) out) -> ()");
@@ -640,5 +659,6 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("gemm_nt", &gemm_nt);
   m.impl("gemm_nt_out", &gemm_nt_out);
   m.impl("gemm_nt_gelu", &gemm_nt_gelu);
+  m.impl("gemm_nt_dgelu", &gemm_nt_dgelu);
   m.impl("lt_gemm_nt", &lt_gemm_nt);
 }

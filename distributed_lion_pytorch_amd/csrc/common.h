@@ -151,6 +151,20 @@ __device__ __forceinline__ float gelu_f(float u, bool exact) {
   return 0.5f * u * (1.f + t);
 }
 
+// d gelu(u) / du, matching gelu_f (shared by the bias+GELU backward kernel and
+// the GEMM's DGELU epilogue)
+constexpr float kSqrt2OverPi = 0.7978845608028654f;
+constexpr float kKappa = 0.044715f;
+constexpr float kInvSqrt2 = 0.7071067811865476f;
+constexpr float kInvSqrt2Pi = 0.3989422804014327f;
+
+__device__ __forceinline__ float gelu_grad(float u, bool exact) {
+  if (exact) return 0.5f * (1.f + erff(u * kInvSqrt2)) + u * kInvSqrt2Pi * __expf(-0.5f * u * u);
+  const float u2 = u * u;
+  const float t = fast_tanh(kSqrt2OverPi * (u + kKappa * u2 * u));
+  return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * kSqrt2OverPi * (1.f + 3.f * kKappa * u2);
+}
+
 // ------------------------------------------------------------ vote counting
 // Spread the 8 bits of a byte into the 8 bytes of a u64 (bit j -> bit 8j), so
 // that summing spread bytes over W <= 255 ranks counts 8 votes in parallel.

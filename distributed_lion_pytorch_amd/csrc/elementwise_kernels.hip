@@ -12,18 +12,6 @@
 
 namespace dlion {
 
-constexpr float kSqrt2OverPi = 0.7978845608028654f;
-constexpr float kKappa = 0.044715f;
-constexpr float kInvSqrt2 = 0.7071067811865476f;
-constexpr float kInvSqrt2Pi = 0.3989422804014327f;
-
-__device__ __forceinline__ float gelu_grad(float u, bool exact) {
-  if (exact) return 0.5f * (1.f + erff(u * kInvSqrt2)) + u * kInvSqrt2Pi * __expf(-0.5f * u * u);
-  const float u2 = u * u;
-  const float t = fast_tanh(kSqrt2OverPi * (u + kKappa * u2 * u));
-  return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * kSqrt2OverPi * (1.f + 3.f * kKappa * u2);
-}
-
 // rows x N, 8 columns per thread per step; EXACT selects erf-GELU
 template <bool EXACT>
 __global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const uint16_t* __restrict__ z,

@@ -1,4 +1,4 @@
-// bf16 GEMM with fused epilogues for gfx950:  C[M,N] = A[M,K] . B[N,K]^T  (+ bias, GELU)
+// bf16 GEMM with fused epilogues for gfx950:  C[M,N] = A[M,K] . B[N,K]^T  (+ bias, GELU, DGELU)
 //
 // Both operands K-contiguous ("NT"), fp32 accumulation in MFMA, bf16 output;
 // the bias / bias+GELU of a linear can ride in the epilogue instead of a
@@ -61,6 +61,7 @@ struct GemmArgs {
   uint16_t* C;
   const uint16_t* bias;
   uint16_t* aux;
+  float* part;  // EPI 4/5: [2 * tiles_m][N] fp32 column partial sums of C
   int lda, ldb, ldc, ldaux;
   int M, N, K;
   int tiles_m, tiles_n;
@@ -318,11 +319,11 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
       const int gm = row_base + row;
       if (gm < g.M && gn < g.N) *reinterpret_cast<uint4*>(g.C + (int64_t)gm * g.ldc + gn) = v;
     }
-  } else {
+  } else if constexpr (EPI <= 3) {
     // EPI 2/3: aux = z (bf16, no bias); C = gelu(z + b) evaluated on the ROUNDED z
     // exactly like the unfused GEMM -> bias_gelu path (3: erf GELU).  The GELU
     // runs in the drain, 8 columns per lane (one bias chunk per lane).
-    park([&](float v, int) { return f32_to_bf16(v); });
+    park([&](float v, int) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(v)); });
     float b8[8];
     if (gn < g.N) {
       Elem<kBF16>::load8(g.bias + gn, b8);
@@ -339,10 +340,69 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
         *reinterpret_cast<uint4*>(g.aux + (int64_t)gm * g.ldaux + gn) = v;
         float z[8];
         Elem<kBF16>::load8(reinterpret_cast<const uint16_t*>(&v), z);
+        bf16x8 hb;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) z[j] = gelu_f(z[j] + b8[j], EPI == 3);
-        Elem<kBF16>::store8(g.C + (int64_t)gm * g.ldc + gn, z);
+        for (int j = 0; j < 8; ++j) hb[j] = static_cast<__bf16>(gelu_f(z[j] + b8[j], EPI == 3));
+        *reinterpret_cast<bf16x8*>(g.C + (int64_t)gm * g.ldc + gn) = hb;
       }
+    }
+  } else {
+    // EPI 4/5 (DGELU, the MLP down-projection's input gradient): g = A.B^T is
+    // rounded to bf16 (what the unfused GEMM stores), then C = g * gelu'(z + b)
+    // with z = aux (the up-projection's pre-activation, an INPUT here) -- the
+    // bias+GELU backward kernel's pass over [tokens, 4C] rides in the drain.
+    // Each wave also sums its 128 rows of C (bf16-rounded, as that kernel does)
+    // per column: one fp32 partial row per wave, part[2 * tm + wr][n], for the
+    // up-projection's bias gradient.
+    // the lane's 16 rows x 8 columns of z are loaded up front -- in flight
+    // while the accumulators are parked, and held in the registers the parked
+    // accumulators free -- instead of one dependent load per drain row
+    uint4 zr[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int gm = min(row_base + i * 8 + (lane >> 3), g.M - 1);
+      zr[i] = gn < g.N ? *reinterpret_cast<const uint4*>(g.aux + (int64_t)gm * g.ldaux + gn) : make_uint4(0, 0, 0, 0);
+    }
+    park([&](float v, int) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(v)); });
+    float b8[8], cs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cs[j] = 0.f;
+    if (gn < g.N) {
+      Elem<kBF16>::load8(g.bias + gn, b8);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b8[j] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = i * 8 + (lane >> 3);
+      const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((ch ^ (row & 7)) << 4));
+      const int gm = row_base + row;
+      if (gm < g.M && gn < g.N) {
+        float gv[8], z[8], o[8];
+        Elem<kBF16>::load8(reinterpret_cast<const uint16_t*>(&v), gv);
+        Elem<kBF16>::load8(reinterpret_cast<const uint16_t*>(&zr[i]), z);
+        bf16x8 ob;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          o[j] = gv[j] * gelu_grad(z[j] + b8[j], EPI == 5);
+          ob[j] = static_cast<__bf16>(o[j]);  // v_cvt_pk_bf16_f32 (RNE)
+          cs[j] += static_cast<float>(ob[j]);  // the bias gradient sums the stored bf16 values
+        }
+        *reinterpret_cast<bf16x8*>(g.C + (int64_t)gm * g.ldc + gn) = ob;
+      }
+    }
+    // fold the 8 lanes that share this lane's 8 columns (lane bits 3..5)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      cs[j] += __shfl_xor(cs[j], 8);
+      cs[j] += __shfl_xor(cs[j], 16);
+      cs[j] += __shfl_xor(cs[j], 32);
+    }
+    if (lane < 8 && gn < g.N) {
+      float* dst = g.part + (int64_t)(2 * tm + wr) * g.N + gn;
+      *reinterpret_cast<float4*>(dst) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
     }
   }
 }
@@ -350,18 +410,20 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
 }  // namespace
 
 hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
-                          void* aux, int ldaux, int M, int N, int K, int epi, hipStream_t st) {
+                          void* aux, int ldaux, int M, int N, int K, int epi, float* part, hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
   if (K % 128 != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 8 != 0) return hipErrorInvalidValue;
   if ((int64_t)M * lda >= (1ll << 31) || (int64_t)N * ldb >= (1ll << 31)) return hipErrorInvalidValue;
   if (epi >= 2 && (aux == nullptr || ldaux % 8 != 0)) return hipErrorInvalidValue;
   if (epi >= 1 && (bias == nullptr || reinterpret_cast<uintptr_t>(bias) % 16 != 0)) return hipErrorInvalidValue;
+  if (epi >= 4 && (part == nullptr || reinterpret_cast<uintptr_t>(part) % 16 != 0)) return hipErrorInvalidValue;
   GemmArgs g;
   g.A = static_cast<const uint16_t*>(A);
   g.B = static_cast<const uint16_t*>(B);
   g.C = static_cast<uint16_t*>(C);
   g.bias = static_cast<const uint16_t*>(bias);
   g.aux = static_cast<uint16_t*>(aux);
+  g.part = part;
   g.lda = lda;
   g.ldb = ldb;
   g.ldc = ldc;
@@ -377,6 +439,8 @@ hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* 
     case 1: hipLaunchKernelGGL(gemm_nt_kernel<1>, grid, block, 0, st, g); break;
     case 2: hipLaunchKernelGGL(gemm_nt_kernel<2>, grid, block, 0, st, g); break;
     case 3: hipLaunchKernelGGL(gemm_nt_kernel<3>, grid, block, 0, st, g); break;
+    case 4: hipLaunchKernelGGL(gemm_nt_kernel<4>, grid, block, 0, st, g); break;
+    case 5: hipLaunchKernelGGL(gemm_nt_kernel<5>, grid, block, 0, st, g); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

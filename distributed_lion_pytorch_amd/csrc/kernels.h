@@ -55,10 +55,12 @@ hipError_t launch_sum_partials(const float* part, int S, int64_t n, int64_t ld, 
 hipError_t launch_colsum(const void* x, float* part, int parts, int64_t rows, int N, hipStream_t st);
 
 // ---- bf16 GEMM C[M,N] = A[M,K] . B[N,K]^T with fused epilogue (gemm.hip)
-// epi: 0 plain, 1 + bias, 2 aux = z, C = gelu_tanh(z + bias), 3 the same with erf GELU.
+// epi: 0 plain, 1 + bias, 2 aux = z, C = gelu_tanh(z + bias), 3 the same with erf GELU,
+// 4 C = bf16(A.B^T) * gelu_tanh'(aux + bias) with aux an input and part [2 * ceil(M/256)][N]
+// fp32 column sums of C (bias gradient partials), 5 the same with erf GELU.
 // Needs K % 128 == 0, N % 8 == 0, leading dims % 8 == 0.
 hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
-                          void* aux, int ldaux, int M, int N, int K, int epi, hipStream_t st);
+                          void* aux, int ldaux, int M, int N, int K, int epi, float* part, hipStream_t st);
 
 // ---- LM head cross-entropy (xent_kernels.hip)
 // variant 0 = auto (DLION_XENT env override), 1 fp32-row, 2 streaming, 3/4/5 packed 16-bit row (256/512/1024 thr)

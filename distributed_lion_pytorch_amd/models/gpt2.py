@@ -92,7 +92,14 @@ class MLP(nn.Module):
 
     def forward(self, x, proj_bias: bool = True):
         shp = x.shape[:-1]
-        h = fused.linear_gelu(x.reshape(-1, x.shape[-1]), self.c_fc.weight, self.c_fc.bias, exact=self.exact_gelu)
+        x2 = x.reshape(-1, x.shape[-1])
+        if torch.is_grad_enabled() and x2.is_cuda:
+            # training: the whole MLP is one autograd op with the bias+GELU
+            # forward and backward fused into GEMM epilogues (ops/fused._MLP)
+            y = fused.mlp_gelu(x2, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight,
+                               exact=self.exact_gelu).view(*shp, -1)
+            return y + self.c_proj.bias if proj_bias else y
+        h = fused.linear_gelu(x2, self.c_fc.weight, self.c_fc.bias, exact=self.exact_gelu)
         h = h.view(*shp, -1)
         return self.c_proj(h) if proj_bias else linear_kn(h, self.c_proj.weight, None)
 

@@ -375,6 +375,97 @@ def linear_gelu(x2d: torch.Tensor, w_in_out: torch.Tensor, bias: torch.Tensor, e
     return bias_gelu(linear_kn(x2d, w_in_out, None), bias, exact)
 
 
+_DGELU_FUSED = os.environ.get("DLION_DGELU_GEMM", "1") != "0"  # A/B switch: fused DGELU backward GEMM
+_GELU_FUSED = os.environ.get("DLION_GELU_GEMM", "1") != "0"  # A/B switch: fused GELU forward GEMM
+
+
+def _own_gemm_ok(a: torch.Tensor, b_nk: torch.Tensor) -> bool:
+    """Shapes the own NT GEMM (csrc/gemm.hip) takes: a [M, K], b [N, K]."""
+    return (a.dim() == 2 and b_nk.dim() == 2 and a.shape[1] == b_nk.shape[1] and a.shape[1] % 128 == 0
+            and b_nk.shape[0] % 8 == 0 and a.stride(1) == 1 and a.stride(0) % 8 == 0 and b_nk.is_contiguous()
+            and a.data_ptr() % 16 == 0 and a.shape[0] * a.stride(0) < 2 ** 31)
+
+
+class _MLP(torch.autograd.Function):
+    """y = gelu(x @ Wfc + b) @ Wproj for the GPT-2 MLP (both weights in HF
+    Conv1D [in, out] layout, no output bias: the caller's residual+norm kernel
+    adds it).  Measured at the bench shape (20480 tokens, C 768, 4C 3072;
+    tools/bench_dgelu.py), per layer:
+
+    * forward: the own NT GEMM with the bias+GELU epilogue writes h and the
+      pre-activation z in one pass -- 129 us against hipBLASLt + the separate
+      bias+GELU kernel's 140 us;
+    * backward: the down-projection's input gradient and the bias+GELU
+      backward are ONE kernel -- the own GEMM's DGELU epilogue rounds
+      g = dy . Wproj^T to bf16 like the unfused GEMM, multiplies by gelu'(z+b)
+      in its drain and emits per-wave column sums for the bias gradient
+      (144 us against hipBLASLt + bias_gelu_bwd's 177 us).
+
+    Weight gradients are split-K GEMMs deposited straight into .grad inside a
+    gradient-accumulation fusion window (ops/linear.py), like every linear."""
+
+    @staticmethod
+    def forward(ctx, x, w_fc, b_fc, w_proj, exact):
+        from .linear import _fuse_target, transposed_weight
+
+        wfc_t = transposed_weight(w_fc) if isinstance(w_fc, torch.nn.Parameter) else w_fc.t().contiguous()
+        if _GELU_FUSED and _own_gemm_ok(x, wfc_t):
+            h, z = hip.ops().gemm_nt_gelu(x, wfc_t, b_fc, exact)
+        else:
+            z = F.linear(x, wfc_t)
+            h = hip.ops().bias_gelu_fwd(z, b_fc, exact)
+        ctx.save_for_backward(x, z, h, w_fc, b_fc, w_proj)
+        ctx.exact = exact
+        ctx.fuse = (_fuse_target(w_fc), _fuse_target(w_proj))
+        ctx.fused_b = _fused_params(b_fc)[0]
+        wp_t = transposed_weight(w_proj) if isinstance(w_proj, torch.nn.Parameter) else w_proj.t()
+        return F.linear(h, wp_t)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .linear import deposit_grad, wgrad, wgrad_into
+
+        x, z, h, w_fc, b_fc, w_proj = ctx.saved_tensors
+        dy = dy.contiguous()
+        if _DGELU_FUSED and _own_gemm_ok(dy, w_proj):
+            dz, part = hip.ops().gemm_nt_dgelu(dy, w_proj, b_fc, z, ctx.exact)
+        else:
+            dz, part = hip.ops().bias_gelu_bwd(dy @ w_proj.t(), z, b_fc, ctx.exact, max(1, min(1024, z.shape[0] // 8)))
+        grads = [None] * 5
+        if ctx.needs_input_grad[0]:
+            grads[0] = F.linear(dz, w_fc)  # dx = dz . Wfc^T, Wfc stored [C, 4C]
+        for i, (w, a, g) in ((1, (w_fc, x, dz)), (3, (w_proj, h, dy))):
+            if ctx.needs_input_grad[i]:
+                if ctx.fuse[(i - 1) // 2]:
+                    wgrad_into(a, g, w)
+                else:
+                    grads[i] = wgrad(a, g)
+        if ctx.needs_input_grad[2]:
+            if ctx.fused_b is not None:
+                deposit_grad(ctx.fused_b, part)
+            else:
+                grads[2] = _sum_rows(part)
+        return tuple(grads)
+
+
+def mlp_gelu(x: torch.Tensor, w_fc: torch.Tensor, b_fc: torch.Tensor, w_proj: torch.Tensor,
+             exact: bool = False) -> torch.Tensor:
+    """gelu(x @ Wfc + b) @ Wproj (weights stored [in, out]) with the fused
+    GEMM epilogues of :class:`_MLP`; plain PyTorch off the GPU path."""
+    shp = x.shape[:-1] + (w_proj.shape[1],)
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.is_cuda and _use_hip(x2):
+        from .linear import autocast_inputs
+
+        x2, w_fc, b_fc, w_proj = autocast_inputs(x2, w_fc, b_fc, w_proj)
+        if (x2.dtype == w_fc.dtype == b_fc.dtype == w_proj.dtype == torch.bfloat16 and w_fc.shape[1] % 8 == 0
+                and b_fc.is_contiguous() and w_fc.is_contiguous() and w_proj.is_contiguous()):
+            with torch.autocast("cuda", enabled=False):
+                return _MLP.apply(x2.contiguous(), w_fc, b_fc, w_proj, bool(exact)).view(shp)
+    h = F.gelu(x2 @ w_fc + b_fc, approximate="none" if exact else "tanh")
+    return (h @ w_proj).view(shp)
+
+
 # ------------------------------------------------------------------ attention
 def _attn_ok(x: torch.Tensor, T: int, D: int) -> bool:
     return x.dtype == torch.bfloat16 and D in (64, 128) and T % 64 == 0 and _use_hip(x)
