@@ -346,7 +346,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     }
   // under dropout the stored row constant is lse + log2(1-p): the backward's
   // exp2(s*scale - lse') is then P/(1-p) directly, and with delta' = delta*(1-p)
-  // (attn_delta_kernel) both backward kernels drop their per-element 1/(1-p)
+  // (computed in the dQ kernel) both backward kernels drop their per-element 1/(1-p)
   // multiplies: dS = P'*(keep ? dP : 0) - P'*delta', Pd = keep ? P' : 0
   if (hf == 0) a.lse[static_cast<int64_t>(bh) * a.T + q] = m + log2f(l) + (DROP ? -log2f(a.inv_keep) : 0.f);
 }
@@ -373,7 +373,21 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
       dof[s] = ld8(dop + 16 * s);
     }
     lse2 = a.lse[static_cast<int64_t>(bh) * a.T + q];
-    dlt = a.delta[static_cast<int64_t>(bh) * a.T + q];
+    // delta = rowsum(dO * O) for this wave's 32 rows, computed here (the dQ
+    // kernel already holds the dO rows) and published for the dKV kernel that
+    // runs next -- instead of a separate pass over O and dO.  Lanes r and r+32
+    // hold the two halves of row q.
+    const __bf16* op = a.o + b * a.o_sb + static_cast<int64_t>(q) * a.o_st + h * a.o_sh + 8 * hf;
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      const bf16x8 of = ld8(op + 16 * s);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += static_cast<float>(of[j]) * static_cast<float>(dof[s][j]);
+    }
+    dlt = xsum32(part);
+    if (a.thresh16) dlt /= a.inv_keep;  // delta * (1-p), see the forward's lse note
+    if (hf == 0) const_cast<float*>(a.delta)[static_cast<int64_t>(bh) * a.T + q] = dlt;
   }
   const uint32_t thr_hi = a.thresh16 << 16;
   const uint32_t arow = drop_row(a.seed, bh, q);
@@ -577,27 +591,6 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
     }
 }
 
-// ------------------------------------------------------------- delta = rowsum(dO*O)
-// D/8 lanes per row, 8 bf16 (16 B) per lane
-template <int D>
-__global__ void __launch_bounds__(256) attn_delta_kernel(AttnArgs a) {
-  constexpr int LPR = D / 8;  // lanes per row
-  const int64_t row = static_cast<int64_t>(blockIdx.x) * (256 / LPR) + threadIdx.x / LPR;
-  const int64_t nrows = static_cast<int64_t>(a.B) * a.H * a.T;
-  if (row >= nrows) return;
-  const int sub = threadIdx.x % LPR;
-  const int bh = static_cast<int>(row / a.T), q = static_cast<int>(row % a.T);
-  const int b = bh / a.H, h = bh % a.H;
-  const int64_t off = b * a.o_sb + static_cast<int64_t>(q) * a.o_st + h * a.o_sh + 8 * sub;
-  const bf16x8 o = ld8(a.o + off), d = ld8(a.dout + off);
-  float acc = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) acc += static_cast<float>(o[j]) * static_cast<float>(d[j]);
-#pragma unroll
-  for (int s = LPR / 2; s > 0; s >>= 1) acc += __shfl_xor(acc, s, LPR);
-  if (sub == 0) const_cast<float*>(a.delta)[row] = a.thresh16 ? acc / a.inv_keep : acc;  // delta * (1-p), see fwd
-}
-
 // ------------------------------------------------------------------ launchers
 // ceil(tiles / 4) blocks of 4 waves per head
 static inline int64_t tile_blocks(int64_t nbh, int T) { return nbh * (((T >> 5) + 3) >> 2); }
@@ -621,17 +614,16 @@ hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
 }
 
 hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) {
-  const int64_t rows = static_cast<int64_t>(a.B) * a.H * a.T;
   const dim3 bq(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T)));
   const dim3 bkv(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.Hkv, a.T)));
+  // dQ first: it also computes delta = rowsum(dO * O), which dKV reads
 #define BWD(DD)                                                                                           \
-  hipLaunchKernelGGL((attn_delta_kernel<DD>), dim3((rows * (DD / 8) + 255) / 256), dim3(256), 0, st, a); \
   if (drop) {                                                                                             \
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), bkv, dim3(256), 0, st, a);                       \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, true>), bq, dim3(256), 0, st, a);                         \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), bkv, dim3(256), 0, st, a);                       \
   } else {                                                                                                \
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), bkv, dim3(256), 0, st, a);                      \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, false>), bq, dim3(256), 0, st, a);                        \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), bkv, dim3(256), 0, st, a);                      \
   }
   if (D == 64) {
     BWD(64)
