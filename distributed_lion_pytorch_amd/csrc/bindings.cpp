@@ -580,6 +580,77 @@ bool lt_gemm_nt(const Tensor& a, const Tensor& b, const std::optional<Tensor>& b
                            static_cast<int>(epi), a.device().index(), cur_stream());
 }
 
+// ------------------------------------------------------------- embedding
+void check_bf16_contig(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous() &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              "dlion embed: ", name, " must be a contiguous, 16-byte aligned bf16 GPU tensor");
+}
+
+// out [B, T, C] = dropout(wte[ids] + wpe[t]) for ids [B, T]
+Tensor embed_fwd(const Tensor& ids, const Tensor& wte, const Tensor& wpe, double p, int64_t seed) {
+  check_dev(ids, "ids");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.dim() == 2, "dlion embed: ids must be int64 [B, T]");
+  check_bf16_contig(wte, "wte");
+  check_bf16_contig(wpe, "wpe");
+  const int64_t C = wte.size(1), T = ids.size(1);
+  TORCH_CHECK(wpe.size(1) == C && T <= wpe.size(0) && C % 8 == 0, "dlion embed: shape mismatch / C % 8 != 0");
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dlion embed: dropout must be in [0, 1)");
+  const c10::DeviceGuard g(ids.device());
+  auto out = at::empty({ids.size(0), T, C}, wte.options());
+  const auto dp = drop_params(p);
+  check_hip(dlion::launch_embed_fwd(ids.data_ptr<int64_t>(), wte.data_ptr(), wpe.data_ptr(), out.data_ptr(), ids.numel(),
+                                    static_cast<int>(C), static_cast<int>(T), wte.size(0), static_cast<uint32_t>(seed),
+                                    dp.first, dp.second, cur_stream()),
+            "embed_fwd");
+  return out;
+}
+
+// dwte[sid] += segmented row sums of the dropout-backward of dx; dwpe (+)= batch sums per position
+void embed_bwd_(const Tensor& dx, const std::optional<Tensor>& sid, const std::optional<Tensor>& perm,
+                const std::optional<Tensor>& dwte, const std::optional<Tensor>& dwpe, int64_t T, bool pos_accumulate,
+                double p, int64_t seed) {
+  check_bf16_contig(dx, "dx");
+  const int64_t C = dx.size(-1), n = dx.numel() / C;
+  TORCH_CHECK(T > 0 && n % T == 0 && C % 8 == 0, "dlion embed: dx must be [B*T, C] with C % 8 == 0");
+  int64_t V = 0;
+  if (dwte.has_value()) {
+    check_bf16_contig(*dwte, "dwte");
+    TORCH_CHECK(dwte->dim() == 2 && dwte->size(1) == C, "dlion embed: dwte must be [V, C]");
+    TORCH_CHECK(sid.has_value() && perm.has_value() && sid->numel() == n && perm->numel() == n &&
+                    sid->scalar_type() == at::kLong && perm->scalar_type() == at::kLong && sid->is_contiguous() &&
+                    perm->is_contiguous(),
+                "dlion embed: the token gradient needs sorted ids and their permutation (int64 [n])");
+    V = dwte->size(0);
+  }
+  if (dwpe.has_value()) {
+    check_bf16_contig(*dwpe, "dwpe");
+    TORCH_CHECK(dwpe->size(-1) == C && dwpe->size(0) >= T, "dlion embed: dwpe must be [>= T, C]");
+  }
+  const c10::DeviceGuard g(dx.device());
+  const auto dp = drop_params(p);
+  check_hip(dlion::launch_embed_bwd(dx.data_ptr(), dwte.has_value() ? sid->data_ptr<int64_t>() : nullptr,
+                                    dwte.has_value() ? perm->data_ptr<int64_t>() : nullptr,
+                                    dwte.has_value() ? dwte->data_ptr() : nullptr,
+                                    dwpe.has_value() ? dwpe->data_ptr() : nullptr, n, static_cast<int>(C),
+                                    static_cast<int>(T), V, pos_accumulate ? 1 : 0, static_cast<uint32_t>(seed),
+                                    dp.first, dp.second, cur_stream()),
+            "embed_bwd");
+}
+
+// y (+)= bf16(x * bf16(s)), s a 1-element fp32 device tensor (no host sync)
+void scale_acc_(const Tensor& x, const Tensor& s, const Tensor& y, bool accumulate) {
+  check_bf16_contig(x, "x");
+  check_bf16_contig(y, "y");
+  check_dev(s, "s");
+  TORCH_CHECK(s.scalar_type() == at::kFloat && s.numel() >= 1, "dlion scale_acc: s must be float32");
+  TORCH_CHECK(x.numel() == y.numel() && x.numel() % 8 == 0, "dlion scale_acc: size mismatch / numel % 8 != 0");
+  const c10::DeviceGuard g(x.device());
+  check_hip(dlion::launch_scale_acc(x.data_ptr(), s.data_ptr<float>(), y.data_ptr(), x.numel(), accumulate ? 1 : 0,
+                                    cur_stream()),
+            "scale_acc");
+}
+
 // dz = (a . b^T) * gelu'(z + bias) -> (dz [M, N] bf16, part [2 * ceil(M/256), N] fp32 bias-grad partials):
 // the MLP down-projection's input gradient fused with the bias+GELU backward
 std::tuple<Tensor, Tensor> gemm_nt_dgelu(const Tensor& a, const Tensor& b, const Tensor& bias, const Tensor& z,
@@ -594,6 +665,11 @@ std::tuple<Tensor, Tensor> gemm_nt_dgelu(const Tensor& a, const Tensor& b, const
 
 TORCH_LIBRARY(dlion, m) {
   m.def("gemm_nt_dgelu(Tensor a, Tensor b, Tensor bias, Tensor z, bool exact) -> (Tensor, Tensor)");
+  m.def("embed_fwd(Tensor ids, Tensor wte, Tensor wpe, float p, int seed) -> Tensor");
+  m.def(
+      "embed_bwd_(Tensor dx, Tensor? sid, Tensor? perm, Tensor(a!)? dwte, Tensor(b!)? dwpe, int T, bool pos_accumulate,"
+      " float p, int seed) -> ()");
+  m.def("scale_acc_(Tensor x, Tensor s, Tensor(a!) y, bool accumulate) -> ()");
   m.def("lt_gemm_nt(Tensor a, Tensor b, Tensor? bias, int epi, Tensor(a!) out) -> bool");
   m.def("gemm_nt(Tensor a, Tensor b, Tensor? bias) -> Tensor");
   m.def("gemm_nt_out(Tensor a, Tensor b, Tensor? bias, Tensor(a!) out) -> ()");
@@ -660,5 +736,8 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("gemm_nt_out", &gemm_nt_out);
   m.impl("gemm_nt_gelu", &gemm_nt_gelu);
   m.impl("gemm_nt_dgelu", &gemm_nt_dgelu);
+  m.impl("embed_fwd", &embed_fwd);
+  m.impl("embed_bwd_", &embed_bwd_);
+  m.impl("scale_acc_", &scale_acc_);
   m.impl("lt_gemm_nt", &lt_gemm_nt);
 }

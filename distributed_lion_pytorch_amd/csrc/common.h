@@ -176,6 +176,32 @@ __device__ __forceinline__ uint64_t spread8(uint32_t b) {
   return x;
 }
 
+// ------------------------------------------------------- dropout keep hash
+// Stateless dropout mask shared by the norm and embedding kernels (and
+// ops/fused.norm_dropout_keep on the host): element e of a flat index space
+// keeps iff 16 bits of mix32(seed ^ (e >> 1) * golden ^ (e >> 33)) >= thresh16.
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// keep bits for 4 consecutive elements starting at flat index idx (idx % 4 == 0):
+// two 32-bit hashes, 16 bits per element
+__device__ __forceinline__ uint32_t keep4(uint32_t seed, uint64_t idx, uint32_t thresh16) {
+  const uint32_t hi = static_cast<uint32_t>(idx >> 33);
+  const uint32_t h0 = mix32(seed ^ static_cast<uint32_t>(idx >> 1) * 0x9E3779B1u ^ hi);
+  const uint32_t h1 = mix32(seed ^ static_cast<uint32_t>((idx >> 1) + 1) * 0x9E3779B1u ^ hi);
+  uint32_t k = 0;
+  k |= ((h0 & 0xffffu) >= thresh16) << 0;
+  k |= ((h0 >> 16) >= thresh16) << 1;
+  k |= ((h1 & 0xffffu) >= thresh16) << 2;
+  k |= ((h1 >> 16) >= thresh16) << 3;
+  return k;
+}
+
 // ------------------------------------------------------------- Philox4x32-10
 // Counter-based RNG for the stochastic-binarization encoder: every
 // (seed, element, step) triple gets an independent, reproducible draw.

@@ -62,6 +62,16 @@ hipError_t launch_colsum(const void* x, float* part, int parts, int64_t rows, in
 hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
                           void* aux, int ldaux, int M, int N, int K, int epi, float* part, hipStream_t st);
 
+// ---- token + position embedding with dropout, scaled gradient accumulation (embedding.hip)
+hipError_t launch_embed_fwd(const int64_t* ids, const void* wte, const void* wpe, void* out, int64_t n, int C, int T,
+                            int64_t V, uint32_t seed, uint32_t thresh16, float inv_keep, hipStream_t st);
+// dwte / dwpe nullable; sid / perm = stably sorted ids and their positions (needed with dwte)
+hipError_t launch_embed_bwd(const void* dx, const int64_t* sid, const int64_t* perm, void* dwte, void* dwpe, int64_t n,
+                            int C, int T, int64_t V, int pos_accumulate, uint32_t seed, uint32_t thresh16,
+                            float inv_keep, hipStream_t st);
+// y (+)= bf16(x * bf16(s[0])), s a device fp32 scalar
+hipError_t launch_scale_acc(const void* x, const float* s, void* y, int64_t n, int accumulate, hipStream_t st);
+
 // ---- LM head cross-entropy (xent_kernels.hip)
 // variant 0 = auto (DLION_XENT env override), 1 fp32-row, 2 streaming, 3/4/5 packed 16-bit row (256/512/1024 thr)
 hipError_t launch_softmax_xent(int dt, void* logits, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,

@@ -131,11 +131,8 @@ class GPT2Model(nn.Module):
         self.gradient_checkpointing = False
 
     def forward(self, input_ids):
-        T = input_ids.shape[1]
-        pos = torch.arange(T, device=input_ids.device)
-        x = self.wte(input_ids) + self.wpe(pos)[None]
-        if self.training and self.embd_pdrop > 0:
-            x = F.dropout(x, self.embd_pdrop, True)
+        p = self.embd_pdrop if self.training else 0.0
+        x = fused.embed(input_ids, self.wte.weight, self.wpe.weight, p)  # gather + add + dropout, one kernel
         if self.gradient_checkpointing and self.training:
             for blk in self.h:
                 x = torch.utils.checkpoint.checkpoint(blk, x, use_reentrant=False)

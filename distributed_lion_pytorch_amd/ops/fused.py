@@ -466,6 +466,70 @@ def mlp_gelu(x: torch.Tensor, w_fc: torch.Tensor, b_fc: torch.Tensor, w_proj: to
     return (h @ w_proj).view(shp)
 
 
+# ------------------------------------------------------------ token embedding
+class _Embed(torch.autograd.Function):
+    """x = dropout(wte[ids] + wpe[t]) for ids [B, T] (csrc/embedding.hip).
+    Backward: the token gradient is a deterministic segmented sum over the
+    stably sorted ids, added in place into wte.grad inside a fusion window
+    (GPT-2's tied wte already holds the LM head's gradient there), instead of
+    ATen's dense [V, C] embedding gradient + AccumulateGrad pass."""
+
+    @staticmethod
+    def forward(ctx, ids, wte, wpe, p, seed):
+        from .linear import _fuse_target
+
+        out = hip.ops().embed_fwd(ids, wte, wpe, p, seed)
+        ctx.save_for_backward(ids)
+        ctx.p, ctx.seed = p, seed
+        ctx.wte = wte if _fuse_target(wte) else None
+        ctx.wpe = wpe if _fuse_target(wpe) else None
+        ctx.shapes = (wte.shape, wpe.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (ids,) = ctx.saved_tensors
+        T = ids.shape[1]
+        dx = dout.contiguous()
+        ops = hip.ops()
+        gw = gp = None
+        sid = perm = dwte = dwpe = None
+        pos_acc = False
+
+        def target(param, shape, dev, dtype):
+            if param is not None:
+                if param.grad is None:
+                    param.grad = torch.zeros(shape, dtype=dtype, device=dev)
+                if param.grad.is_contiguous() and param.grad.dtype == dtype:
+                    return param.grad, None
+            buf = torch.zeros(shape, dtype=dtype, device=dev)
+            return buf, buf
+
+        if ctx.needs_input_grad[1]:
+            sid, perm = torch.sort(ids.reshape(-1), stable=True)
+            dwte, gw = target(ctx.wte, ctx.shapes[0], dx.device, dx.dtype)
+        if ctx.needs_input_grad[2]:
+            dwpe, gp = target(ctx.wpe, ctx.shapes[1], dx.device, dx.dtype)
+            pos_acc = True  # rows >= T stay as they are (zeros when fresh)
+        ops.embed_bwd_(dx, sid, perm, dwte, dwpe, T, pos_acc, ctx.p, ctx.seed)
+        return None, gw, gp, None, None
+
+
+_EMBED_FUSED = os.environ.get("DLION_FUSED_EMBED", "1") != "0"  # A/B switch for _Embed
+
+
+def embed(ids: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor, p: float) -> torch.Tensor:
+    """dropout(wte[ids] + wpe[arange(T)]) for ids [B, T]: one kernel each way on
+    the GPU (bf16), the ATen chain elsewhere."""
+    T = ids.shape[1]
+    if (_EMBED_FUSED and ids.is_cuda and wte.dtype == torch.bfloat16 and wpe.dtype == torch.bfloat16 and wte.shape[1] % 8 == 0
+            and wte.is_contiguous() and wpe.is_contiguous() and T <= wpe.shape[0] and _use_hip(wte)):
+        with torch.autocast("cuda", enabled=False):
+            return _Embed.apply(ids.contiguous(), wte, wpe, float(p), _new_seed() if p > 0 else 0)
+    x = F.embedding(ids, wte) + F.embedding(torch.arange(T, device=ids.device), wpe)[None]
+    return F.dropout(x, p, True) if p > 0 else x
+
+
 # ------------------------------------------------------------------ attention
 def _attn_ok(x: torch.Tensor, T: int, D: int) -> bool:
     return x.dtype == torch.bfloat16 and D in (64, 128) and T % 64 == 0 and _use_hip(x)
@@ -656,15 +720,40 @@ class _LMHeadCE(torch.autograd.Function):
             dw = (logits.t() @ h2d)[:v] if ctx.needs_input_grad[1] else None
             ctx.save_for_backward(dh, dw if dw is not None else dh.new_empty(0), n_valid)
             ctx.has_dw = dw is not None
+            from .linear import _fuse_target
+
+            ctx.weight = weight if dw is not None and _fuse_target(weight) else None
         del logits
         return loss
 
     @staticmethod
     def backward(ctx, g):
         dh, dw, n_valid = ctx.saved_tensors
-        scale = (g / n_valid).to(dh.dtype)
-        gh = dh * scale if ctx.needs_input_grad[0] else None
-        gw = dw * scale if ctx.has_dw and ctx.needs_input_grad[1] else None
+        if not (dh.is_cuda and dh.dtype == torch.bfloat16 and _use_hip(dh)):
+            scale = (g / n_valid).to(dh.dtype)
+            gh = dh * scale if ctx.needs_input_grad[0] else None
+            gw = dw * scale if ctx.has_dw and ctx.needs_input_grad[1] else None
+            return gh, gw, None, None
+        # one pass each: bf16(x * bf16(g / n)) with the scale on the device; the
+        # weight gradient is added straight into .grad inside a fusion window
+        # (tied GPT-2 wte: the embedding backward then adds its rows in place)
+        s = (g.float() / n_valid).reshape(1)
+        ops = hip.ops()
+        gh = gw = None
+        if ctx.needs_input_grad[0]:
+            gh = torch.empty_like(dh)
+            ops.scale_acc_(dh, s, gh, False)
+        if ctx.has_dw and ctx.needs_input_grad[1]:
+            w = ctx.weight
+            if w is not None and w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == dw.dtype:
+                ops.scale_acc_(dw, s, w.grad, True)
+            else:
+                out = torch.empty_like(dw)
+                ops.scale_acc_(dw, s, out, False)
+                if w is not None:
+                    w.grad = out if w.grad is None else w.grad + out
+                else:
+                    gw = out
         return gh, gw, None, None
 
 
