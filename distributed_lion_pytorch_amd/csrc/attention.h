@@ -17,6 +17,8 @@ struct AttnArgs {
   __bf16* dv;
   float* lse;          // [B][H][T] base-2 log-sum-exp of scaled scores
   const float* delta;  // [B][H][T] rowsum(dO * O)
+  float* colsum;       // nullable, [B * T/32][3 * H * D]: per-32-row column sums of dq | dk | dv (packed
+                       // qkv bias gradient partials; needs H == Hkv)
   int64_t q_sb, q_st, q_sh;
   int64_t k_sb, k_st, k_sh;
   int64_t v_sb, v_st, v_sh;

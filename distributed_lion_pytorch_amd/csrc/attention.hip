@@ -455,6 +455,19 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
       const int qq = qtile * 32 + acc_row(reg, hf);
       base[static_cast<int64_t>(qq) * a.dq_st + 32 * t + r] = static_cast<__bf16>(dq[t][reg] * a.scale);
     }
+  if (a.colsum != nullptr) {
+    // the c_attn bias gradient's partials: column sums of the stored (bf16) dq
+    // over this wave's 32 rows; lanes r and r+32 hold the two row halves
+    float* cs = a.colsum + static_cast<int64_t>(b * (a.T >> 5) + qtile) * (3 * a.H * D) + h * D;
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t) {
+      float sum = 0.f;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) sum += static_cast<float>(static_cast<__bf16>(dq[t][reg] * a.scale));
+      sum = xsum32(sum);
+      if (hf == 0) cs[32 * t + r] = sum;
+    }
+  }
 }
 
 // -------------------------------------------------------------- backward dKV
@@ -589,6 +602,24 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
       dkb[off] = static_cast<__bf16>(dk[t][reg] * a.scale);
       dvb[off] = static_cast<__bf16>(dv[t][reg]);
     }
+  if (a.colsum != nullptr) {  // bias-gradient partials of the k and v columns (H == Hkv)
+    float* cs = a.colsum + static_cast<int64_t>(b * ntiles + ktile) * (3 * a.H * D) + hk * D;
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t) {
+      float sk = 0.f, sv = 0.f;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        sk += static_cast<float>(static_cast<__bf16>(dk[t][reg] * a.scale));
+        sv += static_cast<float>(static_cast<__bf16>(dv[t][reg]));
+      }
+      sk = xsum32(sk);
+      sv = xsum32(sv);
+      if (hf == 0) {
+        cs[a.H * D + 32 * t + r] = sk;
+        cs[2 * a.H * D + 32 * t + r] = sv;
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------ launchers

@@ -227,7 +227,8 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tens
 }
 
 void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& out, const Tensor& dout,
-              const Tensor& lse, double p, int64_t seed, const Tensor& dq, const Tensor& dk, const Tensor& dv) {
+              const Tensor& lse, double p, int64_t seed, const Tensor& dq, const Tensor& dk, const Tensor& dv,
+              const std::optional<Tensor>& colsum) {
   auto a = attn_args(q, k, v, p, seed);
   check_bthd(out, "out");
   check_bthd(dout, "dout");
@@ -249,6 +250,15 @@ void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
   a.dv = static_cast<__bf16*>(dv.data_ptr());
   a.dq_sb = dq.stride(0); a.dq_st = dq.stride(1); a.dq_sh = dq.stride(2);
   a.dk_sb = dk.stride(0); a.dk_st = dk.stride(1); a.dk_sh = dk.stride(2);
+  a.colsum = nullptr;
+  if (colsum.has_value()) {
+    TORCH_CHECK(a.H == a.Hkv, "dlion attn: bias-gradient partials need H == Hkv");
+    TORCH_CHECK(colsum->is_cuda() && colsum->scalar_type() == at::kFloat && colsum->is_contiguous() &&
+                    colsum->dim() == 2 && colsum->size(0) == q.size(0) * (q.size(1) / 32) &&
+                    colsum->size(1) == 3 * q.size(2) * q.size(3),
+                "dlion attn: colsum must be fp32 [B * T / 32, 3 * H * D]");
+    a.colsum = colsum->data_ptr<float>();
+  }
   check_hip(dlion::launch_attn_bwd(a, static_cast<int>(q.size(3)), a.thresh16 > 0, cur_stream()), "attn_bwd");
 }
 
@@ -692,7 +702,7 @@ TORCH_LIBRARY(dlion, m) {
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float p, int seed) -> (Tensor, Tensor)");
   m.def(
       "attn_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout, Tensor lse, float p, int seed,"
-      " Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
+      " Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor(d!)? colsum=None) -> ()");
   m.def("softmax_xent_(Tensor(a!) logits, Tensor labels, int v, int variant=0) -> Tensor");
   m.def(
       "lion_local(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, float decay, float neg_lr,"

@@ -74,9 +74,8 @@ class Attention(nn.Module):
     def forward(self, x, proj_bias: bool = True):
         """proj_bias=False leaves c_proj's bias to the caller's fused
         residual+dropout+LayerNorm kernel (its gradient comes out of it too)."""
-        B, T, _ = x.shape
-        qkv = self.c_attn(x).view(B, T, 3, self.n_head, self.head_dim)
-        y = fused.causal_attention(qkv, self.attn_pdrop if self.training else 0.0)  # [B, T, C]
+        y = fused.qkv_attention(x, self.c_attn.weight, self.c_attn.bias, self.n_head,
+                                self.attn_pdrop if self.training else 0.0)  # [B, T, C]
         return self.c_proj(y) if proj_bias else linear_kn(y, self.c_proj.weight, None)
 
 

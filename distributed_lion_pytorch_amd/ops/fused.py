@@ -596,6 +596,78 @@ def causal_attention(qkv: torch.Tensor, dropout_p: float) -> torch.Tensor:
     return y.transpose(1, 2).reshape(B, T, H * D)
 
 
+class _QKVAttention(torch.autograd.Function):
+    """y = causal_attention(x @ Wqkv + b) for GPT-2's packed c_attn projection
+    (Wqkv in HF Conv1D [C, 3C] layout).  One op so that the backward can take
+    the c_attn bias gradient from the attention kernels themselves: the dQ /
+    dKV kernels emit per-32-row column sums of the dq | dk | dv values they
+    store (csrc/attention.hip), replacing a column-sum pass over the [tokens,
+    3C] gradient."""
+
+    @staticmethod
+    def forward(ctx, x2d, w, b, B, T, H, p, seed):
+        from .linear import _fuse_target, transposed_weight
+
+        C3 = w.shape[1]
+        D = C3 // (3 * H)
+        wt = transposed_weight(w) if isinstance(w, torch.nn.Parameter) else w.t()
+        qkv = F.linear(x2d, wt, b).view(B, T, 3, H, D)
+        out, lse = hip.ops().attn_fwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], p, seed)
+        ctx.save_for_backward(x2d, w, qkv, out, lse)
+        ctx.p, ctx.seed = p, seed
+        ctx.fuse = _fuse_target(w)
+        ctx.fused_b = _fused_params(b)[0]
+        return out.view(B, T, H * D)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .linear import deposit_grad, wgrad, wgrad_into
+
+        x2d, w, qkv, out, lse = ctx.saved_tensors
+        B, T = qkv.shape[:2]
+        dout = dy.reshape(out.shape).contiguous()
+        dqkv = torch.empty_like(qkv)
+        part = torch.empty(B * (T // 32), w.shape[1], dtype=torch.float32, device=qkv.device)
+        hip.ops().attn_bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], out, dout, lse, ctx.p, ctx.seed,
+                           dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], part)
+        g = dqkv.view(B * T, -1)
+        dx = g @ w.t() if ctx.needs_input_grad[0] else None
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            if ctx.fuse:
+                wgrad_into(x2d, g, w)
+            else:
+                dw = wgrad(x2d, g)
+        if ctx.needs_input_grad[2]:
+            if ctx.fused_b is not None:
+                deposit_grad(ctx.fused_b, part)
+            else:
+                db = _sum_rows(part)
+        return dx, dw, db, None, None, None, None, None
+
+
+_QKV_FUSED = os.environ.get("DLION_QKV_FUSED", "1") != "0"  # A/B switch for _QKVAttention
+
+
+def qkv_attention(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, n_head: int, dropout_p: float) -> torch.Tensor:
+    """GPT-2 attention core: causal_attention((x @ Wqkv + b).view(B, T, 3, H, D))
+    -> [B, T, C], as one op on the GPU path (see _QKVAttention)."""
+    from .linear import autocast_inputs, linear_kn
+
+    B, T, C = x.shape
+    D = w.shape[1] // (3 * n_head)
+    if x.is_cuda:
+        x, w, b = autocast_inputs(x, w, b)
+    if (_QKV_FUSED and b is not None and x.is_cuda and x.dtype == w.dtype == b.dtype == torch.bfloat16
+            and _attn_ok(x, T, D)
+            and w.is_contiguous() and b.is_contiguous()):
+        with torch.autocast("cuda", enabled=False):
+            return _QKVAttention.apply(x.reshape(B * T, C).contiguous(), w, b, B, T, n_head, float(dropout_p),
+                                       _new_seed())
+    qkv = linear_kn(x, w, b).view(B, T, 3, n_head, D)
+    return causal_attention(qkv, dropout_p)
+
+
 def causal_attention_gqa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, dropout_p: float = 0.0) -> torch.Tensor:
     """q [B,T,H,D], k/v [B,T,Hkv,D] -> [B,T,H*D] (grouped-query causal attention)."""
     B, T, H, D = q.shape

@@ -65,3 +65,32 @@ def test_packed_qkv_attention_matches_reference(p, cuda):
     ref.backward(dout.float())
     _close(out, ref, 2e-2)
     _close(a.grad, r.grad, 3e-2)
+
+
+@pytest.mark.parametrize("fuse", [False, True])
+def test_qkv_attention_bias_grad_from_kernels(fuse, cuda):
+    """GPT-2 c_attn projection + attention as one op: the c_attn bias gradient
+    comes from the dQ/dKV kernels' column partials; all gradients vs fp32."""
+    from distributed_lion_pytorch_amd.ops import fused
+    from distributed_lion_pytorch_amd.ops.linear import grad_accumulation_fusion
+
+    hip.require()
+    torch.manual_seed(5)
+    B, T, H, D = 2, 128, 4, 64
+    C = H * D
+    x = torch.randn(B, T, C, device=cuda).bfloat16().requires_grad_(True)
+    w = torch.nn.Parameter((torch.randn(C, 3 * C, device=cuda) / C ** 0.5).bfloat16())
+    b = torch.nn.Parameter((0.1 * torch.randn(3 * C, device=cuda)).bfloat16())
+    dy = torch.randn(B, T, C, device=cuda).bfloat16()
+    with grad_accumulation_fusion(fuse):
+        y = fused.qkv_attention(x, w, b, H, 0.0)
+        y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    qkv = (xr @ wr + br).view(B, T, 3, H, D).permute(2, 0, 3, 1, 4)
+    yr = torch.nn.functional.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], is_causal=True)
+    yr = yr.transpose(1, 2).reshape(B, T, C)
+    yr.backward(dy.float())
+    rel = lambda a, r: ((a.float() - r).abs().max() / (r.abs().max() + 1e-6)).item()  # noqa: E731
+    assert rel(y, yr) < 2e-2
+    for got, ref in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert rel(got, ref) < 3e-2, rel(got, ref)
