@@ -216,8 +216,7 @@ class GPT2LMHeadModel(PreTrainedModel):
             # shift inside the fused LM-head + cross-entropy (HF semantics:
             # position t predicts label t+1, ignore_index -100).  With
             # num_items_in_batch the sum is normalised by it (HF GA-aware loss).
-            loss = fused.lm_head_cross_entropy(h[:, :-1], self.lm_head.weight, labels[:, 1:],
-                                               normalizer=num_items_in_batch)
+            loss = fused.causal_lm_loss(h, self.lm_head.weight, labels, normalizer=num_items_in_batch)
             if not self.training:
                 logits = F.linear(h, self.lm_head.weight)
         else:
@@ -226,8 +225,8 @@ class GPT2LMHeadModel(PreTrainedModel):
 
     def sequence_logps(self, input_ids: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         """Sum of log p(label_t | <t) per sequence (DPO); labels -100 ignored."""
-        h = self.transformer(input_ids)[:, :-1]
-        return fused.token_logps(h, self.lm_head.weight, labels[:, 1:]).sum(-1)
+        h = self.transformer(input_ids)
+        return fused.token_logps(h, self.lm_head.weight, fused.shift_labels(labels)).sum(-1)
 
     def flops_per_token(self, seq_len: int) -> float:
         """Training FLOPs per token (6N + attention), for MFU reporting."""

@@ -253,8 +253,7 @@ class LlamaForCausalLM(PreTrainedModel):
         h = self.model(input_ids)
         loss = logits = None
         if labels is not None:
-            loss = fused.lm_head_cross_entropy(h[:, :-1], self.lm_head.weight, labels[:, 1:],
-                                               normalizer=num_items_in_batch)
+            loss = fused.causal_lm_loss(h, self.lm_head.weight, labels, normalizer=num_items_in_batch)
             if not self.training:
                 logits = F.linear(h, self.lm_head.weight)
         else:
@@ -275,6 +274,6 @@ def sequence_logps(model, input_ids: torch.Tensor, labels: torch.Tensor) -> torc
     """Per-sequence summed token log-probabilities under ``model`` (any of our
     causal LMs): used by the DPO loss (policy and frozen reference)."""
     base = model.model if hasattr(model, "model") and isinstance(model.model, LlamaModel) else model.transformer
-    h = base(input_ids)[:, :-1]
-    # fused LM head + log-softmax gather (no fp32 [B, T, V] logits)
-    return fused.token_logps(h, model.lm_head.weight, labels[:, 1:]).sum(-1)
+    h = base(input_ids)
+    # fused LM head + log-softmax gather (no fp32 [B, T, V] logits), labels shifted in place of h
+    return fused.token_logps(h, model.lm_head.weight, fused.shift_labels(labels)).sum(-1)

@@ -910,6 +910,27 @@ def lm_head_cross_entropy(h: torch.Tensor, weight: torch.Tensor, labels: torch.T
     return _LMHeadCE.apply(h2d, weight, labels.reshape(-1), normalizer)
 
 
+def shift_labels(labels: torch.Tensor) -> torch.Tensor:
+    """HF causal-LM label shift without slicing the hidden states: position t
+    is scored against labels[t + 1]; the last position gets -100 (ignored).
+    The LM head then runs on the whole [B, T] hidden-state block in place --
+    no [B, T-1] copy of h forward, no scatter of its gradient backward, and
+    M = B * T keeps the GEMMs tile-aligned."""
+    out = torch.full_like(labels, -100)
+    out[..., :-1] = labels[..., 1:]
+    return out
+
+
+_SHIFT_LABELS = os.environ.get("DLION_SHIFT_LABELS", "1") != "0"  # A/B switch: shift labels, not h
+
+
+def causal_lm_loss(h: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor, normalizer=None) -> torch.Tensor:
+    """Shifted next-token cross-entropy of the LM head on h [B, T, C]."""
+    if not _SHIFT_LABELS:
+        return lm_head_cross_entropy(h[:, :-1], weight, labels[:, 1:], normalizer=normalizer)
+    return lm_head_cross_entropy(h, weight, shift_labels(labels), normalizer=normalizer)
+
+
 def reference_lm_loss(h, weight, labels):
     """Unfused reference (HF semantics) used by tests."""
     logits = (h.reshape(-1, h.shape[-1]) @ weight.t()).float()
