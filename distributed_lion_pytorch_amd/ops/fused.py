@@ -196,12 +196,27 @@ def _param_grads(part2d, C, fused, present):
         for i in need:
             out[i] = _sum_rows(part2d[:, i * C:(i + 1) * C])
     dep = [i for i in range(3) if present[i] and fused[i] is not None]
-    if len(dep) > 1 and _JOINT and dep == list(range(dep[0], dep[0] + len(dep))) and _deposit_joint(
-            [fused[i] for i in dep], part2d[:, dep[0] * C:(dep[-1] + 1) * C], C):
-        return tuple(out)
+    if len(dep) > 1 and _JOINT and dep == list(range(dep[0], dep[0] + len(dep))):
+        from .linear import defer_partials
+
+        params = [fused[i] for i in dep]
+        sub = part2d[:, dep[0] * C:(dep[-1] + 1) * C]
+        if defer_partials(("joint",) + tuple(id(p) for p in params), sub,
+                          lambda pc: _deposit_joint_or_each(params, pc, C)):
+            return tuple(out)
+        if _deposit_joint(params, sub, C):
+            return tuple(out)
     for i in dep:
         deposit_grad(fused[i], part2d[:, i * C:(i + 1) * C])
     return tuple(out)
+
+
+def _deposit_joint_or_each(params, part2d, C) -> None:
+    from .linear import deposit_grad
+
+    if not _deposit_joint(params, part2d, C):
+        for j, p in enumerate(params):
+            deposit_grad(p, part2d[:, j * C:(j + 1) * C], defer=False)
 
 
 def _deposit_joint(params, part2d, C) -> bool:
