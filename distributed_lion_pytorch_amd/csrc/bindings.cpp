@@ -504,6 +504,25 @@ Tensor rope(const Tensor& x, const Tensor& cos, const Tensor& sin, bool inverse)
   return y;
 }
 
+// in place on x (same layout rules as rope): each lane reads its rotate-half
+// pair before writing it, so x may be a strided slice of a packed gradient
+void rope_(const Tensor& x, const Tensor& cos, const Tensor& sin, bool inverse) {
+  TORCH_CHECK(x.dim() == 4 && x.is_cuda() && x.scalar_type() == at::kBFloat16, "dlion rope_: x must be bf16 [B, T, H, D]");
+  const int64_t B = x.size(0), T = x.size(1), H = x.size(2), D = x.size(3);
+  TORCH_CHECK(x.stride(3) == 1 && x.stride(2) == D && (B == 1 || x.stride(0) == T * x.stride(1)) &&
+                  x.stride(1) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && D % 8 == 0,
+              "dlion rope_: x must have contiguous heads and a uniform, 16-byte aligned token stride");
+  for (const Tensor* t : {&cos, &sin})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->dim() == 2 &&
+                    t->size(0) >= T && t->size(1) == D,
+                "dlion rope_: cos/sin must be contiguous bf16 [>=T, D]");
+  const c10::DeviceGuard dg(x.device());
+  check_hip(dlion::launch_rope(x.data_ptr(), cos.data_ptr(), sin.data_ptr(), x.data_ptr(), B * T,
+                               static_cast<int>(T), static_cast<int>(H), static_cast<int>(D), inverse, x.stride(1),
+                               x.stride(1), cur_stream()),
+            "rope_");
+}
+
 // ---------------------------------------------------------------- GEMM (NT)
 // a [M, K], b [N, K] (rows may be strided, unit column stride) -> c [M, N] bf16
 void check_gemm_operand(const Tensor& t, const char* name) {
@@ -688,6 +707,7 @@ TORCH_LIBRARY(dlion, m) {
   m.def("swiglu_bwd(Tensor dh, Tensor g, Tensor u) -> (Tensor, Tensor)");
   m.def("swiglu_bwd_fused(Tensor dh, Tensor g, Tensor u) -> Tensor");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, bool inverse) -> Tensor");
+  m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, bool inverse) -> ()");
   m.def(
       "add_norm_fwd(Tensor x, Tensor? y, Tensor? bias, Tensor gamma, Tensor? beta, float eps, bool rms, float p,"
       " int seed) -> (Tensor, Tensor, Tensor, Tensor)");
@@ -742,6 +762,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("swiglu_bwd_fused", &swiglu_bwd_fused);
   m.impl("rope", &rope);
+  m.impl("rope_", &rope_);
   m.impl("gemm_nt", &gemm_nt);
   m.impl("gemm_nt_out", &gemm_nt_out);
   m.impl("gemm_nt_gelu", &gemm_nt_gelu);

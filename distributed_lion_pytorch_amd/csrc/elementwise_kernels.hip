@@ -209,8 +209,10 @@ __device__ __forceinline__ void store4(uint16_t* p, const float (&o)[4]) {
 // ATen's slice / neg / cat / 2 mul / add chain.  inverse = the transpose
 // rotation (the backward).  Thread = 4 consecutive dims of the first half and
 // their partners in the second half.
-__global__ void __launch_bounds__(256) rope_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ cs,
-                                                  const uint16_t* __restrict__ sn, uint16_t* __restrict__ y,
+// x and y may be the same buffer (rope_ in place): each thread reads its
+// rotate-half pair before writing it, so x / y are not __restrict__
+__global__ void __launch_bounds__(256) rope_kernel(const uint16_t* x, const uint16_t* __restrict__ cs,
+                                                  const uint16_t* __restrict__ sn, uint16_t* y,
                                                   int64_t rows, int T, int H, int D, bool inverse, int64_t x_ld,
                                                   int64_t y_ld) {
   const int hd = D / 2, q = hd / 4;  // quads per half

@@ -110,8 +110,7 @@ class LlamaAttention(nn.Module):
         q = q.view(B, T, self.n_head, self.head_dim)
         k = k.view(B, T, self.n_kv, self.head_dim)
         v = v.view(B, T, self.n_kv, self.head_dim)
-        q, k = apply_rope(q, cos, sin), apply_rope(k, cos, sin)
-        y = fused.causal_attention_gqa(q, k, v, self.attn_dropout if self.training else 0.0)
+        y = fused.rope_attention(q, k, v, cos, sin, self.attn_dropout if self.training else 0.0)
         return _lin(self.o_proj, y)
 
 

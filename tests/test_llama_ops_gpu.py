@@ -153,3 +153,40 @@ def test_linear_multi_matches_separate(fuse, cuda):
     for w, r in zip(ws, refs):
         err = (w.grad.float() - r.grad).abs().max().item() / r.grad.abs().max().item()
         assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("H,Hkv", [(4, 4), (8, 2)])
+def test_rope_attention_packed_grads(H, Hkv, cuda):
+    """Fused RoPE + GQA attention on column views of a fused q|k|v output: the
+    values and gradients match rope_reference + SDPA in fp32, and the three
+    gradients come back as adjacent column blocks of one buffer (the fused
+    projection's backward then needs no concatenation)."""
+    from distributed_lion_pytorch_amd.ops import fused
+    from distributed_lion_pytorch_amd.ops.linear import _adjacent_views
+
+    hip.require()
+    torch.manual_seed(H)
+    B, T, D = 2, 128, 128
+    W = (H + 2 * Hkv) * D
+    qkv = torch.randn(B, T, W, device=cuda).bfloat16().requires_grad_(True)
+    q = qkv[..., :H * D].view(B, T, H, D)
+    k = qkv[..., H * D:(H + Hkv) * D].view(B, T, Hkv, D)
+    v = qkv[..., (H + Hkv) * D:].view(B, T, Hkv, D)
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
+    f = torch.outer(torch.arange(T, device=cuda).float(), inv)
+    emb = torch.cat([f, f], -1)
+    cos, sin = emb.cos().bfloat16(), emb.sin().bfloat16()
+    y = fused.rope_attention(q, k, v, cos, sin)
+    dy = torch.randn_like(y)
+    gq, gk, gv = torch.autograd.grad(y, (q, k, v), dy)
+    assert _adjacent_views([g.reshape(B, T, -1) for g in (gq, gk, gv)]) is not None
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    qh = fused.rope_reference(qr, cos.float(), sin.float()).transpose(1, 2)
+    kh = fused.rope_reference(kr, cos.float(), sin.float()).transpose(1, 2).repeat_interleave(H // Hkv, 1)
+    vh = vr.transpose(1, 2).repeat_interleave(H // Hkv, 1)
+    yr = torch.nn.functional.scaled_dot_product_attention(qh, kh, vh, is_causal=True).transpose(1, 2).reshape(B, T, -1)
+    rq, rk, rv = torch.autograd.grad(yr, (qr, kr, vr), dy.float())
+    rel = lambda a, r: ((a.float() - r).abs().max() / (r.abs().max() + 1e-6)).item()  # noqa: E731
+    assert rel(y, yr) < 2e-2
+    for got, ref in ((gq, rq), (gk, rk), (gv, rv)):
+        assert rel(got, ref) < 3e-2, rel(got, ref)
