@@ -680,6 +680,27 @@ void scale_acc_(const Tensor& x, const Tensor& s, const Tensor& y, bool accumula
             "scale_acc");
 }
 
+// diagnostic: c = a . b^T with per-block timestamps stamps [blocks, 8] int64
+Tensor gemm_nt_stamped(const Tensor& a, const Tensor& b, const Tensor& stamps) {
+  check_gemm_operand(a, "a");
+  check_gemm_operand(b, "b");
+  TORCH_CHECK(gemm_nt_supported(a, b), "dlion gemm: unsupported shape");
+  const int64_t blocks = ((a.size(0) + 255) / 256) * ((b.size(0) + 255) / 256);
+  TORCH_CHECK(stamps.is_cuda() && stamps.scalar_type() == at::kLong && stamps.is_contiguous() &&
+                  stamps.numel() >= blocks * 8,
+              "dlion gemm: stamps must be int64 [blocks, 8]");
+  auto c = at::empty({a.size(0), b.size(0)}, a.options());
+  const c10::DeviceGuard g(a.device());
+  check_hip(dlion::launch_gemm_nt_stamped(a.data_ptr(), static_cast<int>(a.stride(0)), b.data_ptr(),
+                                          static_cast<int>(b.stride(0)), c.data_ptr(), static_cast<int>(c.stride(0)),
+                                          static_cast<int>(a.size(0)), static_cast<int>(b.size(0)),
+                                          static_cast<int>(a.size(1)),
+                                          reinterpret_cast<unsigned long long*>(stamps.data_ptr<int64_t>()),
+                                          cur_stream()),
+            "gemm_nt_stamped");
+  return c;
+}
+
 // dz = (a . b^T) * gelu'(z + bias) -> (dz [M, N] bf16, part [2 * ceil(M/256), N] fp32 bias-grad partials):
 // the MLP down-projection's input gradient fused with the bias+GELU backward
 std::tuple<Tensor, Tensor> gemm_nt_dgelu(const Tensor& a, const Tensor& b, const Tensor& bias, const Tensor& z,
@@ -694,6 +715,7 @@ std::tuple<Tensor, Tensor> gemm_nt_dgelu(const Tensor& a, const Tensor& b, const
 
 TORCH_LIBRARY(dlion, m) {
   m.def("gemm_nt_dgelu(Tensor a, Tensor b, Tensor bias, Tensor z, bool exact) -> (Tensor, Tensor)");
+  m.def("gemm_nt_stamped(Tensor a, Tensor b, Tensor(a!) stamps) -> Tensor");
   m.def("embed_fwd(Tensor ids, Tensor wte, Tensor wpe, float p, int seed) -> Tensor");
   m.def(
       "embed_bwd_(Tensor dx, Tensor? sid, Tensor? perm, Tensor(a!)? dwte, Tensor(b!)? dwpe, int T, bool pos_accumulate,"
@@ -767,6 +789,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("gemm_nt_out", &gemm_nt_out);
   m.impl("gemm_nt_gelu", &gemm_nt_gelu);
   m.impl("gemm_nt_dgelu", &gemm_nt_dgelu);
+  m.impl("gemm_nt_stamped", &gemm_nt_stamped);
   m.impl("embed_fwd", &embed_fwd);
   m.impl("embed_bwd_", &embed_bwd_);
   m.impl("scale_acc_", &scale_acc_);

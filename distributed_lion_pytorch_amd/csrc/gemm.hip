@@ -62,6 +62,7 @@ struct GemmArgs {
   const uint16_t* bias;
   uint16_t* aux;
   float* part;  // EPI 4/5: [2 * tiles_m][N] fp32 column partial sums of C
+  unsigned long long* stamps;  // diagnostic build only (STAMP): [blocks][8] timestamps
   int lda, ldb, ldc, ldaux;
   int M, N, K;
   int tiles_m, tiles_n;
@@ -90,8 +91,26 @@ struct Stage {
   int off[2][2][2];  // [ab][half][piece]
 };
 
-template <int EPI>
+// Diagnostic stamps (STAMP builds only, tools/gemm_stamps.py): s_memtime at
+// fixed points plus s_memrealtime at entry / exit, written by vector stores.
+#define DLION_STAMP(dst)                                                            \
+  if constexpr (STAMP) {                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(dst) :: "memory");    \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+  }
+#define DLION_RSTAMP(dst)                                                           \
+  if constexpr (STAMP) {                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(dst) :: "memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+  }
+
+template <int EPI, bool STAMP = false>
 __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
+  unsigned long long st_[7] = {0, 0, 0, 0, 0, 0, 0};
+  DLION_RSTAMP(st_[5])
+  DLION_STAMP(st_[0])
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
 
   const int tid = threadIdx.x;
@@ -189,7 +208,7 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
     _Pragma("unroll") for (int mt = 0; mt < 2; ++mt)                             \
     _Pragma("unroll") for (int nt = 0; nt < 4; ++nt)                             \
     _Pragma("unroll") for (int s = 0; s < 2; ++s)                                \
-      acc[2 * (P) + mt][nt] = mfma16(afr[mt][s], bfr[nt][s], acc[2 * (P) + mt][nt]); \
+      acc[2 * (P) + mt][nt] = mfma16(bfr[nt][s], afr[mt][s], acc[2 * (P) + mt][nt]); \
     __builtin_amdgcn_s_setprio(0);                                               \
   } while (0)
 
@@ -220,6 +239,7 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
   // retiring wait by >= 1 phase and a restage follows the last read by >= 2
   // phases in both group orders (re-derived with the half-phase offset).
   if (wr == 1) __builtin_amdgcn_s_barrier();
+  DLION_STAMP(st_[1])
 
   for (int it = 0; it < nit; ++it) {
     const int kt = 2 * it;
@@ -276,34 +296,42 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
 #undef DLION_GEMM_PHASE_MATH
 #undef DLION_GEMM_MFMA
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups: every MFMA and LDS read is done
+  DLION_STAMP(st_[2])
 
-  // ---- epilogue.  acc[mt][nt][j] = C[wr*128 + 16mt + 4(lane>>4) + j][wc*64 + 16nt + (lane&15)]
+  // ---- epilogue.  The MFMA operands are swapped (B fragment first), so each
+  // 16x16 accumulator block is transposed: acc[mt][nt][j] =
+  // C[wr*128 + 16mt + (lane&15)][wc*64 + 16nt + 4(lane>>4) + j] -- a lane owns
+  // 4 consecutive columns of one row, parked with one 8-byte LDS write instead
+  // of four 2-byte ones (32 instead of 128 park writes per lane).
   uint8_t* reg = lds + w * (128 * 128);
-  const int col_l = lane & 15;
-  float bv[4] = {0.f, 0.f, 0.f, 0.f};
+  float bv[4][4] = {};
   if constexpr (EPI == 1) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int n = n0 + wc * 64 + nt * 16 + col_l;
-      bv[nt] = n < g.N ? bf16_to_f32(g.bias[n]) : 0.f;
-    }
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wc * 64 + nt * 16 + 4 * (lane >> 4) + j;
+        bv[nt][j] = n < g.N ? bf16_to_f32(g.bias[n]) : 0.f;
+      }
   }
   const int row_base = m0 + wr * 128;
   const int col_base = n0 + wc * 64;
 
-  // park one bf16 value per (mt, nt, j) at [row][col] with 16-byte chunk ^= row & 7
+  // park 4 bf16 per (mt, nt) at [row][col..col+3] with 16-byte chunk ^= row & 7
   auto park = [&](auto fn) {
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int row = mt * 16 + (lane >> 4) * 4 + j;
-          const int col = nt * 16 + col_l;
-          const int chunk = (col >> 3) ^ (row & 7);
-          *reinterpret_cast<uint16_t*>(reg + row * 128 + chunk * 16 + (col & 7) * 2) = fn(acc[mt][nt][j], nt);
-        }
+      for (int nt = 0; nt < 4; ++nt) {
+        const int row = mt * 16 + (lane & 15);
+        const int col = nt * 16 + 4 * (lane >> 4);
+        const int chunk = (col >> 3) ^ (row & 7);
+        const uint32_t lo = static_cast<uint32_t>(fn(acc[mt][nt][0], nt, 0)) |
+                            (static_cast<uint32_t>(fn(acc[mt][nt][1], nt, 1)) << 16);
+        const uint32_t hi = static_cast<uint32_t>(fn(acc[mt][nt][2], nt, 2)) |
+                            (static_cast<uint32_t>(fn(acc[mt][nt][3], nt, 3)) << 16);
+        *reinterpret_cast<uint2*>(reg + row * 128 + chunk * 16 + (col & 7) * 2) = make_uint2(lo, hi);
+      }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
   };
@@ -311,7 +339,8 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
   const int gn = col_base + ch * 8;
 
   if constexpr (EPI <= 1) {
-    park([&](float v, int nt) { return f32_to_bf16(v + bv[nt]); });
+    park([&](float v, int nt, int j) { return f32_to_bf16(v + bv[nt][j]); });
+    DLION_STAMP(st_[3])
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int row = i * 8 + (lane >> 3);
@@ -319,11 +348,17 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
       const int gm = row_base + row;
       if (gm < g.M && gn < g.N) *reinterpret_cast<uint4*>(g.C + (int64_t)gm * g.ldc + gn) = v;
     }
+    if constexpr (STAMP) {
+      DLION_STAMP(st_[4])
+      DLION_RSTAMP(st_[6])
+      // per-lane value -> a vector store; lane i of wave 0 writes stamp i
+      if (tid < 8) g.stamps[static_cast<int64_t>(blockIdx.x) * 8 + tid] = tid < 7 ? st_[tid < 7 ? tid : 0] : 0ull;
+    }
   } else if constexpr (EPI <= 3) {
     // EPI 2/3: aux = z (bf16, no bias); C = gelu(z + b) evaluated on the ROUNDED z
     // exactly like the unfused GEMM -> bias_gelu path (3: erf GELU).  The GELU
     // runs in the drain, 8 columns per lane (one bias chunk per lane).
-    park([&](float v, int) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(v)); });
+    park([&](float v, int, int) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(v)); });
     float b8[8];
     if (gn < g.N) {
       Elem<kBF16>::load8(g.bias + gn, b8);
@@ -363,7 +398,7 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
       const int gm = min(row_base + i * 8 + (lane >> 3), g.M - 1);
       zr[i] = gn < g.N ? *reinterpret_cast<const uint4*>(g.aux + (int64_t)gm * g.ldaux + gn) : make_uint4(0, 0, 0, 0);
     }
-    park([&](float v, int) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(v)); });
+    park([&](float v, int, int) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(v)); });
     float b8[8], cs[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) cs[j] = 0.f;
@@ -408,6 +443,27 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
 }
 
 }  // namespace
+
+// diagnostic: plain GEMM (EPI 0) with per-block timestamps into stamps[grid][8]
+hipError_t launch_gemm_nt_stamped(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
+                                  unsigned long long* stamps, hipStream_t st) {
+  if (K % 128 != 0 || N % 8 != 0) return hipErrorInvalidValue;
+  GemmArgs g{};
+  g.A = static_cast<const uint16_t*>(A);
+  g.B = static_cast<const uint16_t*>(B);
+  g.C = static_cast<uint16_t*>(C);
+  g.lda = lda;
+  g.ldb = ldb;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.tiles_m = (M + kBM - 1) / kBM;
+  g.tiles_n = (N + kBN - 1) / kBN;
+  g.stamps = stamps;
+  hipLaunchKernelGGL((gemm_nt_kernel<0, true>), dim3(g.tiles_m * g.tiles_n), dim3(512), 0, st, g);
+  return hipGetLastError();
+}
 
 hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
                           void* aux, int ldaux, int M, int N, int K, int epi, float* part, hipStream_t st) {

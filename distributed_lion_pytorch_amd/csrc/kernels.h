@@ -72,6 +72,10 @@ hipError_t launch_embed_bwd(const void* dx, const int64_t* sid, const int64_t* p
 // y (+)= bf16(x * bf16(s[0])), s a device fp32 scalar
 hipError_t launch_scale_acc(const void* x, const float* s, void* y, int64_t n, int accumulate, hipStream_t st);
 
+// diagnostic build of the plain GEMM with per-block timestamps (tools/gemm_stamps.py)
+hipError_t launch_gemm_nt_stamped(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
+                                  unsigned long long* stamps, hipStream_t st);
+
 // ---- LM head cross-entropy (xent_kernels.hip)
 // variant 0 = auto (DLION_XENT env override), 1 fp32-row, 2 streaming, 3/4/5 packed 16-bit row (256/512/1024 thr)
 hipError_t launch_softmax_xent(int dt, void* logits, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,
