@@ -339,7 +339,7 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
   const int gn = col_base + ch * 8;
 
   if constexpr (EPI <= 1) {
-    park([&](float v, int nt, int j) { return f32_to_bf16(v + bv[nt][j]); });
+    park([&](float v, int nt, int j) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(v + bv[nt][j])); });
     DLION_STAMP(st_[3])
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
