@@ -711,9 +711,81 @@ std::tuple<Tensor, Tensor> gemm_nt_dgelu(const Tensor& a, const Tensor& b, const
   return {dz, part};
 }
 
+// ------------------------------------------------------------- LoRA
+void check_lora_rows(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2 && t.stride(1) == 1 &&
+                  t.stride(0) % 8 == 0 && t.size(1) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              "dlion lora: ", name, " must be a 2-D bf16 GPU tensor, unit column stride, row stride and width % 8 == 0");
+}
+
+// u [M, r] = scale * drop(x) . w^T, w [r, K]
+Tensor lora_rows(const Tensor& x, const Tensor& w, double scale, double p, int64_t seed) {
+  check_lora_rows(x, "x");
+  check_bf16_contig(w, "w");
+  const int64_t r = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == x.size(1) && (r == 8 || r == 16) && x.size(1) % 32 == 0,
+              "dlion lora: w must be [8|16, K] with K % 32 == 0");
+  const c10::DeviceGuard g(x.device());
+  auto u = at::empty({x.size(0), r}, x.options());
+  const auto dp = drop_params(p);
+  check_hip(dlion::launch_lora_rows(x.data_ptr(), x.stride(0), w.data_ptr(), u.data_ptr(), x.size(0),
+                                    static_cast<int>(x.size(1)), static_cast<int>(r), static_cast<float>(scale),
+                                    static_cast<uint32_t>(seed), dp.first, dp.second, cur_stream()),
+            "lora_rows");
+  return u;
+}
+
+// out [M, N] = o + bf16(s * u . b^T)
+Tensor lora_up(const Tensor& o, const Tensor& u, const Tensor& b, double s) {
+  check_lora_rows(o, "o");
+  check_bf16_contig(u, "u");
+  check_bf16_contig(b, "b");
+  const int64_t r = u.size(1);
+  TORCH_CHECK(u.dim() == 2 && u.size(0) == o.size(0) && b.dim() == 2 && b.size(0) == o.size(1) && b.size(1) == r &&
+                  (r == 8 || r == 16),
+              "dlion lora: shape mismatch (u [M, r], b [N, r], r in {8, 16})");
+  const c10::DeviceGuard g(o.device());
+  auto out = at::empty({o.size(0), o.size(1)}, o.options());
+  check_hip(dlion::launch_lora_up(o.data_ptr(), o.stride(0), u.data_ptr(), b.data_ptr(), out.data_ptr(), o.size(0),
+                                  static_cast<int>(o.size(1)), static_cast<int>(r), static_cast<float>(s), cur_stream()),
+            "lora_up");
+  return out;
+}
+
+// no a: (part [P, N, r] = yscale * per-range g^T y, -);
+// a:    (part [P, r, N] = yscale * per-range y^T drop(g), dx = drop'(y . a))
+std::tuple<Tensor, Tensor> lora_cols(const Tensor& g, const Tensor& y, const std::optional<Tensor>& a, double yscale,
+                                     double p, int64_t seed) {
+  check_lora_rows(g, "g");
+  check_bf16_contig(y, "y");
+  const int64_t r = y.size(1), M = g.size(0), N = g.size(1);
+  TORCH_CHECK(y.dim() == 2 && y.size(0) == M && (r == 8 || r == 16), "dlion lora: y must be [M, 8|16]");
+  const bool mode1 = a.has_value();
+  if (mode1) {
+    check_bf16_contig(*a, "a");
+    TORCH_CHECK(a->dim() == 2 && a->size(0) == r && a->size(1) == N, "dlion lora: a must be [r, N]");
+  }
+  const c10::DeviceGuard dg(g.device());
+  const int parts = dlion::lora_cols_parts(M, static_cast<int>(N));
+  auto part = mode1 ? at::empty({parts, r, N}, g.options().dtype(at::kFloat))
+                    : at::empty({parts, N, r}, g.options().dtype(at::kFloat));
+  Tensor dx = mode1 ? at::empty({M, N}, g.options()) : Tensor();
+  const auto dp = drop_params(mode1 ? p : 0.0);
+  check_hip(dlion::launch_lora_cols(g.data_ptr(), g.stride(0), y.data_ptr(), mode1 ? a->data_ptr() : nullptr,
+                                    mode1 ? dx.data_ptr() : nullptr, part.data_ptr<float>(), M, static_cast<int>(N),
+                                    static_cast<int>(r), parts, mode1 ? 1 : 0, static_cast<float>(yscale),
+                                    static_cast<uint32_t>(seed), dp.first,
+                                    dp.second, cur_stream()),
+            "lora_cols");
+  return {part, dx};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dlion, m) {
+  m.def("lora_rows(Tensor x, Tensor w, float scale, float p, int seed) -> Tensor");
+  m.def("lora_up(Tensor o, Tensor u, Tensor b, float s) -> Tensor");
+  m.def("lora_cols(Tensor g, Tensor y, Tensor? a, float yscale, float p, int seed) -> (Tensor, Tensor)");
   m.def("gemm_nt_dgelu(Tensor a, Tensor b, Tensor bias, Tensor z, bool exact) -> (Tensor, Tensor)");
   m.def("gemm_nt_stamped(Tensor a, Tensor b, Tensor(a!) stamps) -> Tensor");
   m.def("embed_fwd(Tensor ids, Tensor wte, Tensor wpe, float p, int seed) -> Tensor");
@@ -794,4 +866,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("embed_bwd_", &embed_bwd_);
   m.impl("scale_acc_", &scale_acc_);
   m.impl("lt_gemm_nt", &lt_gemm_nt);
+  m.impl("lora_rows", &lora_rows);
+  m.impl("lora_up", &lora_up);
+  m.impl("lora_cols", &lora_cols);
 }

@@ -201,6 +201,11 @@ __device__ __forceinline__ uint32_t keep4(uint32_t seed, uint64_t idx, uint32_t 
   k |= ((h1 >> 16) >= thresh16) << 3;
   return k;
 }
+// keep bits for 8 consecutive elements (idx % 8 == 0); all kept when thresh16 == 0
+__device__ __forceinline__ uint32_t keep8(uint32_t seed, uint64_t idx, uint32_t thresh16) {
+  if (!thresh16) return 0xffu;
+  return keep4(seed, idx, thresh16) | (keep4(seed, idx + 4, thresh16) << 4);
+}
 
 // ------------------------------------------------------------- Philox4x32-10
 // Counter-based RNG for the stochastic-binarization encoder: every

@@ -24,11 +24,6 @@ __device__ __forceinline__ void drop8(float (&v)[8], uint32_t kp, float inv_keep
   for (int j = 0; j < 8; ++j) v[j] = ((kp >> j) & 1u) ? v[j] * inv_keep : 0.f;
 }
 
-__device__ __forceinline__ uint32_t keep8(uint32_t seed, uint64_t idx, uint32_t thresh16) {
-  if (!thresh16) return 0xffu;
-  return keep4(seed, idx, thresh16) | (keep4(seed, idx + 4, thresh16) << 4);
-}
-
 __global__ void __launch_bounds__(256) embed_fwd_kernel(const int64_t* __restrict__ ids, const uint16_t* __restrict__ wte,
                                                         const uint16_t* __restrict__ wpe, uint16_t* __restrict__ out,
                                                         int64_t n, int C, int T, int64_t V, uint32_t seed,

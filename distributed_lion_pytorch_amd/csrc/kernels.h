@@ -76,6 +76,21 @@ hipError_t launch_scale_acc(const void* x, const float* s, void* y, int64_t n, i
 hipError_t launch_gemm_nt_stamped(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
                                   unsigned long long* stamps, hipStream_t st);
 
+// ---- LoRA adapter streams (lora.hip), bf16, r in {8, 16}, widths % 8 == 0
+// out[t, :r] = scale * drop(in)[t, :] . w^T, w [r, K]; dropout when thresh16 > 0
+hipError_t launch_lora_rows(const void* in, int64_t ldin, const void* w, void* out, int64_t rows, int K, int r,
+                            float scale, uint32_t seed, uint32_t thresh16, float inv_keep, hipStream_t st);
+// out [rows, N] = o + bf16(s * u . b^T), u [rows, r], b [N, r]
+hipError_t launch_lora_up(const void* o, int64_t ldo, const void* u, const void* b, void* out, int64_t rows, int N, int r,
+                          float s, hipStream_t st);
+// part fp32 = yscale * per-row-range y^T g'; mode 0: g' = g, part [parts, N, r]; mode 1:
+// g' = drop(g), part [parts, r, N], also dx = drop'(y . a) with a [r, N]; lora_cols_parts picks
+// the range count
+int lora_cols_parts(int64_t rows, int N);
+hipError_t launch_lora_cols(const void* g, int64_t ldg, const void* y, const void* a, void* dx, float* part, int64_t rows,
+                            int N, int r, int parts, int mode, float yscale, uint32_t seed, uint32_t thresh16,
+                            float inv_keep, hipStream_t st);
+
 // ---- LM head cross-entropy (xent_kernels.hip)
 // variant 0 = auto (DLION_XENT env override), 1 fp32-row, 2 streaming, 3/4/5 packed 16-bit row (256/512/1024 thr)
 hipError_t launch_softmax_xent(int dt, void* logits, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,

@@ -140,8 +140,7 @@ def _proj(x, layers):
     if not x.is_cuda or len({w.dtype for w in bases}) != 1:
         return tuple(_lin(layer, x) for layer in layers)
     outs = linear_multi_nk(x, bases)
-    return tuple(layer.lora_delta(x) + o if isinstance(layer, LoraLinear) and not layer.merged else o
-                 for layer, o in zip(layers, outs))
+    return tuple(layer.add_adapter(x, o) if isinstance(layer, LoraLinear) else o for layer, o in zip(layers, outs))
 
 
 class LlamaMLP(nn.Module):

@@ -22,6 +22,7 @@ from typing import List, Optional
 import torch
 import torch.nn as nn
 
+from ..ops import fused
 from ..ops.linear import linear_nk
 
 
@@ -64,11 +65,16 @@ class LoraLinear(nn.Module):
         """The adapter path alone: dropout(x) A^T B^T * (alpha / r)."""
         return self.lora_B(self.lora_A(self.dropout(x))) * self.scaling
 
-    def forward(self, x):
-        y = linear_nk(x, self.base_layer.weight, self.base_layer.bias)
+    def add_adapter(self, x, y):
+        """y + lora_delta(x); on the GPU the fused csrc/lora.hip kernels
+        (ops/fused.lora_add), with the dropout mask drawn in-kernel."""
         if self.merged:
             return y
-        return y + self.lora_delta(x)
+        p = self.dropout.p if isinstance(self.dropout, nn.Dropout) and self.dropout.training else 0.0
+        return fused.lora_add(y, x, self.lora_A.weight, self.lora_B.weight, self.scaling, p)
+
+    def forward(self, x):
+        return self.add_adapter(x, linear_nk(x, self.base_layer.weight, self.base_layer.bias))
 
     @torch.no_grad()
     def merge(self):

@@ -264,8 +264,9 @@ class _AddNorm(torch.autograd.Function):
         parts = _norm_parts(rows, C)
         dx, dy, part = hip.ops().add_norm_bwd(dh.contiguous(), None if dxo is None else dxo.contiguous(), xo, gamma,
                                               mean, rstd, ctx.rms, ctx.p, ctx.seed, True, parts)
+        need = ctx.needs_input_grad
         dgamma, dbeta, dbias = _param_grads(part.view(-1, 3 * C), C, ctx.fused_params,
-                                            (True, ctx.has_beta, ctx.has_bias))
+                                            (need[3], ctx.has_beta and need[4], ctx.has_bias and need[2]))
         return dy, dx, dbias, dgamma, dbeta, None, None, None, None
 
 
@@ -285,7 +286,9 @@ class _Norm(torch.autograd.Function):
         parts = _norm_parts(x.numel() // C, C)
         dx, _, part = hip.ops().add_norm_bwd(dh.contiguous(), None, x, gamma, mean, rstd, ctx.rms, 0.0, 0, False,
                                              parts)
-        dgamma, dbeta, _ = _param_grads(part.view(-1, 3 * C), C, ctx.fused_params, (True, ctx.has_beta, False))
+        need = ctx.needs_input_grad
+        dgamma, dbeta, _ = _param_grads(part.view(-1, 3 * C), C, ctx.fused_params,
+                                        (need[1], ctx.has_beta and need[2], False))
         return dx, dgamma, dbeta, None, None
 
 
@@ -753,6 +756,85 @@ def rope_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cos: torch
             out = _RopeAttention.apply(q, k, v, cos.contiguous(), sin.contiguous(), float(dropout_p), _new_seed())
         return out.view(B, T, H * D)
     return causal_attention_gqa(rope(q, cos, sin), rope(k, cos, sin), v, dropout_p)
+
+
+# ------------------------------------------------------------------- LoRA
+def _lora_rows_ok(t: torch.Tensor) -> bool:
+    return (t.dim() == 2 and t.dtype == torch.bfloat16 and t.stride(1) == 1 and t.stride(0) % 8 == 0
+            and t.shape[1] % 8 == 0 and t.data_ptr() % 16 == 0)
+
+
+def _lora_weight_grad(param, part2d: torch.Tensor, fuse: bool):
+    """Deposit (fusion window) or return the column sums of fp32 partials."""
+    from .linear import deposit_grad
+
+    if fuse:
+        deposit_grad(param, part2d, defer=False)  # MB-sized stacks: nothing to gain from deferral
+        return None
+    return hip.ops().sum_partials(part2d).view_as(param)
+
+
+class _LoraAdd(torch.autograd.Function):
+    """out = o + s * (drop(x) A^T) B^T with the csrc/lora.hip streams: the
+    forward reads x once (dropout from the stateless hash, never stored) and
+    o once; the backward reads dout twice (du, dB) and x once (dA and dx in
+    the same pass).  o's gradient is dout itself, so a fused projection's
+    packed gradient buffer stays packed."""
+
+    @staticmethod
+    def forward(ctx, o, x, a, b, s, p, seed):
+        from .linear import _fuse_target
+
+        ops = hip.ops()
+        u = ops.lora_rows(x, a, 1.0, p, seed)
+        out = ops.lora_up(o, u, b, s)
+        ctx.save_for_backward(x, u, a, b)
+        ctx.s, ctx.p, ctx.seed = s, p, seed
+        ctx.fuse = (_fuse_target(a), _fuse_target(b))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, u, a, b = ctx.saved_tensors
+        if not _lora_rows_ok(dout):
+            dout = dout.contiguous()
+        ops = hip.ops()
+        ga = gb = dx = None
+        if ctx.needs_input_grad[3]:
+            part_b, _ = ops.lora_cols(dout, u, None, ctx.s, 0.0, 0)
+            gb = _lora_weight_grad(b, part_b.view(part_b.shape[0], -1), ctx.fuse[1])
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            du = ops.lora_rows(dout, b.t().contiguous(), ctx.s, 0.0, 0)
+            part_a, dx = ops.lora_cols(x, du, a, 1.0, ctx.p, ctx.seed)
+            if ctx.needs_input_grad[2]:
+                ga = _lora_weight_grad(a, part_a.view(part_a.shape[0], -1), ctx.fuse[0])
+        return dout if ctx.needs_input_grad[0] else None, dx, ga, gb, None, None, None
+
+
+_LORA_FUSED = os.environ.get("DLION_LORA_FUSED", "1") != "0"  # A/B switch for _LoraAdd
+
+
+def lora_add(o: torch.Tensor, x: torch.Tensor, a: torch.Tensor, b: torch.Tensor, scaling: float,
+             p: float) -> torch.Tensor:
+    """o + dropout(x, p) A^T B^T * scaling (peft's LoRA output, A [r, K],
+    B [N, r]); the fused HIP path for bf16 GPU tensors with r in {8, 16}."""
+    r = a.shape[0]
+    if _LORA_FUSED and x.is_cuda and r in (8, 16) and _use_hip(x):
+        from .linear import autocast_inputs
+
+        o_, x_, a_, b_ = autocast_inputs(o, x, a, b)
+        if x_.dtype == o_.dtype == a_.dtype == b_.dtype == torch.bfloat16 and a_.is_contiguous() and b_.is_contiguous():
+            x2 = x_.reshape(-1, x_.shape[-1])
+            o2 = o_.reshape(-1, o_.shape[-1])
+            if not _lora_rows_ok(x2):
+                x2 = x2.contiguous()
+            if (_lora_rows_ok(o2) and _lora_rows_ok(x2) and a_.shape[1] == x2.shape[1] and b_.shape[0] == o2.shape[1]
+                    and x2.shape[1] % 32 == 0 and o2.shape[1] % 32 == 0):
+                with torch.autocast("cuda", enabled=False):
+                    out = _LoraAdd.apply(o2, x2, a_, b_, float(scaling), float(p), _new_seed() if p > 0 else 0)
+                return out.view(o.shape)
+    xd = F.dropout(x, p, True) if p > 0 else x
+    return o + F.linear(F.linear(xd, a), b) * scaling
 
 
 _M32 = 0xFFFFFFFF

@@ -170,7 +170,7 @@ def _acc_gemm(params, cols, a3, b3) -> bool:
 
 
 def _fuse_target(w) -> bool:
-    return (_FUSE_ACCUM["on"] and isinstance(w, torch.nn.Parameter) and w.is_cuda
+    return (_FUSE_ACCUM["on"] and isinstance(w, torch.nn.Parameter) and w.requires_grad and w.is_cuda
             and w.dtype == torch.bfloat16 and w.is_contiguous())
 
 
@@ -331,7 +331,7 @@ def cached_derived(w: torch.Tensor, tag: str, fn) -> torch.Tensor:
     step).  Used for per-step weight layouts (transposed, vocab-padded)."""
     import weakref
 
-    key = (w._version, _WEIGHT_GEN[0], w.data_ptr())
+    key = (w._version, _WEIGHT_GEN[0] if w.requires_grad else -1, w.data_ptr())  # frozen: see cat_weights
     ck = (id(w), tag)
     hit = _WT_CACHE.get(ck)
     if hit is not None and hit[0]() is w and hit[1] == key:
@@ -419,7 +419,12 @@ def cat_weights(ws) -> torch.Tensor:
     if len(ws) == 1:
         return ws[0]
     ck = tuple(id(w) for w in ws)
-    key = (_WEIGHT_GEN[0],) + tuple((w._version, w.data_ptr()) for w in ws)
+    # the optimizer's kernels write trainable weights through raw pointers (no
+    # _version bump): those are re-concatenated after every step; frozen ones
+    # (LoRA base weights, a DPO reference model) stay cached -- the re-cat of a
+    # Llama-2-7B layer's q/k/v + gate/up weights was ~2.7 % of a LoRA SFT step
+    gen = _WEIGHT_GEN[0] if any(w.requires_grad for w in ws) else -1
+    key = (gen,) + tuple((w._version, w.data_ptr()) for w in ws)
     hit = _CAT_CACHE.get(ck)
     if hit is not None and all(r() is w for r, w in zip(hit[0], ws)) and hit[1] == key:
         return hit[2]
