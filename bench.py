@@ -240,7 +240,7 @@ def main():
     prof = None
     if args.profile_dir and rank == 0:
         prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
-                                                  torch.profiler.ProfilerActivity.CUDA])
+                                                  torch.profiler.ProfilerActivity.CUDA], record_shapes=True)
         prof.__enter__()
     with timer:
         for _ in range(args.steps):
@@ -251,6 +251,10 @@ def main():
         prof.export_chrome_trace(os.path.join(args.profile_dir, "trace.json"))
         with open(os.path.join(args.profile_dir, "top_kernels.txt"), "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40))
+        with open(os.path.join(args.profile_dir, "top_ops_by_shape.txt"), "w") as f:
+            f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=80,
+                                                                          max_name_column_width=40,
+                                                                          max_shapes_column_width=90))
     elapsed = torch.tensor([timer.elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)

@@ -10,6 +10,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "kernels.h"
 
 namespace dlion {
@@ -711,6 +713,52 @@ std::tuple<Tensor, Tensor> gemm_nt_dgelu(const Tensor& a, const Tensor& b, const
   return {dz, part};
 }
 
+// ------------------------------------------------------------- weight-gradient GEMM
+// out [splits, M, N] fp32: out[z] = sum over split z's rows of P^T Q, the rows running over the
+// concatenation of the segments P[i] [rows, M] / Q[i] [rows, N] (same shape and row stride each)
+void gemm_tn_check_launch(at::TensorList P, at::TensorList Q, int64_t splits, const Tensor& out, bool accumulate) {
+  TORCH_CHECK(!P.empty() && P.size() == Q.size() && P.size() <= 16, "dlion gemm_tn: 1..16 segment pairs");
+  const int64_t rows = P[0].size(0), M = P[0].size(1), N = Q[0].size(1);
+  const int64_t ldp = P[0].stride(0), ldq = Q[0].stride(0);
+  std::vector<const void*> pp, qq;
+  for (size_t i = 0; i < P.size(); ++i) {
+    for (const Tensor* t : {&P[i], &Q[i]}) {
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->stride(1) == 1 &&
+                      reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                  "dlion gemm_tn: operands must be 2-D bf16 GPU tensors with unit column stride, 16-byte aligned");
+    }
+    TORCH_CHECK(P[i].size(0) == rows && Q[i].size(0) == rows && P[i].size(1) == M && Q[i].size(1) == N &&
+                    P[i].stride(0) == ldp && Q[i].stride(0) == ldq,
+                "dlion gemm_tn: every segment must have the same shape and row stride");
+    pp.push_back(P[i].data_ptr());
+    qq.push_back(Q[i].data_ptr());
+  }
+  TORCH_CHECK(rows % 128 == 0 && M % 8 == 0 && N % 8 == 0 && ldp % 8 == 0 && ldq % 8 == 0,
+              "dlion gemm_tn: rows % 128, M % 8, N % 8 and row strides % 8 must be 0");
+  TORCH_CHECK(splits >= 1 && splits <= static_cast<int64_t>(P.size()) * rows / 128, "dlion gemm_tn: bad split count");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.dim() == 3 &&
+                  out.size(0) == splits && out.size(1) == M && out.size(2) == N,
+              "dlion gemm_tn: out must be a contiguous fp32 [splits, M, N] tensor");
+  const c10::DeviceGuard g(P[0].device());
+  check_hip(dlion::launch_gemm_tn(pp.data(), qq.data(), static_cast<int>(P.size()), rows, static_cast<int>(ldp),
+                                  static_cast<int>(ldq), out.data_ptr<float>(), static_cast<int>(M),
+                                  static_cast<int>(N), static_cast<int>(splits), accumulate, cur_stream()),
+            "gemm_tn");
+}
+
+Tensor gemm_tn(at::TensorList P, at::TensorList Q, int64_t splits) {
+  TORCH_CHECK(!P.empty() && !Q.empty(), "dlion gemm_tn: no operands");
+  auto out = at::empty({splits, P[0].size(1), Q[0].size(1)}, P[0].options().dtype(at::kFloat));
+  gemm_tn_check_launch(P, Q, splits, out, false);
+  return out;
+}
+
+// out[z] (+)= the split-z partial of P^T Q (out: the fp32 [splits, M, N] accumulator)
+void gemm_tn_(at::TensorList P, at::TensorList Q, const Tensor& out, bool accumulate) {
+  TORCH_CHECK(out.dim() == 3, "dlion gemm_tn_: out must be [splits, M, N]");
+  gemm_tn_check_launch(P, Q, out.size(0), out, accumulate);
+}
+
 // ------------------------------------------------------------- LoRA
 void check_lora_rows(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2 && t.stride(1) == 1 &&
@@ -783,6 +831,8 @@ std::tuple<Tensor, Tensor> lora_cols(const Tensor& g, const Tensor& y, const std
 }  // namespace
 
 TORCH_LIBRARY(dlion, m) {
+  m.def("gemm_tn(Tensor[] P, Tensor[] Q, int splits) -> Tensor");
+  m.def("gemm_tn_(Tensor[] P, Tensor[] Q, Tensor(a!) out, bool accumulate) -> ()");
   m.def("lora_rows(Tensor x, Tensor w, float scale, float p, int seed) -> Tensor");
   m.def("lora_up(Tensor o, Tensor u, Tensor b, float s) -> Tensor");
   m.def("lora_cols(Tensor g, Tensor y, Tensor? a, float yscale, float p, int seed) -> (Tensor, Tensor)");
@@ -866,6 +916,8 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("embed_bwd_", &embed_bwd_);
   m.impl("scale_acc_", &scale_acc_);
   m.impl("lt_gemm_nt", &lt_gemm_nt);
+  m.impl("gemm_tn", &gemm_tn);
+  m.impl("gemm_tn_", &gemm_tn_);
   m.impl("lora_rows", &lora_rows);
   m.impl("lora_up", &lora_up);
   m.impl("lora_cols", &lora_cols);

@@ -133,16 +133,17 @@ def release_split_k_accumulators() -> None:
     _ACC.clear()
 
 
-def _acc_gemm(params, cols, a3, b3) -> bool:
-    """Accumulate bmm(a3, b3) (fp32, [S, R, C]) into the window's buffer for
-    `params` (column blocks `cols` of the flattened R*C).  False if the buffer
-    cannot be used (over budget, single-micro-batch window): the caller then
-    deposits into ``param.grad`` directly, on top of any flushed partials."""
+def _acc_gemm(params, cols, a, b, s) -> bool:
+    """Accumulate the s split-K partials of a^T b (fp32, [s, R, C]; a [T, R],
+    b [T, C] token-major) into the window's buffer for `params` (column blocks
+    `cols` of the flattened R*C).  False if the buffer cannot be used (over
+    budget, single-micro-batch window): the caller then deposits into
+    ``param.grad`` directly, on top of any flushed partials."""
     if not _FUSE_ACCUM["multi"]:
         return False
     key = tuple(id(p) for p in params)
     ent = _ACC.get(key)
-    shape = (a3.shape[0], a3.shape[1], b3.shape[2])
+    shape = (s, a.shape[1], b.shape[1])
     if ent is None or any(r() is not p for r, p in zip(ent[0], params)) or tuple(ent[1].shape) != shape:
         if ent is not None:
             if key in _PENDING:
@@ -158,15 +159,78 @@ def _acc_gemm(params, cols, a3, b3) -> bool:
                 _PENDING.remove(k)
         if used + math.prod(shape) * 4 > _ACC_BUDGET:
             return False
-        buf = torch.empty(shape, device=a3.device, dtype=torch.float32)
+        buf = torch.empty(shape, device=a.device, dtype=torch.float32)
         ent = [[weakref.ref(p) for p in params], buf, [(weakref.ref(p), c0, n) for p, (c0, n) in zip(params, cols)]]
         _ACC[key] = ent
-    if key in _PENDING:
-        torch.baddbmm(ent[1], a3, b3, out_dtype=torch.float32, out=ent[1])
-    else:
-        torch.bmm(a3, b3, out_dtype=torch.float32, out=ent[1])
+    accumulate = key in _PENDING
+    wgrad_partials(a, b, s, out=ent[1], accumulate=accumulate)
+    if not accumulate:
         _PENDING.append(key)
     return True
+
+
+# ------------------------------------------------------- weight-gradient GEMMs
+# dW = a^T b over the tokens: both operands token-major.  The own TN kernel
+# (csrc/gemm_tn.hip) writes / accumulates fp32 split-K partials; measured at
+# the GPT-2 shapes against torch.bmm / baddbmm (hipBLASLt) with each side's
+# best split (tools/bench_wgrad.py, 20480 tokens): c_attn 69 vs 94 us, c_fc
+# 86 vs 110, mlp c_proj 86 vs 107, attn c_proj 40 vs 38.
+_TN_ON = os.environ.get("DLION_TN_GEMM", "1") != "0"  # A/B switch for the own TN kernel
+
+
+def _tn_eligible(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return (_TN_ON and a.is_cuda and a.dtype == b.dtype == torch.bfloat16 and a.dim() == b.dim() == 2
+            and a.shape[0] == b.shape[0] and a.shape[0] % 128 == 0 and a.shape[1] % 8 == 0 and b.shape[1] % 8 == 0
+            and a.stride(1) == 1 and b.stride(1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
+            and a.stride(0) >= a.shape[1] and b.stride(0) >= b.shape[1]
+            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
+            and a.shape[0] * max(a.stride(0), b.stride(0)) < 2 ** 31)
+
+
+_TN_WAVE = int(os.environ.get("DLION_TN_WAVE", "256"))  # grid-size target of tn_split_factor
+_TN_MIN_TILES = 16  # below: hipBLASLt (attn c_proj 768x768, 9 tiles: 43 us vs 55 us in the step)
+
+
+def tn_split_factor(M: int, R: int, C: int) -> int:
+    """Splits of the token axis for the own TN kernel: as many as keep the
+    (256x256 tiles x splits) grid within one wave of the 256 CUs, <= 16."""
+    tiles = math.ceil(R / 256) * math.ceil(C / 256)
+    return max(1, min(16, _TN_WAVE // tiles, M // 128))
+
+
+def wgrad_splits(a: torch.Tensor, b: torch.Tensor) -> tuple:
+    """(split count, own TN kernel?) for a^T b."""
+    from . import hip
+
+    M, R, C = a.shape[0], a.shape[1], b.shape[1]
+    if (math.ceil(R / 256) * math.ceil(C / 256) >= _TN_MIN_TILES and _tn_eligible(a, b) and hip.available()):
+        return tn_split_factor(M, R, C), True
+    return split_k_factor(M, R, C), False
+
+
+def wgrad_partials(a: torch.Tensor, b: torch.Tensor, s: int, out=None, accumulate: bool = False,
+                   own: bool | None = None) -> torch.Tensor:
+    """fp32 [s, R, C] split-K partials of a^T b (a [T, R], b [T, C]); into /
+    onto `out` when given.  own: use the TN kernel (default: wgrad_splits'
+    choice)."""
+    from . import hip
+
+    M = a.shape[0]
+    if own is None:
+        own = wgrad_splits(a, b)[1]
+    if own and s <= M // 128:
+        if out is None:
+            return hip.ops().gemm_tn([a], [b], s)
+        hip.ops().gemm_tn_([a], [b], out, accumulate)
+        return out
+    a3, b3 = a.view(s, M // s, a.shape[1]).transpose(1, 2), b.view(s, M // s, b.shape[1])
+    if out is None:
+        return torch.bmm(a3, b3, out_dtype=torch.float32)
+    if accumulate:
+        torch.baddbmm(out, a3, b3, out_dtype=torch.float32, out=out)
+    else:
+        torch.bmm(a3, b3, out_dtype=torch.float32, out=out)
+    return out
 
 
 def _fuse_target(w) -> bool:
@@ -272,19 +336,22 @@ def wgrad_into(a: torch.Tensor, b: torch.Tensor, w: torch.nn.Parameter) -> None:
     g = w.grad
     M, K = a.shape
     N = b.shape[1]
-    s = split_k_factor(M, K, N)
+    s, own = wgrad_splits(a, b)
     grad_ok = g is None or (g.is_contiguous() and g.dtype == w.dtype)
-    if s > 1 and (K * N) % 4 == 0 and grad_ok:
+    if (s > 1 or own) and (K * N) % 4 == 0 and grad_ok and (own or M % s == 0):  # own kernel: uneven splits OK
         from . import hip
 
         if hip.available():
-            a3, b3 = a.view(s, M // s, K).transpose(1, 2), b.view(s, M // s, N)
-            if _FUSE_ACCUM["on"] and _acc_gemm([w], [(0, K * N)], a3, b3):
+            if _FUSE_ACCUM["on"] and _acc_gemm([w], [(0, K * N)], a, b, s):
                 return  # reduced into w.grad when the accumulation window closes
             g = w.grad  # _acc_gemm may have flushed earlier partials into it
             grad_ok = g is None or (g.is_contiguous() and g.dtype == w.dtype)
-            if g is not None and grad_ok:
-                hip.ops().sum_partials_acc_(torch.bmm(a3, b3, out_dtype=torch.float32), g)
+            if grad_ok:
+                part = wgrad_partials(a, b, s).view(s, K * N)
+                if g is None:
+                    w.grad = hip.ops().sum_partials(part).view_as(w)
+                else:
+                    hip.ops().sum_partials_acc_(part, g)
                 return
     if not grad_ok or g is None:
         fresh = wgrad(a, b)
@@ -297,15 +364,17 @@ def wgrad(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """a^T @ b for a [M, K], b [M, N] (-> [K, N]) with token-axis split-K."""
     M, K = a.shape
     N = b.shape[1]
-    s = split_k_factor(M, K, N) if a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) else 1
-    if s == 1:
+    if not (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16)):
         return a.t() @ b
-    part = torch.bmm(a.view(s, M // s, K).transpose(1, 2), b.view(s, M // s, N), out_dtype=torch.float32)
+    s, own = wgrad_splits(a, b)
+    if (s == 1 and not own) or (M % s and not own):
+        return a.t() @ b
+    part = wgrad_partials(a, b, s)
     if a.dtype == torch.bfloat16 and (K * N) % 4 == 0:
         from . import hip
 
         if hip.available():
-            return hip.ops().sum_partials(part)  # one pass: fp32 sum -> bf16
+            return hip.ops().sum_partials(part.view(s, K * N)).view(K, N)  # one pass: fp32 sum -> bf16
     return part.sum(0).to(a.dtype)
 
 
@@ -509,20 +578,18 @@ def _multi_wgrad_into(dy, x2d, params, sizes) -> None:
     """params[i].grad (+)= (dy[:, block i])^T x2d for every block, one GEMM."""
     M, N = dy.shape
     K = x2d.shape[1]
-    s = split_k_factor(M, N, K)
-    if s > 1 and (N * K) % 4 == 0 and M % s == 0:
+    s, own = wgrad_splits(dy, x2d)
+    if (s > 1 or own) and (N * K) % 4 == 0 and (own or M % s == 0):
         from . import hip
 
         if hip.available():
-            a3, b3 = dy.view(s, M // s, N).transpose(1, 2), x2d.view(s, M // s, K)
             cols, off = [], 0
             for n in sizes:
                 cols.append((off * K, n * K))
                 off += n
-            if _FUSE_ACCUM["on"] and _acc_gemm(list(params), cols, a3, b3):
+            if _FUSE_ACCUM["on"] and _acc_gemm(list(params), cols, dy, x2d, s):
                 return  # reduced into each params[i].grad when the window closes
-            part = torch.bmm(a3, b3, out_dtype=torch.float32)
-            flat = part.view(s, N * K)
+            flat = wgrad_partials(dy, x2d, s).view(s, N * K)
             off = 0
             for p, n in zip(params, sizes):
                 deposit_grad(p, flat[:, off * K:(off + n) * K])

@@ -1,0 +1,38 @@
+"""Weight-gradient GEMM (csrc/gemm_tn.hip): sum over its split slices of
+P^T Q against a PyTorch fp32 reference, over several segments, strided
+operands, edge tiles and split counts."""
+import pytest
+import torch
+
+from distributed_lion_pytorch_amd.ops import hip
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,N,rows,nseg,splits,ldp_pad,ldq_pad", [
+    (256, 256, 128, 1, 1, 0, 0),
+    (768, 2304, 1024, 2, 3, 0, 0),
+    (776, 264, 256, 3, 2, 8, 16),   # edge tiles in both dims, row strides > width
+    (3072, 768, 512, 4, 7, 0, 0),   # uneven splits of 16 k-tile pairs
+])
+def test_gemm_tn_matches_fp32(cuda, M, N, rows, nseg, splits, ldp_pad, ldq_pad):
+    hip.require()
+    torch.manual_seed(0)
+    P = [torch.randn(rows, M + ldp_pad, device=cuda, dtype=torch.bfloat16)[:, :M] for _ in range(nseg)]
+    Q = [torch.randn(rows, N + ldq_pad, device=cuda, dtype=torch.bfloat16)[:, :N] for _ in range(nseg)]
+    out = hip.ops().gemm_tn(P, Q, splits)
+    assert out.shape == (splits, M, N) and out.dtype == torch.float32
+    ref = torch.cat(P).float().t() @ torch.cat(Q).float()
+    err = (out.sum(0) - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-3, err
+
+
+def test_gemm_tn_split_slices_are_partial_sums(cuda):
+    hip.require()
+    torch.manual_seed(1)
+    P = [torch.randn(512, 256, device=cuda, dtype=torch.bfloat16)]
+    Q = [torch.randn(512, 512, device=cuda, dtype=torch.bfloat16)]
+    out = hip.ops().gemm_tn(P, Q, 2)  # 2 pairs of 64-row k-tiles: rows 0..255 and 256..511
+    for z, (a, b) in enumerate(((0, 256), (256, 512))):
+        ref = P[0][a:b].float().t() @ Q[0][a:b].float()
+        assert (out[z] - ref).abs().max().item() / ref.abs().max().item() < 1e-3
