@@ -39,6 +39,21 @@ n unknown); ``release_split_k_accumulators()`` frees them, and
 ``DLION_SPLITK_ACC=0`` disables them.  A change of split factor inside a window
 (micro-batches with different token counts) first flushes the running
 partials into ``param.grad``, then starts a fresh buffer.
+
+Deferred weight gradients (own TN kernel, csrc/gemm_tn.hip): inside a
+multi-micro-batch window the weight gradient is not computed per micro-batch
+at all.  Its two token-major operands (the layer input and the output
+gradient) are kept, and the window's exit runs ONE GEMM per weight whose
+reduction axis is the concatenation of all micro-batches (the kernel takes up
+to 16 operand segments): the fp32 split-K partials are written once per step
+instead of read-modified-written every micro-batch, and each split runs a
+long K.  Measured at the GPT-2 bench shapes (tools/bench_wgrad.py --window 8):
+c_fc / mlp c_proj 103 -> 80 us, c_attn 86 -> 62 us, attn c_proj 43 -> 29 us
+per micro-batch.  The kept operands cost memory (~500 MB per GPT-2 layer per
+micro-batch at 20480 tokens), capped by ``DLION_WGRAD_DEFER_GB`` (default:
+a quarter of the device memory); past the cap, or at 16 segments, a weight's
+segments are reduced early into its accumulator.  ``DLION_WGRAD_DEFER=0``
+disables the deferral.
 """
 from __future__ import annotations
 
@@ -53,6 +68,10 @@ _FUSE_ACCUM = {"on": False, "multi": True}
 _ACC_BUDGET = (8 << 30) if os.environ.get("DLION_SPLITK_ACC", "1") != "0" else 0  # bytes of fp32 accumulators
 _ACC: dict = {}  # key -> [weakrefs of params, fp32 buffer [S, ...], [(param ref, col0, ncols)]]
 _PENDING: list = []  # keys written in the current window, in order
+_WDEFER_ON = os.environ.get("DLION_WGRAD_DEFER", "1") != "0"
+_WDEFER: dict = {}  # key -> [params, cols, [a segments], [b segments], [versions]]
+_WDEFER_BYTES = [0]
+_WDEFER_MAX_SEG = 16  # csrc/gemm_tn.hip kMaxSeg
 
 
 @contextlib.contextmanager
@@ -77,6 +96,7 @@ def grad_accumulation_fusion(enabled: bool = True, micro_batches: int | None = N
                 flush_deferred_partials()
             _PENDING.clear()
             _clear_deferred()
+            _drop_deferred()
 
 
 def begin_fusion_window(micro_batches: int | None = None) -> bool:
@@ -101,6 +121,7 @@ def end_fusion_window(flush: bool = True) -> None:
         flush_deferred_partials()
     _PENDING.clear()
     _clear_deferred()
+    _drop_deferred()
 
 
 def fusion_window_open() -> bool:
@@ -115,9 +136,78 @@ def _flush_entry(ent) -> None:
             deposit_grad(p, flat[:, c0:c0 + n])
 
 
+def _wdefer_budget() -> int:
+    gb = os.environ.get("DLION_WGRAD_DEFER_GB")
+    if gb is not None:
+        return int(float(gb) * (1 << 30))
+    try:
+        return torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory // 4
+    except Exception:
+        return 0
+
+
+def _run_deferred(key) -> None:
+    """One TN GEMM over every kept segment of `key` into its accumulator."""
+    from . import hip
+
+    params, cols, segs_a, segs_b, vers = _WDEFER.pop(key)
+    _WDEFER_BYTES[0] -= sum(t.numel() * t.element_size() for t in segs_a + segs_b)
+    for t, v in zip(segs_a + segs_b, vers):
+        if t._version != v:
+            raise RuntimeError("dlion: an operand kept for a deferred weight gradient was modified in place")
+    ent = _ACC[key]
+    accumulate = key in _PENDING
+    hip.ops().gemm_tn_(segs_a, segs_b, ent[1], accumulate)
+    if not accumulate:
+        _PENDING.append(key)
+
+
+def _run_all_deferred() -> None:
+    for key in list(_WDEFER):
+        _run_deferred(key)
+
+
+def _drop_deferred() -> None:
+    _WDEFER.clear()
+    _WDEFER_BYTES[0] = 0
+
+
+def _defer_wgrad(params, cols, a, b, s) -> bool:
+    """Keep a^T b's operands for one window-level GEMM (see the module notes).
+    False if not applicable (fallback: _acc_gemm now)."""
+    if not (_WDEFER_ON and _FUSE_ACCUM["multi"]):
+        return False
+    key = tuple(id(p) for p in params)
+    nb = a.numel() * a.element_size() + b.numel() * b.element_size()
+    ent = _WDEFER.get(key)
+    if ent is not None:
+        a0, b0 = ent[2][0], ent[3][0]
+        if (a.shape != a0.shape or b.shape != b0.shape or a.stride() != a0.stride() or b.stride() != b0.stride()
+                or any(r() is not p for r, p in zip(ent[0], params))):
+            _run_deferred(key)
+            ent = None
+    if _WDEFER_BYTES[0] + nb > _wdefer_budget():
+        if ent is not None:
+            _run_deferred(key)
+        return False
+    if ent is None:
+        # the accumulator [s, R, C] the window's exit reduces into param.grad
+        if not _ensure_acc(params, cols, (s, a.shape[1], b.shape[1]), a.device):
+            return False
+        ent = _WDEFER[key] = [[weakref.ref(p) for p in params], cols, [], [], []]
+    ent[2].append(a)
+    ent[3].append(b)
+    ent[4].extend([a._version, b._version])
+    _WDEFER_BYTES[0] += nb
+    if len(ent[2]) == _WDEFER_MAX_SEG:
+        _run_deferred(key)
+    return True
+
+
 def flush_split_k_accumulators() -> None:
     """Reduce every split-K accumulator written in this window into its
     parameters' ``.grad`` (one fused sum + deposit per weight)."""
+    _run_all_deferred()
     for key in _PENDING:
         ent = _ACC.get(key)
         if ent is not None:
@@ -130,7 +220,34 @@ def release_split_k_accumulators() -> None:
     into ``param.grad`` first).  Call after training to return the memory."""
     flush_split_k_accumulators()
     flush_deferred_partials()
+    _drop_deferred()
     _ACC.clear()
+
+
+def _ensure_acc(params, cols, shape, device) -> bool:
+    """Make sure the window accumulator of `params` has `shape` (flushing a
+    differently shaped one that already holds this window's partials)."""
+    key = tuple(id(p) for p in params)
+    ent = _ACC.get(key)
+    if ent is not None and all(r() is p for r, p in zip(ent[0], params)) and tuple(ent[1].shape) == tuple(shape):
+        return True
+    if ent is not None:
+        if key in _PENDING:
+            # split factor / token count changed inside the window: the
+            # partials so far go into param.grad before the buffer is replaced
+            _flush_entry(ent)
+            _PENDING.remove(key)
+        _ACC.pop(key)
+    used = sum(e[1].numel() * 4 for e in _ACC.values() if all(r() is not None for r in e[0]))
+    for k in [k for k, e in _ACC.items() if any(r() is None for r in e[0])]:
+        _ACC.pop(k)  # parameters gone: drop their buffers
+        if k in _PENDING:
+            _PENDING.remove(k)
+    if used + math.prod(shape) * 4 > _ACC_BUDGET:
+        return False
+    buf = torch.empty(shape, device=device, dtype=torch.float32)
+    _ACC[key] = [[weakref.ref(p) for p in params], buf, [(weakref.ref(p), c0, n) for p, (c0, n) in zip(params, cols)]]
+    return True
 
 
 def _acc_gemm(params, cols, a, b, s) -> bool:
@@ -142,26 +259,11 @@ def _acc_gemm(params, cols, a, b, s) -> bool:
     if not _FUSE_ACCUM["multi"]:
         return False
     key = tuple(id(p) for p in params)
-    ent = _ACC.get(key)
-    shape = (s, a.shape[1], b.shape[1])
-    if ent is None or any(r() is not p for r, p in zip(ent[0], params)) or tuple(ent[1].shape) != shape:
-        if ent is not None:
-            if key in _PENDING:
-                # split factor / token count changed inside the window: the
-                # partials so far go into param.grad before the buffer is replaced
-                _flush_entry(ent)
-                _PENDING.remove(key)
-            _ACC.pop(key)
-        used = sum(e[1].numel() * 4 for e in _ACC.values() if all(r() is not None for r in e[0]))
-        for k in [k for k, e in _ACC.items() if any(r() is None for r in e[0])]:
-            _ACC.pop(k)  # parameters gone: drop their buffers
-            if k in _PENDING:
-                _PENDING.remove(k)
-        if used + math.prod(shape) * 4 > _ACC_BUDGET:
-            return False
-        buf = torch.empty(shape, device=a.device, dtype=torch.float32)
-        ent = [[weakref.ref(p) for p in params], buf, [(weakref.ref(p), c0, n) for p, (c0, n) in zip(params, cols)]]
-        _ACC[key] = ent
+    if key in _WDEFER:
+        _run_deferred(key)  # keep the micro-batch order of the accumulation simple
+    if not _ensure_acc(params, cols, (s, a.shape[1], b.shape[1]), a.device):
+        return False
+    ent = _ACC[key]
     accumulate = key in _PENDING
     wgrad_partials(a, b, s, out=ent[1], accumulate=accumulate)
     if not accumulate:
@@ -342,7 +444,8 @@ def wgrad_into(a: torch.Tensor, b: torch.Tensor, w: torch.nn.Parameter) -> None:
         from . import hip
 
         if hip.available():
-            if _FUSE_ACCUM["on"] and _acc_gemm([w], [(0, K * N)], a, b, s):
+            if _FUSE_ACCUM["on"] and ((own and _defer_wgrad([w], [(0, K * N)], a, b, s))
+                                      or _acc_gemm([w], [(0, K * N)], a, b, s)):
                 return  # reduced into w.grad when the accumulation window closes
             g = w.grad  # _acc_gemm may have flushed earlier partials into it
             grad_ok = g is None or (g.is_contiguous() and g.dtype == w.dtype)
@@ -587,7 +690,8 @@ def _multi_wgrad_into(dy, x2d, params, sizes) -> None:
             for n in sizes:
                 cols.append((off * K, n * K))
                 off += n
-            if _FUSE_ACCUM["on"] and _acc_gemm(list(params), cols, dy, x2d, s):
+            if _FUSE_ACCUM["on"] and ((own and _defer_wgrad(list(params), cols, dy, x2d, s))
+                                      or _acc_gemm(list(params), cols, dy, x2d, s)):
                 return  # reduced into each params[i].grad when the window closes
             flat = wgrad_partials(dy, x2d, s).view(s, N * K)
             off = 0

@@ -36,3 +36,29 @@ def test_gemm_tn_split_slices_are_partial_sums(cuda):
     for z, (a, b) in enumerate(((0, 256), (256, 512))):
         ref = P[0][a:b].float().t() @ Q[0][a:b].float()
         assert (out[z] - ref).abs().max().item() / ref.abs().max().item() < 1e-3
+
+
+@pytest.mark.parametrize("defer", [True, False])
+def test_window_wgrad_deferral(cuda, monkeypatch, defer):
+    """Inside a multi-micro-batch fusion window the weight gradients are kept
+    as operand segments and reduced by ONE TN GEMM at the window's exit
+    (ops/linear._defer_wgrad); the result equals the per-micro-batch sum."""
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    monkeypatch.setattr(L, "_WDEFER_ON", defer)
+    torch.manual_seed(2)
+    T, K, N, mbs = 512, 768, 2304, 3
+    w = torch.nn.Parameter(torch.zeros(K, N, device=cuda, dtype=torch.bfloat16))
+    xs = [torch.randn(T, K, device=cuda, dtype=torch.bfloat16) for _ in range(mbs)]
+    gs = [torch.randn(T, N, device=cuda, dtype=torch.bfloat16) for _ in range(mbs)]
+    L.release_split_k_accumulators()
+    with L.grad_accumulation_fusion(True, micro_batches=mbs):
+        for x, g in zip(xs, gs):
+            L.wgrad_into(x, g, w)
+        assert bool(L._WDEFER) == defer
+        assert w.grad is None  # nothing reduced before the window closes
+    assert not L._WDEFER
+    ref = sum(x.float().t() @ g.float() for x, g in zip(xs, gs))
+    err = (w.grad.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 8e-3, err
