@@ -402,6 +402,21 @@ void sum_partials_acc_(const Tensor& part, const Tensor& out) {
             "sum_partials_acc_");
 }
 
+// out (+)= bf16(s[0] * sum_s part[s]): the LM head's split-K weight gradient scaled by the
+// loss gradient (a device scalar) and accumulated into .grad in one pass
+void sum_partials_scaled_(const Tensor& part, const Tensor& s, const Tensor& out, bool accumulate) {
+  const auto P = partials(part);
+  check_dev(s, "s");
+  TORCH_CHECK(s.scalar_type() == at::kFloat && s.numel() >= 1, "dlion: scale must be float32");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == P.n,
+              "dlion: target must be a contiguous bf16 tensor of the partial row size");
+  TORCH_CHECK(P.n % 4 == 0, "dlion: partial row length must be a multiple of 4");
+  const c10::DeviceGuard g(part.device());
+  check_hip(dlion::launch_sum_partials(P.ptr, static_cast<int>(P.S), P.n, P.ld, out.data_ptr(), accumulate, cur_stream(),
+                                       s.data_ptr<float>()),
+            "sum_partials_scaled_");
+}
+
 // fp32 [parts, N] column-sum partials of a bf16 [rows, N] matrix
 Tensor colsum_partials(const Tensor& x, int64_t parts) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(),
@@ -862,6 +877,7 @@ TORCH_LIBRARY(dlion, m) {
   m.def("bias_gelu_bwd(Tensor dh, Tensor z, Tensor b, bool exact, int parts) -> (Tensor, Tensor)");
   m.def("sum_partials(Tensor part) -> Tensor");
   m.def("sum_partials_acc_(Tensor part, Tensor(a!) out) -> ()");
+  m.def("sum_partials_scaled_(Tensor part, Tensor s, Tensor(a!) out, bool accumulate) -> ()");
   m.def("colsum_partials(Tensor x, int parts) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float p, int seed) -> (Tensor, Tensor)");
   m.def(
@@ -901,6 +917,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("bias_gelu_bwd", &bias_gelu_bwd);
   m.impl("sum_partials", &sum_partials);
   m.impl("sum_partials_acc_", &sum_partials_acc_);
+  m.impl("sum_partials_scaled_", &sum_partials_scaled_);
   m.impl("colsum_partials", &colsum_partials);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);

@@ -80,8 +80,10 @@ __global__ void __launch_bounds__(1024) bias_gelu_bwd_kernel(const uint16_t* __r
 // fused into the split-K reduction)), 4 elements per thread
 template <bool ACC>
 __global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restrict__ part, int S, int64_t n,
-                                                          int64_t ld, uint16_t* __restrict__ out) {
+                                                          int64_t ld, uint16_t* __restrict__ out,
+                                                          const float* __restrict__ scale) {
   const int64_t n4 = n / 4;
+  const float sc = scale ? scale[0] : 1.f;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n4;
        i += static_cast<int64_t>(gridDim.x) * 256) {
     float4 acc = reinterpret_cast<const float4*>(part)[i];
@@ -89,6 +91,7 @@ __global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restri
       const float4 v = reinterpret_cast<const float4*>(part + static_cast<int64_t>(s) * ld)[i];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
+    acc.x *= sc; acc.y *= sc; acc.z *= sc; acc.w *= sc;
     if constexpr (ACC) {
       const uint2 o = reinterpret_cast<const uint2*>(out)[i];
       acc.x += bf16_to_f32(o.x & 0xffffu);
@@ -255,7 +258,8 @@ constexpr int kTallQ = 8, kTallR = 32;
 template <bool ACC>
 __global__ void __launch_bounds__(kTallQ * kTallR) sum_partials_tall_kernel(const float* __restrict__ part, int S,
                                                                            int64_t n, int64_t ld,
-                                                                           uint16_t* __restrict__ out) {
+                                                                           uint16_t* __restrict__ out,
+                                                                           const float* __restrict__ scale) {
   __shared__ float4 red[kTallR][kTallQ];
   const int q = threadIdx.x % kTallQ, r = threadIdx.x / kTallQ;
   const int64_t col4 = static_cast<int64_t>(blockIdx.x) * kTallQ + q;  // float4 column index
@@ -275,6 +279,10 @@ __global__ void __launch_bounds__(kTallQ * kTallR) sum_partials_tall_kernel(cons
     for (int i = 1; i < kTallR; ++i) {
       const float4 v = red[i][q];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    if (scale) {
+      const float sc = scale[0];
+      acc.x *= sc; acc.y *= sc; acc.z *= sc; acc.w *= sc;
     }
     if constexpr (ACC) {
       const uint2 o = reinterpret_cast<const uint2*>(out)[col4];
@@ -377,7 +385,7 @@ hipError_t launch_rope(const void* x, const void* cos, const void* sin, void* y,
 }
 
 hipError_t launch_sum_partials(const float* part, int S, int64_t n, int64_t ld, void* out, bool accumulate,
-                               hipStream_t st) {
+                               hipStream_t st, const float* scale) {
   if (n % 4 != 0 || ld % 4 != 0 || ld < n) return hipErrorInvalidValue;
   const int64_t n4 = n / 4;
   auto O = static_cast<uint16_t*>(out);
@@ -386,13 +394,13 @@ hipError_t launch_sum_partials(const float* part, int S, int64_t n, int64_t ld, 
     const int64_t blocks = (n4 + kTallQ - 1) / kTallQ;
     if (blocks > 0x7fffffff) return hipErrorInvalidValue;
     const dim3 g(static_cast<unsigned>(blocks)), blk(kTallQ * kTallR);
-    if (accumulate) hipLaunchKernelGGL(sum_partials_tall_kernel<true>, g, blk, 0, st, part, S, n, ld, O);
-    else hipLaunchKernelGGL(sum_partials_tall_kernel<false>, g, blk, 0, st, part, S, n, ld, O);
+    if (accumulate) hipLaunchKernelGGL(sum_partials_tall_kernel<true>, g, blk, 0, st, part, S, n, ld, O, scale);
+    else hipLaunchKernelGGL(sum_partials_tall_kernel<false>, g, blk, 0, st, part, S, n, ld, O, scale);
     return hipGetLastError();
   }
   const dim3 g(grid_for(n / 4, 256)), blk(256);
-  if (accumulate) hipLaunchKernelGGL(sum_partials_kernel<true>, g, blk, 0, st, part, S, n, ld, O);
-  else hipLaunchKernelGGL(sum_partials_kernel<false>, g, blk, 0, st, part, S, n, ld, O);
+  if (accumulate) hipLaunchKernelGGL(sum_partials_kernel<true>, g, blk, 0, st, part, S, n, ld, O, scale);
+  else hipLaunchKernelGGL(sum_partials_kernel<false>, g, blk, 0, st, part, S, n, ld, O, scale);
   return hipGetLastError();
 }
 

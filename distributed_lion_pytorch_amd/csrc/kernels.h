@@ -50,8 +50,9 @@ hipError_t launch_swiglu_bwd(const void* dh, const void* g, const void* u, void*
                              int64_t F, int64_t ld_in, int64_t ld_out, hipStream_t st);
 hipError_t launch_rope(const void* x, const void* cos, const void* sin, void* y, int64_t rows, int T, int H, int D,
                        bool inverse, int64_t x_ld, int64_t y_ld, hipStream_t st);
+// out (+)= bf16(scale[0] * sum_s part[s]) (scale: optional device scalar)
 hipError_t launch_sum_partials(const float* part, int S, int64_t n, int64_t ld, void* out, bool accumulate,
-                               hipStream_t st);
+                               hipStream_t st, const float* scale = nullptr);
 hipError_t launch_colsum(const void* x, float* part, int parts, int64_t rows, int N, hipStream_t st);
 
 // ---- bf16 GEMM C[M,N] = A[M,K] . B[N,K]^T with fused epilogue (gemm.hip)

@@ -915,6 +915,25 @@ def _lm_dgrad(g: torch.Tensor, weight: torch.Tensor, wp: torch.Tensor) -> torch.
     return g @ wp
 
 
+_LM_TN = os.environ.get("DLION_LM_TN", "1") != "0"  # A/B switch for _lm_wgrad_partials
+
+
+def _lm_wgrad_partials(g: torch.Tensor, h2d: torch.Tensor, v: int):
+    """The LM head's weight gradient g^T h (g = softmax - onehot [N, Vp]) as
+    fp32 split partials [S, v*C] from the own TN kernel (csrc/gemm_tn.hip), or
+    None when not applicable.  GPT-2: 591 output tiles -> 3 splits (7 short
+    waves instead of 3 long ones); the backward reduces, scales by the loss
+    gradient and deposits them in one pass.  Measured 1.62 ms (hipBLASLt) vs
+    ~1.3 ms + 0.15 ms of partial traffic (tools/bench_wgrad.py)."""
+    from .linear import _tn_eligible, tn_split_factor
+
+    if not (_LM_TN and g.shape[1] % 8 == 0 and _tn_eligible(g, h2d) and hip.available()):
+        return None
+    s = tn_split_factor(g.shape[0], g.shape[1], h2d.shape[1])
+    part = hip.ops().gemm_tn([g], [h2d], s)  # [S, Vp, C]
+    return part.view(s, -1)[:, : v * h2d.shape[1]]
+
+
 class _LMHeadCE(torch.autograd.Function):
     """loss = mean_{labels != -100} CE(h @ W^T, labels), gradients computed in
     the forward pass (the loss gradient is a scalar multiple of
@@ -939,7 +958,13 @@ class _LMHeadCE(torch.autograd.Function):
         loss = row_loss.sum() / n_valid
         if need_grad:
             dh = _lm_dgrad(logits, weight, wp)  # [N, C]
-            dw = (logits.t() @ h2d)[:v] if ctx.needs_input_grad[1] else None
+            dw = None
+            ctx.dw_parts = False
+            if ctx.needs_input_grad[1]:
+                dw = _lm_wgrad_partials(logits, h2d, v)
+                ctx.dw_parts = dw is not None
+                if dw is None:
+                    dw = (logits.t() @ h2d)[:v]
             ctx.save_for_backward(dh, dw if dw is not None else dh.new_empty(0), n_valid)
             ctx.has_dw = dw is not None
             from .linear import _fuse_target
@@ -965,7 +990,19 @@ class _LMHeadCE(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gh = torch.empty_like(dh)
             ops.scale_acc_(dh, s, gh, False)
-        if ctx.has_dw and ctx.needs_input_grad[1]:
+        if ctx.has_dw and ctx.needs_input_grad[1] and ctx.dw_parts:
+            # fp32 split partials [S, v*C] (row-strided): reduce + scale + deposit in one pass
+            w = ctx.weight
+            if w is not None and w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == dh.dtype:
+                ops.sum_partials_scaled_(dw, s, w.grad, True)
+            else:
+                out = torch.empty(dw.shape[1] // dh.shape[1], dh.shape[1], dtype=dh.dtype, device=dh.device)
+                ops.sum_partials_scaled_(dw, s, out, False)
+                if w is not None:
+                    w.grad = out if w.grad is None else w.grad + out
+                else:
+                    gw = out
+        elif ctx.has_dw and ctx.needs_input_grad[1]:
             w = ctx.weight
             if w is not None and w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == dw.dtype:
                 ops.scale_acc_(dw, s, w.grad, True)

@@ -293,11 +293,24 @@ _TN_WAVE = int(os.environ.get("DLION_TN_WAVE", "256"))  # grid-size target of tn
 _TN_MIN_TILES = 16  # below: hipBLASLt (attn c_proj 768x768, 9 tiles: 43 us vs 55 us in the step)
 
 
+_TN_CU_RATE = 4.9e12  # FLOP/s of one CU in the TN kernel (1.25 PF/s over 256 CUs)
+_TN_BW = 5.0e12  # B/s for the fp32 partials (written once, read once by the reduction)
+
+
 def tn_split_factor(M: int, R: int, C: int) -> int:
-    """Splits of the token axis for the own TN kernel: as many as keep the
-    (256x256 tiles x splits) grid within one wave of the 256 CUs, <= 16."""
+    """Splits of the token axis for the own TN kernel: minimises waves of
+    (256x256 tiles x splits) blocks x per-block time + the fp32 partial
+    traffic (splits x R x C x 8 bytes).  GPT-2 c_fc: 7 (252 blocks, one wave),
+    c_attn: 9; the LM head's 591 tiles: 3 (7 waves instead of 3 long ones);
+    Llama-sized weights: 1."""
     tiles = math.ceil(R / 256) * math.ceil(C / 256)
-    return max(1, min(16, _TN_WAVE // tiles, M // 128))
+    best, best_cost = 1, None
+    for s in range(1, max(1, min(16, M // 128)) + 1):
+        waves = math.ceil(tiles * s / _TN_WAVE)
+        cost = waves * (2.0 * 65536 * M / s) / _TN_CU_RATE + 8.0 * s * R * C / _TN_BW
+        if best_cost is None or cost < best_cost:
+            best, best_cost = s, cost
+    return best
 
 
 def wgrad_splits(a: torch.Tensor, b: torch.Tensor) -> tuple:

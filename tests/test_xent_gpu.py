@@ -71,3 +71,27 @@ def test_lm_head_ce_parameter_uses_own_dgrad_gemm(cuda):
     from distributed_lion_pytorch_amd.ops.linear import _WT_CACHE
 
     assert (id(w), "pad_t") in _WT_CACHE
+
+
+@pytest.mark.parametrize("preexisting_grad", [False, True])
+def test_lm_head_ce_weight_grad_on_tn_kernel(cuda, preexisting_grad):
+    """Token count % 128 == 0: the LM head's weight gradient comes from the own
+    TN kernel as fp32 split partials, reduced + scaled (+ accumulated) in one
+    pass (ops/fused._lm_wgrad_partials, sum_partials_scaled_)."""
+    hip.require()
+    torch.manual_seed(3)
+    V, C = 50257, 256
+    h = torch.randn(2, 128, C, device=cuda).bfloat16().requires_grad_()
+    w = torch.nn.Parameter((0.05 * torch.randn(V, C, device=cuda)).bfloat16())
+    g0 = (0.01 * torch.randn(V, C, device=cuda)).bfloat16() if preexisting_grad else None
+    if g0 is not None:
+        w.grad = g0.clone()
+    labels = torch.randint(0, V, (2, 128), device=cuda)
+    loss = 3.0 * fused.lm_head_cross_entropy(h, w, labels)  # a non-unit loss gradient
+    loss.backward()
+    hr, wr = h.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    ref = 3.0 * torch.nn.functional.cross_entropy((hr @ wr.t()).view(-1, V), labels.view(-1))
+    ref.backward()
+    want = wr.grad + (g0.float() if g0 is not None else 0.0)
+    assert (w.grad.float() - want).abs().max().item() < 2e-2 * want.abs().max().item() + 1e-4
+    assert (h.grad.float() - hr.grad).abs().max().item() < 2e-2 * hr.grad.abs().max().item() + 1e-4
