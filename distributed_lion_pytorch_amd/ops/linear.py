@@ -318,7 +318,11 @@ def wgrad_splits(a: torch.Tensor, b: torch.Tensor) -> tuple:
     from . import hip
 
     M, R, C = a.shape[0], a.shape[1], b.shape[1]
-    if (math.ceil(R / 256) * math.ceil(C / 256) >= _TN_MIN_TILES and _tn_eligible(a, b) and hip.available()):
+    # small outputs: hipBLASLt per micro-batch, but the own kernel when the
+    # window defers the GEMM (attn c_proj over 8 micro-batches: 29 vs 43 us/mb)
+    deferred = _WDEFER_ON and _FUSE_ACCUM["on"] and _FUSE_ACCUM["multi"]
+    if ((deferred or math.ceil(R / 256) * math.ceil(C / 256) >= _TN_MIN_TILES) and _tn_eligible(a, b)
+            and hip.available()):
         return tn_split_factor(M, R, C), True
     return split_k_factor(M, R, C), False
 

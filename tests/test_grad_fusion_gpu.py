@@ -40,14 +40,16 @@ def test_fused_accumulation_matches_autograd(family, cuda):
         assert err < 2e-2, (n, err)
 
 
-def test_split_k_accumulator_window(cuda):
+def test_split_k_accumulator_window(cuda, monkeypatch):
     """Split-K weight gradients stay in fp32 [S, K, N] buffers across the
     micro-batches of one window (GEMM epilogue accumulation) and reach
     param.grad once, when the window closes; the sum is fp32-exact to bf16
-    rounding of the final gradient."""
+    rounding of the final gradient.  (Deferral off: this is the per-micro-batch
+    accumulator path; tests/test_gemm_tn_gpu.py covers the deferred one.)"""
     from distributed_lion_pytorch_amd.ops import linear as L
 
     hip.require()
+    monkeypatch.setattr(L, "_WDEFER_ON", False)
     torch.manual_seed(3)
     K, N, M = 256, 768, 2048
     assert L.split_k_factor(M, K, N) > 1
