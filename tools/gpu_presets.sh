@@ -1,16 +1,13 @@
-# BASELINE configs on one MI355X: reference algorithm A/B, Llama-2-7B LoRA SFT / DPO, Llama-3-8B full-param
+# Every BASELINE preset of bench.py on one GPU (+ the HF run_clm path), one JSON line each,
+# into gpurun_out/presets.jsonl.  usage: bash tools/gpu_presets.sh
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/presets
-out=gpurun_out/presets/presets.jsonl
-: > $out
-timeout -k 10 300 python bench.py --impl reference --steps 3 --warmup 1 2>/dev/null | tail -1 >> $out || exit 1
-for t in sft dpo llama3; do
-  timeout -k 10 400 python bench.py --task $t --steps 4 --warmup 2 2>/dev/null | tail -1 >> $out || exit 1
-done
-python - <<'PY'
-import json
-for l in open("gpurun_out/presets/presets.jsonl"):
-    d = json.loads(l)
-    print(f"{d['config']['task']:7s} {d['config']['impl']:9s} {d['config']['model']:28s} {d['value']:>12,.1f} tok/s  {d['ms_per_step']:9.1f} ms/step")
-PY
+OUT=gpurun_out/presets.jsonl
+: > $OUT
+run() { timeout -k 10 600 python bench.py "$@" 2>gpurun_out/preset_err.log | tail -1 >> $OUT || { tail -20 gpurun_out/preset_err.log; exit 1; }; }
+run --steps 8 --warmup 2
+run --impl reference --steps 3 --warmup 1
+run --task sft --steps 4 --warmup 2
+run --task dpo --steps 3 --warmup 1
+run --task llama3 --steps 4 --warmup 2
+STEPS=12 bash tools/gpu_runclm.sh presets --logging_steps 5 || exit 1
