@@ -62,3 +62,33 @@ def test_window_wgrad_deferral(cuda, monkeypatch, defer):
     ref = sum(x.float().t() @ g.float() for x, g in zip(xs, gs))
     err = (w.grad.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 8e-3, err
+
+
+@pytest.mark.parametrize("case", ["varying_tokens", "tiny_budget", "many_segments", "shared_weight"])
+def test_window_wgrad_deferral_edge_cases(cuda, monkeypatch, case):
+    """Deferred weight gradients against the fp32 sum in the branches that
+    reshape or bypass the kept segments: a token count change inside the
+    window (segments flushed, accumulator re-split), a memory cap below one
+    micro-batch (per-micro-batch accumulation), more micro-batches than the
+    kernel's 16 segments, and one weight used twice per micro-batch (tied
+    layers: both calls land in the same kept segments)."""
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    torch.manual_seed(4)
+    K, N = 256, 768
+    Ms = {"varying_tokens": [1024, 1024, 512, 1024], "many_segments": [256] * 18}.get(case, [512, 512, 512])
+    if case == "tiny_budget":
+        monkeypatch.setattr(L, "_wdefer_budget", lambda: 1)
+    w = torch.nn.Parameter(torch.zeros(K, N, device=cuda, dtype=torch.bfloat16))
+    reps = 2 if case == "shared_weight" else 1
+    xs = [torch.randn(m, K, device=cuda, dtype=torch.bfloat16) for m in Ms for _ in range(reps)]
+    gs = [torch.randn(x.shape[0], N, device=cuda, dtype=torch.bfloat16) for x in xs]
+    L.release_split_k_accumulators()
+    with L.grad_accumulation_fusion(True, micro_batches=len(Ms)):
+        for x, g in zip(xs, gs):
+            L.wgrad_into(x, g, w)
+    assert not L._WDEFER
+    ref = sum(x.float().t() @ g.float() for x, g in zip(xs, gs))
+    err = (w.grad.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 8e-3, err
