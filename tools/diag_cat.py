@@ -21,11 +21,19 @@ def traced(ts):
 
 
 L._adjacent_views = traced
-cfg = llama_config("llama-tiny", hidden_size=512, intermediate_size=1024, num_attention_heads=4, num_key_value_heads=4)
+import sys
+
+if len(sys.argv) > 1 and sys.argv[1] == "7b":  # Llama-2-7B layer shapes, 2 layers, the SFT micro-batch
+    cfg = llama_config("llama-2-7b", num_hidden_layers=2)
+    B, T = 4, 1024
+else:
+    cfg = llama_config("llama-tiny", hidden_size=512, intermediate_size=1024, num_attention_heads=4,
+                       num_key_value_heads=4)
+    B, T = 2, 256
 model = LlamaForCausalLM(cfg).to("cuda", torch.bfloat16)
 inject_lora(model, LoraConfig(r=8, lora_alpha=16, lora_dropout=0.05))
 model.train()
-ids = torch.randint(0, 512, (2, 256), device="cuda")
+ids = torch.randint(0, 512, (B, T), device="cuda")
 model(input_ids=ids, labels=ids).loss.backward()
 torch.cuda.synchronize()
 with profile(activities=[ProfilerActivity.CPU], record_shapes=True) as prof:
