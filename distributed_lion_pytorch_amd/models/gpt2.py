@@ -28,7 +28,7 @@ from transformers import GPT2Config, PreTrainedModel
 from transformers.modeling_outputs import CausalLMOutputWithCrossAttentions
 
 from ..ops import fused
-from ..ops.linear import linear_kn
+from ..ops.linear import linear_kn, no_wgrad_deferral_this_window
 
 GPT2_SIZES = {
     "gpt2": dict(n_embd=768, n_layer=12, n_head=12),
@@ -133,6 +133,7 @@ class GPT2Model(nn.Module):
         p = self.embd_pdrop if self.training else 0.0
         x = fused.embed(input_ids, self.wte.weight, self.wpe.weight, p)  # gather + add + dropout, one kernel
         if self.gradient_checkpointing and self.training:
+            no_wgrad_deferral_this_window()  # keep checkpointing's memory saving (ops/linear.py)
             for blk in self.h:
                 x = torch.utils.checkpoint.checkpoint(blk, x, use_reentrant=False)
             return fused.layer_norm(x, self.ln_f)

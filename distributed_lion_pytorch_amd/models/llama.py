@@ -20,7 +20,7 @@ from transformers import LlamaConfig, PreTrainedModel
 from transformers.modeling_outputs import CausalLMOutputWithPast
 
 from ..ops import fused
-from ..ops.linear import linear_multi_nk, linear_nk
+from ..ops.linear import linear_multi_nk, linear_nk, no_wgrad_deferral_this_window
 
 LLAMA_SIZES = {
     "llama-2-7b": dict(hidden_size=4096, intermediate_size=11008, num_hidden_layers=32, num_attention_heads=32,
@@ -183,6 +183,7 @@ class LlamaModel(nn.Module):
         x = self.embed_tokens(input_ids)
         cos, sin = self.rotary.tables(T, x.device, x.dtype)
         if self.gradient_checkpointing and self.training:
+            no_wgrad_deferral_this_window()  # keep checkpointing's memory saving (ops/linear.py)
             for layer in self.layers:
                 x = torch.utils.checkpoint.checkpoint(layer, x, cos, sin, use_reentrant=False)
             return self.norm(x)

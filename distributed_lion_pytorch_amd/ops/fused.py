@@ -435,6 +435,10 @@ class _MLP(torch.autograd.Function):
         ctx.save_for_backward(x, z, h, w_fc, b_fc, w_proj)
         ctx.exact = exact
         ctx.fuse = (_fuse_target(w_fc), _fuse_target(w_proj))
+        # deposit targets: the Parameter objects themselves -- under non-reentrant
+        # activation checkpointing ctx.saved_tensors hands back recomputed
+        # aliases, and a .grad set on an alias is lost
+        ctx.wparams = (w_fc, w_proj)
         ctx.fused_b = _fused_params(b_fc)[0]
         wp_t = transposed_weight(w_proj) if isinstance(w_proj, torch.nn.Parameter) else w_proj.t()
         return F.linear(h, wp_t)
@@ -452,7 +456,7 @@ class _MLP(torch.autograd.Function):
         grads = [None] * 5
         if ctx.needs_input_grad[0]:
             grads[0] = F.linear(dz, w_fc)  # dx = dz . Wfc^T, Wfc stored [C, 4C]
-        for i, (w, a, g) in ((1, (w_fc, x, dz)), (3, (w_proj, h, dy))):
+        for i, (w, a, g) in ((1, (ctx.wparams[0], x, dz)), (3, (ctx.wparams[1], h, dy))):
             if ctx.needs_input_grad[i]:
                 if ctx.fuse[(i - 1) // 2]:
                     wgrad_into(a, g, w)
@@ -634,6 +638,7 @@ class _QKVAttention(torch.autograd.Function):
         ctx.save_for_backward(x2d, w, qkv, out, lse)
         ctx.p, ctx.seed = p, seed
         ctx.fuse = _fuse_target(w)
+        ctx.wparam = w  # deposit target (see _MLP: saved tensors may be checkpoint aliases)
         ctx.fused_b = _fused_params(b)[0]
         return out.view(B, T, H * D)
 
@@ -653,7 +658,7 @@ class _QKVAttention(torch.autograd.Function):
         dw = db = None
         if ctx.needs_input_grad[1]:
             if ctx.fuse:
-                wgrad_into(x2d, g, w)
+                wgrad_into(x2d, g, ctx.wparam)
             else:
                 dw = wgrad(x2d, g)
         if ctx.needs_input_grad[2]:
@@ -791,6 +796,7 @@ class _LoraAdd(torch.autograd.Function):
         ctx.save_for_backward(x, u, a, b)
         ctx.s, ctx.p, ctx.seed = s, p, seed
         ctx.fuse = (_fuse_target(a), _fuse_target(b))
+        ctx.abparams = (a, b)  # deposit targets (see _MLP: saved tensors may be checkpoint aliases)
         return out
 
     @staticmethod
@@ -802,12 +808,12 @@ class _LoraAdd(torch.autograd.Function):
         ga = gb = dx = None
         if ctx.needs_input_grad[3]:
             part_b, _ = ops.lora_cols(dout, u, None, ctx.s, 0.0, 0)
-            gb = _lora_weight_grad(b, part_b.view(part_b.shape[0], -1), ctx.fuse[1])
+            gb = _lora_weight_grad(ctx.abparams[1], part_b.view(part_b.shape[0], -1), ctx.fuse[1])
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             du = ops.lora_rows(dout, b.t().contiguous(), ctx.s, 0.0, 0)
             part_a, dx = ops.lora_cols(x, du, a, 1.0, ctx.p, ctx.seed)
             if ctx.needs_input_grad[2]:
-                ga = _lora_weight_grad(a, part_a.view(part_a.shape[0], -1), ctx.fuse[0])
+                ga = _lora_weight_grad(ctx.abparams[0], part_a.view(part_a.shape[0], -1), ctx.fuse[0])
         return dout if ctx.needs_input_grad[0] else None, dx, ga, gb, None, None, None
 
 

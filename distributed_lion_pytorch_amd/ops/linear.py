@@ -64,7 +64,7 @@ import weakref
 
 import torch
 
-_FUSE_ACCUM = {"on": False, "multi": True}
+_FUSE_ACCUM = {"on": False, "multi": True, "nodefer": False}
 _ACC_BUDGET = (8 << 30) if os.environ.get("DLION_SPLITK_ACC", "1") != "0" else 0  # bytes of fp32 accumulators
 _ACC: dict = {}  # key -> [weakrefs of params, fp32 buffer [S, ...], [(param ref, col0, ncols)]]
 _PENDING: list = []  # keys written in the current window, in order
@@ -97,6 +97,7 @@ def grad_accumulation_fusion(enabled: bool = True, micro_batches: int | None = N
             _PENDING.clear()
             _clear_deferred()
             _drop_deferred()
+            _FUSE_ACCUM["nodefer"] = False
 
 
 def begin_fusion_window(micro_batches: int | None = None) -> bool:
@@ -122,10 +123,20 @@ def end_fusion_window(flush: bool = True) -> None:
     _PENDING.clear()
     _clear_deferred()
     _drop_deferred()
+    _FUSE_ACCUM["nodefer"] = False
 
 
 def fusion_window_open() -> bool:
     return bool(_FUSE_ACCUM["on"])
+
+
+def no_wgrad_deferral_this_window() -> None:
+    """Called by activation-checkpointed forwards: keeping every micro-batch's
+    layer inputs alive until the window's exit would undo the checkpointing's
+    memory saving, so this window computes its weight gradients per
+    micro-batch (into the fp32 accumulators) instead."""
+    if _FUSE_ACCUM["on"]:
+        _FUSE_ACCUM["nodefer"] = True
 
 
 def _flush_entry(ent) -> None:
@@ -175,7 +186,7 @@ def _drop_deferred() -> None:
 def _defer_wgrad(params, cols, a, b, s) -> bool:
     """Keep a^T b's operands for one window-level GEMM (see the module notes).
     False if not applicable (fallback: _acc_gemm now)."""
-    if not (_WDEFER_ON and _FUSE_ACCUM["multi"]):
+    if not (_WDEFER_ON and _FUSE_ACCUM["multi"]) or _FUSE_ACCUM["nodefer"]:
         return False
     key = tuple(id(p) for p in params)
     nb = a.numel() * a.element_size() + b.numel() * b.element_size()
@@ -320,7 +331,7 @@ def wgrad_splits(a: torch.Tensor, b: torch.Tensor) -> tuple:
     M, R, C = a.shape[0], a.shape[1], b.shape[1]
     # small outputs: hipBLASLt per micro-batch, but the own kernel when the
     # window defers the GEMM (attn c_proj over 8 micro-batches: 29 vs 43 us/mb)
-    deferred = _WDEFER_ON and _FUSE_ACCUM["on"] and _FUSE_ACCUM["multi"]
+    deferred = _WDEFER_ON and _FUSE_ACCUM["on"] and _FUSE_ACCUM["multi"] and not _FUSE_ACCUM["nodefer"]
     if ((deferred or math.ceil(R / 256) * math.ceil(C / 256) >= _TN_MIN_TILES) and _tn_eligible(a, b)
             and hip.available()):
         return tn_split_factor(M, R, C), True

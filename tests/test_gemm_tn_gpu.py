@@ -92,3 +92,47 @@ def test_window_wgrad_deferral_edge_cases(cuda, monkeypatch, case):
     ref = sum(x.float().t() @ g.float() for x, g in zip(xs, gs))
     err = (w.grad.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 8e-3, err
+
+
+def test_checkpointed_model_skips_wgrad_deferral(cuda, monkeypatch):
+    """Activation checkpointing + a multi-micro-batch window: the layer inputs
+    are not kept for a window-level GEMM (that would undo the checkpointing's
+    memory saving); the gradients equal the non-checkpointed deferred run's."""
+    from distributed_lion_pytorch_amd.models.gpt2 import GPT2LMHeadModel, gpt2_config
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    torch.manual_seed(5)
+    cfg = gpt2_config("gpt2-tiny")
+    cfg.resid_pdrop = cfg.embd_pdrop = cfg.attn_pdrop = 0.0
+    model = GPT2LMHeadModel(cfg).to(cuda, torch.bfloat16)
+    batches = [torch.randint(0, cfg.vocab_size, (2, 128), device=cuda) for _ in range(3)]
+    kept = []
+    orig = L._defer_wgrad
+
+    def spy(*args):
+        r = orig(*args)
+        kept.append(r)
+        return r
+
+    monkeypatch.setattr(L, "_defer_wgrad", spy)
+
+    def run(ckpt):
+        if ckpt:
+            model.gradient_checkpointing_enable()
+        else:
+            model.gradient_checkpointing_disable()
+        model.zero_grad(set_to_none=True)
+        kept.clear()
+        with L.grad_accumulation_fusion(True, micro_batches=len(batches)):
+            for ids in batches:
+                model(input_ids=ids, labels=ids).loss.backward()
+        return any(kept), {n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None}
+
+    kept_plain, g_plain = run(False)
+    kept_ckpt, g_ckpt = run(True)
+    assert kept_plain and not kept_ckpt
+    assert set(g_plain) == set(g_ckpt)
+    for n in g_plain:
+        err = (g_ckpt[n] - g_plain[n]).abs().max().item() / max(g_plain[n].abs().max().item(), 1e-6)
+        assert err < 3e-2, n

@@ -104,3 +104,28 @@ def test_lora_fusion_window_deposits(cuda):
     assert set(g_plain) == set(g_fused)
     for n in g_plain:
         assert _rel(g_fused[n], g_plain[n]) < 3e-2, n
+
+
+def test_lora_grads_reach_parameters_under_checkpointing(cuda):
+    """Activation checkpointing (the DPO preset) + a fusion window: the adapter
+    gradients must land on the Parameter objects, not on the recomputed
+    aliases that ctx.saved_tensors returns under non-reentrant checkpointing."""
+    hip.require()
+    model = _tiny_llama(cuda)
+    batches = [torch.randint(0, 512, (2, 128), device=cuda) for _ in range(2)]
+
+    def run(ckpt):
+        if ckpt:
+            model.gradient_checkpointing_enable()
+        else:
+            model.gradient_checkpointing_disable()
+        model.zero_grad(set_to_none=True)
+        with L.grad_accumulation_fusion(True, micro_batches=len(batches)):
+            for ids in batches:
+                model(input_ids=ids, labels=ids).loss.backward()
+        return {n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None}
+
+    g_plain, g_ckpt = run(False), run(True)
+    assert set(g_plain) == set(g_ckpt) and any("lora_A" in n for n in g_ckpt)
+    for n in g_plain:
+        assert _rel(g_ckpt[n], g_plain[n]) < 3e-2, n
