@@ -402,6 +402,30 @@ void sum_partials_acc_(const Tensor& part, const Tensor& out) {
             "sum_partials_acc_");
 }
 
+// out (+)= bf16(sum of every row of every stack in `parts`) -- a fusion window's per-micro-batch
+// partial stacks reduced in one kernel, no concatenation
+void sum_partials_multi_(at::TensorList parts, const Tensor& out, bool accumulate) {
+  TORCH_CHECK(!parts.empty() && parts.size() <= 16, "dlion: 1..16 partial stacks");
+  std::vector<const float*> ptrs;
+  std::vector<int64_t> rows, lds;
+  int64_t n = -1;
+  for (const auto& t : parts) {
+    const auto P = partials(t);
+    TORCH_CHECK(n < 0 || P.n == n, "dlion: partial stacks must have the same row length");
+    n = P.n;
+    ptrs.push_back(P.ptr);
+    rows.push_back(P.S);
+    lds.push_back(P.ld);
+  }
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kBFloat16 && out.is_contiguous() && out.numel() == n,
+              "dlion: target must be a contiguous bf16 tensor of the partial row size");
+  TORCH_CHECK(n % 4 == 0, "dlion: partial row length must be a multiple of 4");
+  const c10::DeviceGuard g(out.device());
+  check_hip(dlion::launch_sum_partials_multi(ptrs.data(), rows.data(), lds.data(), static_cast<int>(parts.size()), n,
+                                             out.data_ptr(), accumulate, cur_stream()),
+            "sum_partials_multi_");
+}
+
 // out (+)= bf16(s[0] * sum_s part[s]): the LM head's split-K weight gradient scaled by the
 // loss gradient (a device scalar) and accumulated into .grad in one pass
 void sum_partials_scaled_(const Tensor& part, const Tensor& s, const Tensor& out, bool accumulate) {
@@ -878,6 +902,7 @@ TORCH_LIBRARY(dlion, m) {
   m.def("sum_partials(Tensor part) -> Tensor");
   m.def("sum_partials_acc_(Tensor part, Tensor(a!) out) -> ()");
   m.def("sum_partials_scaled_(Tensor part, Tensor s, Tensor(a!) out, bool accumulate) -> ()");
+  m.def("sum_partials_multi_(Tensor[] parts, Tensor(a!) out, bool accumulate) -> ()");
   m.def("colsum_partials(Tensor x, int parts) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float p, int seed) -> (Tensor, Tensor)");
   m.def(
@@ -918,6 +943,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("sum_partials", &sum_partials);
   m.impl("sum_partials_acc_", &sum_partials_acc_);
   m.impl("sum_partials_scaled_", &sum_partials_scaled_);
+  m.impl("sum_partials_multi_", &sum_partials_multi_);
   m.impl("colsum_partials", &colsum_partials);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);

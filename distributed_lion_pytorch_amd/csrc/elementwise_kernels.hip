@@ -298,6 +298,54 @@ __global__ void __launch_bounds__(kTallQ * kTallR) sum_partials_tall_kernel(cons
   }
 }
 
+// The tall reduction over up to kMaxPartSeg separately allocated stacks (the
+// per-micro-batch partials a fusion window keeps): no concatenation copy.
+constexpr int kMaxPartSeg = 16;
+struct PartSegs {
+  const float* ptr[kMaxPartSeg];
+  int64_t rows[kMaxPartSeg];
+  int64_t ld4[kMaxPartSeg];  // row stride in float4 units
+  int nseg;
+};
+template <bool ACC>
+__global__ void __launch_bounds__(kTallQ * kTallR) sum_partials_multi_kernel(const PartSegs sg, int64_t n,
+                                                                            uint16_t* __restrict__ out) {
+  __shared__ float4 red[kTallR][kTallQ];
+  const int q = threadIdx.x % kTallQ, r = threadIdx.x / kTallQ;
+  const int64_t col4 = static_cast<int64_t>(blockIdx.x) * kTallQ + q;
+  const int64_t n4 = n / 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col4 < n4) {
+    for (int k = 0; k < sg.nseg; ++k) {
+      const float4* p = reinterpret_cast<const float4*>(sg.ptr[k]) + col4;
+      for (int64_t s = r; s < sg.rows[k]; s += kTallR) {
+        const float4 v = p[s * sg.ld4[k]];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+  }
+  red[r][q] = acc;
+  __syncthreads();
+  if (r == 0 && col4 < n4) {
+#pragma unroll 8
+    for (int i = 1; i < kTallR; ++i) {
+      const float4 v = red[i][q];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    if constexpr (ACC) {
+      const uint2 o = reinterpret_cast<const uint2*>(out)[col4];
+      acc.x += bf16_to_f32(o.x & 0xffffu);
+      acc.y += bf16_to_f32(o.x >> 16);
+      acc.z += bf16_to_f32(o.y & 0xffffu);
+      acc.w += bf16_to_f32(o.y >> 16);
+    }
+    uint2 w;
+    w.x = static_cast<uint32_t>(f32_to_bf16(acc.x)) | (static_cast<uint32_t>(f32_to_bf16(acc.y)) << 16);
+    w.y = static_cast<uint32_t>(f32_to_bf16(acc.z)) | (static_cast<uint32_t>(f32_to_bf16(acc.w)) << 16);
+    reinterpret_cast<uint2*>(out)[col4] = w;
+  }
+}
+
 static inline int grid_for(int64_t work, int64_t per_block) {
   int64_t g = (work + per_block - 1) / per_block;
   if (g > 2048) g = 2048;
@@ -401,6 +449,26 @@ hipError_t launch_sum_partials(const float* part, int S, int64_t n, int64_t ld, 
   const dim3 g(grid_for(n / 4, 256)), blk(256);
   if (accumulate) hipLaunchKernelGGL(sum_partials_kernel<true>, g, blk, 0, st, part, S, n, ld, O, scale);
   else hipLaunchKernelGGL(sum_partials_kernel<false>, g, blk, 0, st, part, S, n, ld, O, scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_sum_partials_multi(const float* const* ptrs, const int64_t* rows, const int64_t* lds, int nseg,
+                                     int64_t n, void* out, bool accumulate, hipStream_t st) {
+  if (nseg < 1 || nseg > kMaxPartSeg || n % 4 != 0) return hipErrorInvalidValue;
+  PartSegs sg{};
+  for (int k = 0; k < nseg; ++k) {
+    if (lds[k] % 4 != 0 || lds[k] < n || reinterpret_cast<uintptr_t>(ptrs[k]) % 16 != 0) return hipErrorInvalidValue;
+    sg.ptr[k] = ptrs[k];
+    sg.rows[k] = rows[k];
+    sg.ld4[k] = lds[k] / 4;
+  }
+  sg.nseg = nseg;
+  const int64_t blocks = (n / 4 + kTallQ - 1) / kTallQ;
+  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  const dim3 g(static_cast<unsigned>(blocks)), blk(kTallQ * kTallR);
+  auto O = static_cast<uint16_t*>(out);
+  if (accumulate) hipLaunchKernelGGL(sum_partials_multi_kernel<true>, g, blk, 0, st, sg, n, O);
+  else hipLaunchKernelGGL(sum_partials_multi_kernel<false>, g, blk, 0, st, sg, n, O);
   return hipGetLastError();
 }
 

@@ -54,6 +54,9 @@ hipError_t launch_rope(const void* x, const void* cos, const void* sin, void* y,
 hipError_t launch_sum_partials(const float* part, int S, int64_t n, int64_t ld, void* out, bool accumulate,
                                hipStream_t st, const float* scale = nullptr);
 hipError_t launch_colsum(const void* x, float* part, int parts, int64_t rows, int N, hipStream_t st);
+// out (+)= bf16(sum over every row of up to 16 fp32 stacks [rows_k, >= n] (row stride lds_k))
+hipError_t launch_sum_partials_multi(const float* const* ptrs, const int64_t* rows, const int64_t* lds, int nseg,
+                                     int64_t n, void* out, bool accumulate, hipStream_t st);
 
 // ---- bf16 GEMM C[M,N] = A[M,K] . B[N,K]^T with fused epilogue (gemm.hip)
 // epi: 0 plain, 1 + bias, 2 aux = z, C = gelu_tanh(z + bias), 3 the same with erf GELU,

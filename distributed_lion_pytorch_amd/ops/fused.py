@@ -226,7 +226,9 @@ def _deposit_joint(params, part2d, C) -> bool:
     such boundaries per micro-batch: 50 fewer ~9 us launches."""
     gs = [p.grad for p in params]
     if all(g is None for g in gs):
-        buf = hip.ops().sum_partials(part2d)  # bf16 [k*C], fresh
+        from .linear import sum_partials_into
+
+        buf = sum_partials_into(part2d)  # bf16 [k*C], fresh
         for j, p in enumerate(params):
             p.grad = buf[j * C:(j + 1) * C].view_as(p)
         return True
@@ -237,7 +239,9 @@ def _deposit_joint(params, part2d, C) -> bool:
         if (g.data_ptr() != g0.data_ptr() + j * C * g0.element_size()
                 or g.untyped_storage().data_ptr() != g0.untyped_storage().data_ptr()):
             return False
-    hip.ops().sum_partials_acc_(part2d, g0.as_strided((len(gs) * C,), (1,)))
+    from .linear import sum_partials_into
+
+    sum_partials_into(part2d, g0.as_strided((len(gs) * C,), (1,)), accumulate=True)
     return True
 
 

@@ -30,6 +30,13 @@ def main():
         own = bench(lambda: ops.gemm_nt(a, b, bb), n=5 if N > 10000 else 20)
         lt = bench(lambda: torch.nn.functional.linear(a, b, bb), n=5 if N > 10000 else 20)
         print(f"{name:24s} N={N:6d}  own {own:8.1f} us   hipBLASLt {lt:8.1f} us   own/lt {own / lt:5.2f}")
+    # the K = 2304 / 3072 GEMMs (N = 768): MLP down-projection forward, c_fc and c_attn input gradients
+    for name, K in (("mlp proj fwd / fc dgrad", 3072), ("c_attn dgrad", 2304)):
+        a = torch.randn(M, K, device="cuda").bfloat16()
+        b = (torch.randn(768, K, device="cuda") / K ** 0.5).bfloat16()
+        own = bench(lambda: ops.gemm_nt(a, b, None))
+        lt = bench(lambda: torch.nn.functional.linear(a, b))
+        print(f"{name:24s} K={K:6d}  own {own:8.1f} us   hipBLASLt {lt:8.1f} us   own/lt {own / lt:5.2f}")
 
 
 if __name__ == "__main__":
