@@ -744,6 +744,22 @@ Tensor gemm_nt_stamped(const Tensor& a, const Tensor& b, const Tensor& stamps) {
 
 // dz = (a . b^T) * gelu'(z + bias) -> (dz [M, N] bf16, part [2 * ceil(M/256), N] fp32 bias-grad partials):
 // the MLP down-projection's input gradient fused with the bias+GELU backward
+// (h, d) = (gelu(a . b^T + bias), gelu'(a . b^T + bias)) in one GEMM drain (EPI 6 / 7)
+std::tuple<Tensor, Tensor> gemm_nt_gelu_d(const Tensor& a, const Tensor& b, const Tensor& bias, bool exact) {
+  auto h = at::empty({a.size(0), b.size(0)}, a.options());
+  auto d = at::empty({a.size(0), b.size(0)}, a.options());
+  gemm_nt_launch(a, b, h, &bias, &d, exact ? 7 : 6);
+  return {h, d};
+}
+
+// (dz, part) = (bf16(a . b^T) * d, fp32 [2 * ceil(M/256), N] column-sum partials of dz) (EPI 8)
+std::tuple<Tensor, Tensor> gemm_nt_dmul(const Tensor& a, const Tensor& b, const Tensor& d) {
+  auto dz = at::empty({a.size(0), b.size(0)}, a.options());
+  auto part = at::empty({2 * ((a.size(0) + 255) / 256), b.size(0)}, a.options().dtype(at::kFloat));
+  gemm_nt_launch(a, b, dz, nullptr, &d, 8, &part);
+  return {dz, part};
+}
+
 std::tuple<Tensor, Tensor> gemm_nt_dgelu(const Tensor& a, const Tensor& b, const Tensor& bias, const Tensor& z,
                                          bool exact) {
   auto dz = at::empty({a.size(0), b.size(0)}, a.options());
@@ -876,6 +892,8 @@ TORCH_LIBRARY(dlion, m) {
   m.def("lora_up(Tensor o, Tensor u, Tensor b, float s) -> Tensor");
   m.def("lora_cols(Tensor g, Tensor y, Tensor? a, float yscale, float p, int seed) -> (Tensor, Tensor)");
   m.def("gemm_nt_dgelu(Tensor a, Tensor b, Tensor bias, Tensor z, bool exact) -> (Tensor, Tensor)");
+  m.def("gemm_nt_gelu_d(Tensor a, Tensor b, Tensor bias, bool exact) -> (Tensor, Tensor)");
+  m.def("gemm_nt_dmul(Tensor a, Tensor b, Tensor d) -> (Tensor, Tensor)");
   m.def("gemm_nt_stamped(Tensor a, Tensor b, Tensor(a!) stamps) -> Tensor");
   m.def("embed_fwd(Tensor ids, Tensor wte, Tensor wpe, float p, int seed) -> Tensor");
   m.def(
@@ -954,6 +972,8 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("gemm_nt_out", &gemm_nt_out);
   m.impl("gemm_nt_gelu", &gemm_nt_gelu);
   m.impl("gemm_nt_dgelu", &gemm_nt_dgelu);
+  m.impl("gemm_nt_gelu_d", &gemm_nt_gelu_d);
+  m.impl("gemm_nt_dmul", &gemm_nt_dmul);
   m.impl("gemm_nt_stamped", &gemm_nt_stamped);
   m.impl("embed_fwd", &embed_fwd);
   m.impl("embed_bwd_", &embed_bwd_);

@@ -165,6 +165,21 @@ __device__ __forceinline__ float gelu_grad(float u, bool exact) {
   return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * kSqrt2OverPi * (1.f + 3.f * kKappa * u2);
 }
 
+// gelu(u) and gelu'(u) from one tanh / erf (the GEMM's GELU epilogue that
+// stores the derivative for the backward instead of the pre-activation)
+__device__ __forceinline__ void gelu_and_grad(float u, bool exact, float& g, float& dg) {
+  if (exact) {
+    const float e = erff(u * kInvSqrt2);
+    g = 0.5f * u * (1.f + e);
+    dg = 0.5f * (1.f + e) + u * kInvSqrt2Pi * __expf(-0.5f * u * u);
+    return;
+  }
+  const float u2 = u * u;
+  const float t = fast_tanh(kSqrt2OverPi * (u + kKappa * u2 * u));
+  g = 0.5f * u * (1.f + t);
+  dg = 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * kSqrt2OverPi * (1.f + 3.f * kKappa * u2);
+}
+
 // ------------------------------------------------------------ vote counting
 // Spread the 8 bits of a byte into the 8 bytes of a u64 (bit j -> bit 8j), so
 // that summing spread bytes over W <= 255 ranks counts 8 votes in parallel.

@@ -354,10 +354,13 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
       // per-lane value -> a vector store; lane i of wave 0 writes stamp i
       if (tid < 8) g.stamps[static_cast<int64_t>(blockIdx.x) * 8 + tid] = tid < 7 ? st_[tid < 7 ? tid : 0] : 0ull;
     }
-  } else if constexpr (EPI <= 3) {
+  } else if constexpr (EPI <= 3 || EPI == 6 || EPI == 7) {
     // EPI 2/3: aux = z (bf16, no bias); C = gelu(z + b) evaluated on the ROUNDED z
     // exactly like the unfused GEMM -> bias_gelu path (3: erf GELU).  The GELU
     // runs in the drain, 8 columns per lane (one bias chunk per lane).
+    // EPI 6/7: the same C, but aux = bf16(gelu'(z + b)) -- the derivative the
+    // backward needs, from the same tanh/erf -- so the backward's drain is one
+    // multiply instead of a GELU derivative per element (EPI 8).
     park([&](float v, int, int) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(v)); });
     float b8[8];
     if (gn < g.N) {
@@ -372,12 +375,24 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
       const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((ch ^ (row & 7)) << 4));
       const int gm = row_base + row;
       if (gm < g.M && gn < g.N) {
-        *reinterpret_cast<uint4*>(g.aux + (int64_t)gm * g.ldaux + gn) = v;
         float z[8];
         Elem<kBF16>::load8(reinterpret_cast<const uint16_t*>(&v), z);
         bf16x8 hb;
+        if constexpr (EPI <= 3) {
+          *reinterpret_cast<uint4*>(g.aux + (int64_t)gm * g.ldaux + gn) = v;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) hb[j] = static_cast<__bf16>(gelu_f(z[j] + b8[j], EPI == 3));
+          for (int j = 0; j < 8; ++j) hb[j] = static_cast<__bf16>(gelu_f(z[j] + b8[j], EPI == 3));
+        } else {
+          bf16x8 db;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float gv, dgv;
+            gelu_and_grad(z[j] + b8[j], EPI == 7, gv, dgv);
+            hb[j] = static_cast<__bf16>(gv);
+            db[j] = static_cast<__bf16>(dgv);
+          }
+          *reinterpret_cast<bf16x8*>(g.aux + (int64_t)gm * g.ldaux + gn) = db;
+        }
         *reinterpret_cast<bf16x8*>(g.C + (int64_t)gm * g.ldc + gn) = hb;
       }
     }
@@ -402,7 +417,7 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
     float b8[8], cs[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) cs[j] = 0.f;
-    if (gn < g.N) {
+    if (EPI != 8 && gn < g.N) {
       Elem<kBF16>::load8(g.bias + gn, b8);
     } else {
 #pragma unroll
@@ -420,7 +435,11 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
         bf16x8 ob;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          o[j] = gv[j] * gelu_grad(z[j] + b8[j], EPI == 5);
+          if constexpr (EPI == 8) {
+            o[j] = gv[j] * z[j];  // aux holds gelu'(z + b) already (EPI 6/7 forward)
+          } else {
+            o[j] = gv[j] * gelu_grad(z[j] + b8[j], EPI == 5);
+          }
           ob[j] = static_cast<__bf16>(o[j]);  // v_cvt_pk_bf16_f32 (RNE)
           cs[j] += static_cast<float>(ob[j]);  // the bias gradient sums the stored bf16 values
         }
@@ -471,8 +490,10 @@ hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* 
   if (K % 128 != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 8 != 0) return hipErrorInvalidValue;
   if ((int64_t)M * lda >= (1ll << 31) || (int64_t)N * ldb >= (1ll << 31)) return hipErrorInvalidValue;
   if (epi >= 2 && (aux == nullptr || ldaux % 8 != 0)) return hipErrorInvalidValue;
-  if (epi >= 1 && (bias == nullptr || reinterpret_cast<uintptr_t>(bias) % 16 != 0)) return hipErrorInvalidValue;
-  if (epi >= 4 && (part == nullptr || reinterpret_cast<uintptr_t>(part) % 16 != 0)) return hipErrorInvalidValue;
+  if (epi >= 1 && epi != 8 && (bias == nullptr || reinterpret_cast<uintptr_t>(bias) % 16 != 0))
+    return hipErrorInvalidValue;
+  if ((epi == 4 || epi == 5 || epi == 8) && (part == nullptr || reinterpret_cast<uintptr_t>(part) % 16 != 0))
+    return hipErrorInvalidValue;
   GemmArgs g;
   g.A = static_cast<const uint16_t*>(A);
   g.B = static_cast<const uint16_t*>(B);
@@ -497,6 +518,9 @@ hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* 
     case 3: hipLaunchKernelGGL(gemm_nt_kernel<3>, grid, block, 0, st, g); break;
     case 4: hipLaunchKernelGGL(gemm_nt_kernel<4>, grid, block, 0, st, g); break;
     case 5: hipLaunchKernelGGL(gemm_nt_kernel<5>, grid, block, 0, st, g); break;
+    case 6: hipLaunchKernelGGL(gemm_nt_kernel<6>, grid, block, 0, st, g); break;
+    case 7: hipLaunchKernelGGL(gemm_nt_kernel<7>, grid, block, 0, st, g); break;
+    case 8: hipLaunchKernelGGL(gemm_nt_kernel<8>, grid, block, 0, st, g); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -61,7 +61,9 @@ hipError_t launch_sum_partials_multi(const float* const* ptrs, const int64_t* ro
 // ---- bf16 GEMM C[M,N] = A[M,K] . B[N,K]^T with fused epilogue (gemm.hip)
 // epi: 0 plain, 1 + bias, 2 aux = z, C = gelu_tanh(z + bias), 3 the same with erf GELU,
 // 4 C = bf16(A.B^T) * gelu_tanh'(aux + bias) with aux an input and part [2 * ceil(M/256)][N]
-// fp32 column sums of C (bias gradient partials), 5 the same with erf GELU.
+// fp32 column sums of C (bias gradient partials), 5 the same with erf GELU; 6 / 7 as 2 / 3 but
+// aux = bf16(gelu'(z + bias)) (output); 8 C = bf16(A.B^T) * aux with aux that derivative (input)
+// and the part column sums of 4 (no bias).
 // Needs K % 128 == 0, N % 8 == 0, leading dims % 8 == 0.
 hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
                           void* aux, int ldaux, int M, int N, int K, int epi, float* part, hipStream_t st);

@@ -399,6 +399,7 @@ def linear_gelu(x2d: torch.Tensor, w_in_out: torch.Tensor, bias: torch.Tensor, e
 
 _DGELU_FUSED = os.environ.get("DLION_DGELU_GEMM", "1") != "0"  # A/B switch: fused DGELU backward GEMM
 _GELU_FUSED = os.environ.get("DLION_GELU_GEMM", "1") != "0"  # A/B switch: fused GELU forward GEMM
+_GELU_DSTORE = os.environ.get("DLION_GELU_DSTORE", "1") != "0"  # A/B switch: store gelu' instead of z
 
 
 def _own_gemm_ok(a: torch.Tensor, b_nk: torch.Tensor) -> bool:
@@ -431,8 +432,18 @@ class _MLP(torch.autograd.Function):
         from .linear import _fuse_target, transposed_weight
 
         wfc_t = transposed_weight(w_fc) if isinstance(w_fc, torch.nn.Parameter) else w_fc.t().contiguous()
+        # the backward's fused DGELU GEMM will run (dy [M, C] against w_proj [4C, C]):
+        # store gelu'(z + b) instead of z (EPI 6/7 -> EPI 8, one multiply per element
+        # in the backward drain instead of a GELU derivative)
+        bwd_own = (_DGELU_FUSED and w_proj.is_contiguous() and w_proj.shape[1] % 128 == 0
+                   and w_proj.shape[0] % 8 == 0 and x.shape[0] * w_proj.shape[1] < 2 ** 31)
+        ctx.dstored = False
         if _GELU_FUSED and _own_gemm_ok(x, wfc_t):
-            h, z = hip.ops().gemm_nt_gelu(x, wfc_t, b_fc, exact)
+            if bwd_own and _GELU_DSTORE:
+                h, z = hip.ops().gemm_nt_gelu_d(x, wfc_t, b_fc, exact)  # z <- gelu'(z + b)
+                ctx.dstored = True
+            else:
+                h, z = hip.ops().gemm_nt_gelu(x, wfc_t, b_fc, exact)
         else:
             z = F.linear(x, wfc_t)
             h = hip.ops().bias_gelu_fwd(z, b_fc, exact)
@@ -453,7 +464,10 @@ class _MLP(torch.autograd.Function):
 
         x, z, h, w_fc, b_fc, w_proj = ctx.saved_tensors
         dy = dy.contiguous()
-        if _DGELU_FUSED and _own_gemm_ok(dy, w_proj):
+        if ctx.dstored:  # z holds gelu'(z + b)
+            assert _own_gemm_ok(dy, w_proj)
+            dz, part = hip.ops().gemm_nt_dmul(dy, w_proj, z)
+        elif _DGELU_FUSED and _own_gemm_ok(dy, w_proj):
             dz, part = hip.ops().gemm_nt_dgelu(dy, w_proj, b_fc, z, ctx.exact)
         else:
             dz, part = hip.ops().bias_gelu_bwd(dy @ w_proj.t(), z, b_fc, ctx.exact, max(1, min(1024, z.shape[0] // 8)))

@@ -38,11 +38,35 @@ def test_gemm_nt_dgelu(M, N, K, exact, cuda):
     assert _rel(part.sum(0), ref.sum(0)) < 1e-2
 
 
-@pytest.mark.parametrize("fused_fwd,fused_bwd", [(True, True), (False, False), (True, False), (False, True)])
-def test_mlp_gelu_grads(fused_fwd, fused_bwd, cuda, monkeypatch):
+@pytest.mark.parametrize("M,N,K", [(512, 1024, 256), (300, 520, 128)])
+@pytest.mark.parametrize("exact", [False, True])
+def test_gemm_nt_gelu_derivative_store_and_multiply(M, N, K, exact, cuda):
+    """EPI 6/7 (h = gelu(z + b), d = gelu'(z + b) from one tanh/erf) and EPI 8
+    (dz = bf16(dy . w^T) * d with bias-gradient partials) against fp32."""
+    hip.require()
+    torch.manual_seed(M + K)
+    x = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=cuda).to(torch.bfloat16)
+    h, d = hip.ops().gemm_nt_gelu_d(x, w, b, exact)
+    z = (x.float() @ w.float().t()).bfloat16().float() + b.float()  # the GEMM output is rounded to bf16 first
+    assert _rel(h, F.gelu(z, approximate="none" if exact else "tanh")) < 1e-2
+    assert _rel(d, _gelu_grad(z, exact)) < 1e-2
+    dy = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w2 = (torch.randn(N, K, device=cuda) / K ** 0.5).to(torch.bfloat16)
+    dz, part = hip.ops().gemm_nt_dmul(dy, w2, d)
+    ref = (dy.float() @ w2.float().t()).bfloat16().float() * d.float()
+    assert _rel(dz, ref) < 1e-2
+    assert _rel(part.sum(0), ref.sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("fused_fwd,fused_bwd,dstore", [(True, True, True), (True, True, False), (False, False, True),
+                                                         (True, False, True), (False, True, True)])
+def test_mlp_gelu_grads(fused_fwd, fused_bwd, dstore, cuda, monkeypatch):
     hip.require()
     monkeypatch.setattr(fused, "_GELU_FUSED", fused_fwd)
     monkeypatch.setattr(fused, "_DGELU_FUSED", fused_bwd)
+    monkeypatch.setattr(fused, "_GELU_DSTORE", dstore)
     torch.manual_seed(3)
     M, C, F4 = 512, 256, 1024
     x = torch.randn(M, C, device=cuda).to(torch.bfloat16).requires_grad_(True)
