@@ -90,6 +90,8 @@ def parse():
     ap.add_argument("--impl", default="native", choices=["native", "reference"])
     ap.add_argument("--fused", default="auto", choices=["auto", "torch", "hip"])
     ap.add_argument("--dropout", type=float, default=None, help="override GPT-2 dropout (default 0.1)")
+    ap.add_argument("--load_in_4bit", action="store_true",
+                    help="frozen base weights in 4-bit NF4 (the reference's bitsandbytes base, models/quant.py)")
     ap.add_argument("--profile_dir", default=None)
     ap.add_argument("--rocm_fa", default=None, help="PyTorch SDPA flash library on ROCm: ck | aotriton")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -140,6 +142,13 @@ def build_native(args, dev):
         ref_model = copy.deepcopy(model).eval()
         for p in ref_model.parameters():
             p.requires_grad_(False)
+    if args.load_in_4bit:
+        from distributed_lion_pytorch_amd.models.quant import QuantConfig, quantize_model
+
+        quantize_model(model, QuantConfig(bnb_4bit_compute_dtype=torch.bfloat16))
+        if ref_model is not None:
+            quantize_model(ref_model, QuantConfig(bnb_4bit_compute_dtype=torch.bfloat16))
+        torch.cuda.empty_cache()
     if args.lora:
         from distributed_lion_pytorch_amd.models.lora import LoraConfig, inject_lora
 
@@ -198,6 +207,7 @@ def main():
     build = build_native if args.impl == "native" else build_reference
     model, opt, cfg = build(args, dev)
     n_params = sum({p.data_ptr(): p.numel() for p in model.parameters()}.values())
+    n_params += sum(m.in_features * m.out_features for m in model.modules() if hasattr(m, "qweight"))  # 4-bit bases
     n_train = sum({p.data_ptr(): p.numel() for p in model.parameters() if p.requires_grad}.values())
 
     if args.task == "dpo":
@@ -283,6 +293,7 @@ def main():
                 "model": f"{args.model} ({n_params / 1e6:.1f}M params)",
                 "trainable_params": n_train,
                 "lora": args.lora,
+                "base_weights": "nf4 (4-bit, frozen)" if args.load_in_4bit else "bf16",
                 "global_batch": world * args.grad_accum * args.micro_batch,
                 "task": args.task,
                 "micro_batch": args.micro_batch,

@@ -883,9 +883,47 @@ std::tuple<Tensor, Tensor> lora_cols(const Tensor& g, const Tensor& y, const std
   return {part, dx};
 }
 
+
+// 4-bit blockwise quantization (quant.hip): w (any float dtype, numel % 64 == 0) -> (q uint8 [n/2], absmax fp32 [n/64])
+std::tuple<Tensor, Tensor> quant4(const Tensor& w, const Tensor& code) {
+  check_dev(w, "w");
+  check_dev(code, "code");
+  TORCH_CHECK(code.scalar_type() == at::kFloat && code.numel() == 16, "dlion quant4: code must be float32[16]");
+  const int64_t n = w.numel();
+  TORCH_CHECK(n % 64 == 0, "dlion quant4: numel must be a multiple of 64, got ", n);
+  const c10::DeviceGuard g(w.device());
+  auto q = at::empty({n / 2}, w.options().dtype(at::kByte));
+  auto absmax = at::empty({n / 64}, w.options().dtype(at::kFloat));
+  check_hip(dlion::launch_quant4(dtype_code(w.scalar_type()), w.data_ptr(), code.data_ptr<float>(),
+                                 q.data_ptr<uint8_t>(), absmax.data_ptr<float>(), n, cur_stream()),
+            "quant4");
+  return {q, absmax};
+}
+
+// out (contiguous, numel n = 2 * q.numel(), any float dtype) = code[q] * absmax
+void dequant4_(const Tensor& q, const Tensor& absmax, const Tensor& code, const Tensor& out) {
+  check_dev(q, "q");
+  check_dev(absmax, "absmax");
+  check_dev(code, "code");
+  check_dev(out, "out");
+  TORCH_CHECK(q.scalar_type() == at::kByte && absmax.scalar_type() == at::kFloat && code.scalar_type() == at::kFloat &&
+                  code.numel() == 16,
+              "dlion dequant4: q uint8, absmax / code float32");
+  const int64_t n = out.numel();
+  TORCH_CHECK(n % 64 == 0 && q.numel() == n / 2 && absmax.numel() == n / 64,
+              "dlion dequant4: out numel ", n, " does not match q ", q.numel(), " / absmax ", absmax.numel());
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "dlion dequant4: q and out must be 16-byte aligned");
+  const c10::DeviceGuard g(out.device());
+  check_hip(dlion::launch_dequant4(dtype_code(out.scalar_type()), q.data_ptr<uint8_t>(), absmax.data_ptr<float>(),
+                                   code.data_ptr<float>(), out.data_ptr(), n, cur_stream()),
+            "dequant4");
+}
 }  // namespace
 
 TORCH_LIBRARY(dlion, m) {
+  m.def("quant4(Tensor w, Tensor code) -> (Tensor, Tensor)");
+  m.def("dequant4_(Tensor q, Tensor absmax, Tensor code, Tensor(a!) out) -> ()");
   m.def("gemm_tn(Tensor[] P, Tensor[] Q, int splits) -> Tensor");
   m.def("gemm_tn_(Tensor[] P, Tensor[] Q, Tensor(a!) out, bool accumulate) -> ()");
   m.def("lora_rows(Tensor x, Tensor w, float scale, float p, int seed) -> Tensor");
@@ -984,4 +1022,6 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("lora_rows", &lora_rows);
   m.impl("lora_up", &lora_up);
   m.impl("lora_cols", &lora_cols);
+  m.impl("quant4", &quant4);
+  m.impl("dequant4_", &dequant4_);
 }

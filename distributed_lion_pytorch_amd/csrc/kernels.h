@@ -103,6 +103,13 @@ hipError_t launch_lora_cols(const void* g, int64_t ldg, const void* y, const voi
                             int N, int r, int parts, int mode, float yscale, uint32_t seed, uint32_t thresh16,
                             float inv_keep, hipStream_t st);
 
+// ---- 4-bit blockwise quantization of frozen weights (quant.hip); n % 64 == 0, 16-byte aligned
+// q [n / 2] uint8 (first element of a pair in the high nibble), absmax [n / 64] fp32, code [16] fp32
+hipError_t launch_quant4(int dt, const void* w, const float* code, uint8_t* q, float* absmax, int64_t n,
+                         hipStream_t st);
+hipError_t launch_dequant4(int dt, const uint8_t* q, const float* absmax, const float* code, void* out, int64_t n,
+                           hipStream_t st);
+
 // ---- LM head cross-entropy (xent_kernels.hip)
 // variant 0 = auto (DLION_XENT env override), 1 fp32-row, 2 streaming, 3/4/5 packed 16-bit row (256/512/1024 thr)
 hipError_t launch_softmax_xent(int dt, void* logits, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,

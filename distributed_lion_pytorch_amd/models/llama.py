@@ -128,18 +128,27 @@ def _proj(x, layers):
     adapter path to their own output.  Falls back to one GEMM per layer off the
     GPU, with biases, or for unknown wrappers."""
     from .lora import LoraLinear
+    from .quant import Linear4bit, linear4bit_multi
 
-    bases = []
+    bases, q4 = [], []
     for layer in layers:
-        if type(layer) is nn.Linear and layer.bias is None:
-            bases.append(layer.weight)
-        elif isinstance(layer, LoraLinear) and layer.base_layer.bias is None:
-            bases.append(layer.base_layer.weight)
+        base = layer.base_layer if isinstance(layer, LoraLinear) else layer
+        if getattr(base, "bias", None) is not None:
+            return tuple(_lin(layer, x) for layer in layers)
+        if type(base) is nn.Linear:
+            bases.append(base.weight)
+        elif isinstance(base, Linear4bit):  # QLoRA base: one expansion + one GEMM (models/quant.py)
+            q4.append(base)
         else:
             return tuple(_lin(layer, x) for layer in layers)
-    if not x.is_cuda or len({w.dtype for w in bases}) != 1:
+    if q4:
+        if bases:
+            return tuple(_lin(layer, x) for layer in layers)
+        outs = linear4bit_multi(x, q4)
+    elif not x.is_cuda or len({w.dtype for w in bases}) != 1:
         return tuple(_lin(layer, x) for layer in layers)
-    outs = linear_multi_nk(x, bases)
+    else:
+        outs = linear_multi_nk(x, bases)
     return tuple(layer.add_adapter(x, o) if isinstance(layer, LoraLinear) else o for layer, o in zip(layers, outs))
 
 

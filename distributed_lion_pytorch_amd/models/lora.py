@@ -24,6 +24,7 @@ import torch.nn as nn
 
 from ..ops import fused
 from ..ops.linear import linear_nk
+from .quant import Linear4bit
 
 
 @dataclass
@@ -45,13 +46,17 @@ class LoraConfig:
 class LoraLinear(nn.Module):
     """y = x W^T (+b) + dropout(x) A^T B^T * (alpha / r); W frozen, B zero-init."""
 
-    def __init__(self, base: nn.Linear, r: int, alpha: int, dropout: float):
+    def __init__(self, base: nn.Module, r: int, alpha: int, dropout: float):
         super().__init__()
         self.base_layer = base
         self.r = r
         self.scaling = alpha / r
-        self.lora_A = nn.Linear(base.in_features, r, bias=False, device=base.weight.device, dtype=base.weight.dtype)
-        self.lora_B = nn.Linear(r, base.out_features, bias=False, device=base.weight.device, dtype=base.weight.dtype)
+        if isinstance(base, Linear4bit):  # QLoRA: adapters in the compute dtype
+            dev, dt = base.qweight.device, base.compute_dtype
+        else:
+            dev, dt = base.weight.device, base.weight.dtype
+        self.lora_A = nn.Linear(base.in_features, r, bias=False, device=dev, dtype=dt)
+        self.lora_B = nn.Linear(r, base.out_features, bias=False, device=dev, dtype=dt)
         self.dropout = nn.Dropout(dropout) if dropout > 0 else nn.Identity()
         nn.init.kaiming_uniform_(self.lora_A.weight, a=math.sqrt(5))
         nn.init.zeros_(self.lora_B.weight)
@@ -74,13 +79,18 @@ class LoraLinear(nn.Module):
         return fused.lora_add(y, x, self.lora_A.weight, self.lora_B.weight, self.scaling, p)
 
     def forward(self, x):
+        if isinstance(self.base_layer, Linear4bit):
+            return self.add_adapter(x, self.base_layer(x))
         return self.add_adapter(x, linear_nk(x, self.base_layer.weight, self.base_layer.bias))
 
     @torch.no_grad()
     def merge(self):
         if not self.merged:
             delta = (self.lora_B.weight.float() @ self.lora_A.weight.float()) * self.scaling
-            self.base_layer.weight.add_(delta.to(self.base_layer.weight.dtype))
+            if isinstance(self.base_layer, Linear4bit):  # peft: dequantize, add, requantize
+                self.base_layer.requantize_(self.base_layer.dequantize(torch.float32) + delta)
+            else:
+                self.base_layer.weight.add_(delta.to(self.base_layer.weight.dtype))
             self.merged = True
 
 
@@ -97,7 +107,7 @@ def inject_lora(model: nn.Module, config: LoraConfig) -> nn.Module:
     for name, module in list(model.named_modules()):
         for child_name, child in list(module.named_children()):
             full = f"{name}.{child_name}" if name else child_name
-            if isinstance(child, nn.Linear) and _match(full, config.target_modules):
+            if isinstance(child, (nn.Linear, Linear4bit)) and _match(full, config.target_modules):
                 setattr(module, child_name, LoraLinear(child, config.r, config.lora_alpha, config.lora_dropout))
                 replaced += 1
     if replaced == 0:

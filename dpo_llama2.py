@@ -6,8 +6,10 @@ unclosed ``{``; and uses an undefined ``base_model``, D9).
 Same ScriptArguments (beta, lr, schedule, LoRA, lengths, steps, ``--lion``,
 ``--async_grad``) and the same in-code TrainingArguments
 (dpo_llama2.py:171-190), MI355X-native underneath:
-* policy + frozen reference replicas in bf16 on each GPU (no 4-bit: D-note in
-  sft_llama2.py), native Llama kernels;
+* policy + frozen reference replicas in bf16 on each GPU by default;
+  ``--load_in_4bit`` stores both frozen bases in 4-bit NF4 like the reference
+  (dpo_llama2.py:133-152 ``load_in_4bit=True``) with the native 4-bit layers
+  (models/quant.py); native Llama kernels;
 * DPO sigmoid loss with chosen/rejected concatenated in one policy forward
   (native trainer: trl is not installed);
 * LoRA targets use Llama module names (q_proj, k_proj, v_proj -- the modules
@@ -78,6 +80,8 @@ class ScriptArguments:
     synthetic_samples: Optional[int] = field(default=10000)
     model_overrides: Optional[str] = field(default=None)
     torch_dtype: Optional[str] = field(default="bfloat16")
+    load_in_4bit: Optional[bool] = field(default=False, metadata={"help": "4-bit frozen bases (dpo_llama2.py:133-152)"})
+    bnb_4bit_quant_type: Optional[str] = field(default="nf4")
     bf16: Optional[bool] = field(default=True)
     seed: Optional[int] = field(default=0)
     use_cpu: Optional[bool] = field(default=False)
@@ -109,6 +113,13 @@ def main(argv=None):
     model_ref = build_model(config, model_name_or_path=script_args.model_name_or_path,
                             torch_dtype=script_args.torch_dtype)
     model_ref.load_state_dict(model.state_dict())  # identical frozen reference (also for random init)
+    if script_args.load_in_4bit:
+        from distributed_lion_pytorch_amd.models.quant import QuantConfig, quantize_model
+
+        qc = QuantConfig(bnb_4bit_quant_type=script_args.bnb_4bit_quant_type,
+                         bnb_4bit_compute_dtype=getattr(torch, script_args.torch_dtype))
+        quantize_model(model, qc)
+        quantize_model(model_ref, qc)
     if script_args.gradient_checkpointing:
         model.gradient_checkpointing_enable()
 

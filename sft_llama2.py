@@ -3,9 +3,10 @@
 /root/reference/sft_llama2.py (same ScriptArguments + HF TrainingArguments,
 ``--lion`` / ``--async_grad``), MI355X-native underneath:
 
-* one full bf16 replica per GPU (288 GB HBM; the reference's 4-bit NF4 base
-  model needs bitsandbytes, which is not part of this stack), native Llama
-  with the gfx950 attention / LM-head kernels;
+* one full bf16 replica per GPU by default (288 GB HBM holds it), native
+  Llama with the gfx950 attention / LM-head kernels; ``--load_in_4bit``
+  reproduces the reference's 4-bit NF4 base model (sft_llama2.py:141-149,
+  bitsandbytes) with the native 4-bit layers (models/quant.py, QLoRA);
 * LoRA (r=8, alpha=16, dropout 0.05, q_proj/v_proj, sft_llama2.py:44-51) via
   the native adapter implementation (peft absent) -- ``--use_lora false``
   trains all weights;
@@ -67,6 +68,9 @@ class ScriptArguments:
     synthetic_samples: Optional[int] = field(default=20000)
     model_overrides: Optional[str] = field(default=None, metadata={"help": "config overrides, e.g. num_hidden_layers=4"})
     torch_dtype: Optional[str] = field(default="bfloat16")
+    load_in_4bit: Optional[bool] = field(default=False, metadata={
+        "help": "frozen base weights in 4-bit (the reference's BitsAndBytesConfig, sft_llama2.py:141-145)"})
+    bnb_4bit_quant_type: Optional[str] = field(default="nf4", metadata={"help": "nf4 | fp4"})
 
 
 def load_samples(script_args, seed):
@@ -105,6 +109,11 @@ def main(argv=None):
     tokenizer = load_tokenizer(script_args.model_name)
     config = load_config(script_args.model_name, overrides=script_args.model_overrides)
     model = build_model(config, model_name_or_path=script_args.model_name, torch_dtype=script_args.torch_dtype)
+    if script_args.load_in_4bit:
+        from distributed_lion_pytorch_amd.models.quant import QuantConfig, quantize_model
+
+        quantize_model(model, QuantConfig(bnb_4bit_quant_type=script_args.bnb_4bit_quant_type,
+                                          bnb_4bit_compute_dtype=getattr(torch, script_args.torch_dtype)))
     if training_args.gradient_checkpointing:
         model.gradient_checkpointing_enable()
     peft_config = None
@@ -139,7 +148,11 @@ def main(argv=None):
         out = os.path.join(training_args.output_dir, "final_checkpoint")
         if script_args.use_lora:
             save_adapter(trainer.model, out)
-            merged = merge_and_unload(trainer.accelerator.unwrap_model(trainer.model))
+            from distributed_lion_pytorch_amd.models.quant import dequantize_model
+
+            # like the reference (sft_llama2.py:195-199: base reloaded in bf16, adapters merged), the
+            # merged checkpoint is a plain compute-dtype model even when training ran on a 4-bit base
+            merged = merge_and_unload(dequantize_model(trainer.accelerator.unwrap_model(trainer.model)))
             merged.save_pretrained(os.path.join(training_args.output_dir, "final_merged_checkpoint"),
                                    safe_serialization=True)
         else:
