@@ -63,3 +63,33 @@ def test_two_ranks_one_gpu_hip_matches_oracle(exchange):
     # HIP kernels vs the per-segment PyTorch oracle (same votes, ATen rounding):
     # identical parameters after 3 distributed steps
     assert torch.equal(hip_res[0]["flat"], ora_res[0]["flat"])
+
+
+def test_bench_contract_two_ranks_under_torchrun(tmp_path):
+    """bench.py as the driver launches it for N > 1 (torch.distributed.run,
+    one process per rank, 127.0.0.1 rendezvous), here with both ranks on the
+    one GPU over gloo: one JSON line from rank 0 with the whole-job value."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--backend", "gloo", "--model", "gpt2-tiny", "--micro_batch", "2", "--grad_accum", "2",
+           "--seq_len", "128"]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 2 * 2 * 2
+    assert out["value"] > 0 and out["higher_is_better"] is True
+    assert out["wire_bytes_per_step_per_rank"] > 0
+    assert abs(out["value"] - 2 * 2 * 2 * 128 * 2 / (out["ms_per_step"] * 2 / 1000)) / out["value"] < 0.01
