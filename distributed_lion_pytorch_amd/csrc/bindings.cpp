@@ -791,13 +791,21 @@ void gemm_tn_check_launch(at::TensorList P, at::TensorList Q, int64_t splits, co
   TORCH_CHECK(rows % 128 == 0 && M % 8 == 0 && N % 8 == 0 && ldp % 8 == 0 && ldq % 8 == 0,
               "dlion gemm_tn: rows % 128, M % 8, N % 8 and row strides % 8 must be 0");
   TORCH_CHECK(splits >= 1 && splits <= static_cast<int64_t>(P.size()) * rows / 128, "dlion gemm_tn: bad split count");
-  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.dim() == 3 &&
-                  out.size(0) == splits && out.size(1) == M && out.size(2) == N,
-              "dlion gemm_tn: out must be a contiguous fp32 [splits, M, N] tensor");
+  const bool bf16_out = out.scalar_type() == at::kBFloat16;
+  if (bf16_out) {
+    TORCH_CHECK(splits == 1 && out.is_cuda() && out.is_contiguous() && out.numel() == M * N &&
+                    reinterpret_cast<uintptr_t>(out.data_ptr()) % 8 == 0,
+                "dlion gemm_tn: a bf16 out must be one contiguous [M, N] (unsplit) tensor");
+  } else {
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.dim() == 3 &&
+                    out.size(0) == splits && out.size(1) == M && out.size(2) == N,
+                "dlion gemm_tn: out must be a contiguous fp32 [splits, M, N] tensor");
+  }
   const c10::DeviceGuard g(P[0].device());
   check_hip(dlion::launch_gemm_tn(pp.data(), qq.data(), static_cast<int>(P.size()), rows, static_cast<int>(ldp),
-                                  static_cast<int>(ldq), out.data_ptr<float>(), static_cast<int>(M),
-                                  static_cast<int>(N), static_cast<int>(splits), accumulate, cur_stream()),
+                                  static_cast<int>(ldq), bf16_out ? nullptr : out.data_ptr<float>(),
+                                  static_cast<int>(M), static_cast<int>(N), static_cast<int>(splits), accumulate,
+                                  cur_stream(), bf16_out ? out.data_ptr() : nullptr),
             "gemm_tn");
 }
 
@@ -808,8 +816,13 @@ Tensor gemm_tn(at::TensorList P, at::TensorList Q, int64_t splits) {
   return out;
 }
 
-// out[z] (+)= the split-z partial of P^T Q (out: the fp32 [splits, M, N] accumulator)
+// out[z] (+)= the split-z partial of P^T Q (out: the fp32 [splits, M, N] accumulator), or, for a
+// bf16 out (any contiguous shape of M * N elements), out (+)= bf16(P^T Q) unsplit
 void gemm_tn_(at::TensorList P, at::TensorList Q, const Tensor& out, bool accumulate) {
+  if (out.scalar_type() == at::kBFloat16) {
+    gemm_tn_check_launch(P, Q, 1, out, accumulate);
+    return;
+  }
   TORCH_CHECK(out.dim() == 3, "dlion gemm_tn_: out must be [splits, M, N]");
   gemm_tn_check_launch(P, Q, out.size(0), out, accumulate);
 }

@@ -81,8 +81,9 @@ hipError_t launch_scale_acc(const void* x, const float* s, void* y, int64_t n, i
 // ---- weight-gradient GEMM (gemm_tn.hip): C[z][M,N] fp32 (+)= P^T Q over split z's rows of the
 // nseg segments (P_i [seg_rows, >= M] ld ldp, Q_i [seg_rows, >= N] ld ldq; bf16, 16-byte aligned).
 // Needs seg_rows % 128 == 0, M % 8 == N % 8 == 0, 1 <= splits <= nseg * seg_rows / 128, nseg <= 16.
+// Cb non-null (splits == 1): C ignored, Cb [M, N] bf16 (+)= bf16(P^T Q) instead (the gradient itself).
 hipError_t launch_gemm_tn(const void* const* P, const void* const* Q, int nseg, int64_t seg_rows, int ldp, int ldq,
-                          float* C, int M, int N, int splits, bool accumulate, hipStream_t st);
+                          float* C, int M, int N, int splits, bool accumulate, hipStream_t st, void* Cb = nullptr);
 
 // diagnostic build of the plain GEMM with per-block timestamps (tools/gemm_stamps.py)
 hipError_t launch_gemm_nt_stamped(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,

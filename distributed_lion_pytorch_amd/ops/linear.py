@@ -520,6 +520,14 @@ def wgrad_into(a: torch.Tensor, b: torch.Tensor, w: torch.nn.Parameter) -> None:
                 return  # reduced into w.grad when the accumulation window closes
             g = w.grad  # _acc_gemm may have flushed earlier partials into it
             grad_ok = g is None or (g.is_contiguous() and g.dtype == w.dtype)
+            if grad_ok and own and s == 1 and w.dtype == torch.bfloat16:
+                # unsplit: the TN kernel writes (adds onto) the bf16 gradient itself
+                if g is None:
+                    w.grad = g = torch.empty_like(w, memory_format=torch.contiguous_format)
+                    hip.ops().gemm_tn_([a], [b], g, False)
+                else:
+                    hip.ops().gemm_tn_([a], [b], g, True)
+                return
             if grad_ok:
                 part = wgrad_partials(a, b, s).view(s, K * N)
                 if g is None:
@@ -543,6 +551,12 @@ def wgrad(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     s, own = wgrad_splits(a, b)
     if (s == 1 and not own) or (M % s and not own):
         return a.t() @ b
+    if own and s == 1 and a.dtype == torch.bfloat16:
+        from . import hip
+
+        out = torch.empty(K, N, dtype=a.dtype, device=a.device)
+        hip.ops().gemm_tn_([a], [b], out, False)  # bf16 straight from the accumulators
+        return out
     part = wgrad_partials(a, b, s)
     if a.dtype == torch.bfloat16 and (K * N) % 4 == 0:
         from . import hip
@@ -669,9 +683,22 @@ def cat_weights(ws) -> torch.Tensor:
     gen = _WEIGHT_GEN[0] if any(w.requires_grad for w in ws) else -1
     key = (gen,) + tuple((w._version, w.data_ptr()) for w in ws)
     hit = _CAT_CACHE.get(ck)
-    if hit is not None and all(r() is w for r, w in zip(hit[0], ws)) and hit[1] == key:
+    same = hit is not None and all(r() is w for r, w in zip(hit[0], ws))
+    if same and hit[1] == key:
         return hit[2]
     with torch.no_grad():
+        old = hit[2] if same else None
+        if (old is not None and old.dtype == ws[0].dtype and old.shape[0] == sum(w.shape[0] for w in ws)
+                and old.shape[1:] == ws[0].shape[1:]):
+            # refreshed in place after an optimizer step (trainable Llama q/k/v, gate/up):
+            # one contiguous device copy per weight into the kept buffer -- no reallocation, and
+            # ~2x the rate of the cat kernel (Llama-3-8B: 64 cats per step, ~6.6 ms)
+            off = 0
+            for w in ws:
+                old[off:off + w.shape[0]].copy_(w.detach())
+                off += w.shape[0]
+            _CAT_CACHE[ck] = (hit[0], key, old)
+            return old
         out = torch.cat([w.detach() for w in ws], 0)
     if hit is None:
         weakref.finalize(ws[0], _CAT_CACHE.pop, ck, None)
@@ -764,6 +791,20 @@ def _multi_wgrad_into(dy, x2d, params, sizes) -> None:
             if _FUSE_ACCUM["on"] and ((own and _defer_wgrad(list(params), cols, dy, x2d, s))
                                       or _acc_gemm(list(params), cols, dy, x2d, s)):
                 return  # reduced into each params[i].grad when the window closes
+            if own and s == 1 and all(p.dtype == torch.bfloat16 for p in params):
+                gs = [p.grad for p in params]
+                if all(g is None for g in gs):  # one buffer; each grad is a row block of it
+                    buf = torch.empty(N, K, dtype=torch.bfloat16, device=dy.device)
+                    hip.ops().gemm_tn_([dy], [x2d], buf, False)
+                    off = 0
+                    for p, n in zip(params, sizes):
+                        p.grad = buf[off:off + n].view_as(p)
+                        off += n
+                    return
+                base = _adjacent_rows(gs) if all(g is not None for g in gs) else None
+                if base is not None and base.dtype == torch.bfloat16 and base.is_contiguous():
+                    hip.ops().gemm_tn_([dy], [x2d], base, True)
+                    return
             flat = wgrad_partials(dy, x2d, s).view(s, N * K)
             off = 0
             for p, n in zip(params, sizes):

@@ -136,3 +136,78 @@ def test_checkpointed_model_skips_wgrad_deferral(cuda, monkeypatch):
     for n in g_plain:
         err = (g_ckpt[n] - g_plain[n]).abs().max().item() / max(g_plain[n].abs().max().item(), 1e-6)
         assert err < 3e-2, n
+
+
+@pytest.mark.parametrize("M,N,rows,nseg", [(256, 256, 128, 1), (776, 264, 256, 2), (1024, 4096, 1024, 1)])
+def test_gemm_tn_bf16_out_matches_fp32(cuda, M, N, rows, nseg):
+    """Unsplit bf16 output (the gradient written from the accumulators, no fp32
+    partials) and its accumulate form: bf16(P^T Q + old) as sum_partials rounds."""
+    hip.require()
+    torch.manual_seed(2)
+    P = [torch.randn(rows, M, device=cuda, dtype=torch.bfloat16) for _ in range(nseg)]
+    Q = [torch.randn(rows, N, device=cuda, dtype=torch.bfloat16) for _ in range(nseg)]
+    ref = torch.cat(P).float().t() @ torch.cat(Q).float()
+    out = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+    hip.ops().gemm_tn_(P, Q, out, False)
+    assert (out.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    # same rounding as the fp32-partial path it replaces
+    part = hip.ops().gemm_tn(P, Q, 1)
+    assert torch.equal(out, hip.ops().sum_partials(part.view(1, -1)).view(M, N))
+    old = torch.randn(M, N, device=cuda, dtype=torch.bfloat16)
+    acc = old.clone()
+    hip.ops().gemm_tn_(P, Q, acc, True)
+    exp = old.clone()
+    hip.ops().sum_partials_acc_(part.view(1, -1), exp.view(-1))
+    assert torch.equal(acc, exp)
+
+
+def test_unsplit_wgrad_into_and_fused_projection_grads(cuda):
+    """Llama-sized weights take the unsplit bf16 path in wgrad_into / the fused
+    q/k/v weight gradient (ops/linear.py); grads equal autograd's."""
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    torch.manual_seed(3)
+    T, K = 1024, 4096
+    ws = [torch.nn.Parameter((torch.randn(n, K, device=cuda) * 0.02).to(torch.bfloat16)) for n in (2048, 1024, 1024)]
+    assert L.wgrad_splits(torch.empty(T, 4096, device=cuda, dtype=torch.bfloat16),
+                          torch.empty(T, K, device=cuda, dtype=torch.bfloat16)) == (1, True)
+    x = torch.randn(T, K, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    refs = [w.detach().float().requires_grad_() for w in ws]
+    for step in range(2):  # one-micro-batch windows (TrainStep, grad_accum 1); the second accumulates
+        with L.grad_accumulation_fusion(True, micro_batches=1):
+            outs = L.linear_multi_nk(x, ws)
+            gs = [torch.randn_like(o) for o in outs]
+            torch.autograd.backward(outs, gs)
+        ro = [x.detach().float() @ r.t() for r in refs]
+        torch.autograd.backward(ro, [g.float() for g in gs])
+    for w, r in zip(ws, refs):
+        assert (w.grad.float() - r.grad).abs().max().item() <= 2e-2 * r.grad.abs().max().item()
+    base = L._adjacent_rows([w.grad for w in ws])
+    assert base is not None and base.shape == (4096, K)
+    # single linear: wgrad_into s == 1
+    w1 = torch.nn.Parameter((torch.randn(4096, K, device=cuda) * 0.02).to(torch.bfloat16))
+    with L.grad_accumulation_fusion(True, micro_batches=1):
+        y = L.linear_nk(x, w1)
+        g = torch.randn_like(y)
+        y.backward(g)
+    ref = g.float().t() @ x.detach().float()
+    assert (w1.grad.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+
+
+def test_cat_weights_refreshes_in_place_after_step(cuda):
+    """Trainable fused-projection weights: after an optimizer step the cached
+    concatenation is refreshed into the same buffer (no reallocation)."""
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    ws = [torch.nn.Parameter(torch.randn(n, 256, device=cuda, dtype=torch.bfloat16)) for n in (256, 128, 128)]
+    c1 = L.cat_weights(ws)
+    assert torch.equal(c1, torch.cat([w.detach() for w in ws]))
+    ptr = c1.data_ptr()
+    assert L.cat_weights(ws) is c1  # cached within a step
+    with torch.no_grad():
+        for w in ws:
+            w.add_(1.0)
+    L.bump_weight_generation()
+    c2 = L.cat_weights(ws)
+    assert c2.data_ptr() == ptr and torch.equal(c2, torch.cat([w.detach() for w in ws]))
