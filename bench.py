@@ -83,6 +83,10 @@ def parse():
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--weight_decay", type=float, default=None)
     ap.add_argument("--gradient_checkpointing", action="store_true")
+    ap.add_argument("--checkpointing_policy", default="auto", choices=["auto", "reference"],
+                    help="auto: checkpoint only when the activations would not fit in HBM (dpo_llama2.py default)")
+    ap.add_argument("--no_gradient_checkpointing", action="store_true",
+                    help="override a preset's checkpointing (the DPO preset's replicas fit 288 GB without it)")
     ap.add_argument("--fuse_accum", type=int, default=1, help="gradient-accumulation fusion (ops/linear.py)")
     ap.add_argument("--max_grad_norm", type=float, default=1.0)
     ap.add_argument("--exchange", default="a2a", help="allgather | a2a | ref_int64")
@@ -101,7 +105,8 @@ def parse():
     for k, v in PRESETS[a.task].items():
         if getattr(a, k, None) is None:
             setattr(a, k, v)
-    a.gradient_checkpointing = a.gradient_checkpointing or bool(getattr(a, "grad_ckpt", False))
+    a.gradient_checkpointing = (a.gradient_checkpointing or bool(getattr(a, "grad_ckpt", False))) and \
+        not a.no_gradient_checkpointing
     return a
 
 
@@ -154,6 +159,13 @@ def build_native(args, dev):
 
         inject_lora(model, LoraConfig(**args.lora))
         model.to(device=dev, dtype=torch.bfloat16)
+    if args.gradient_checkpointing:
+        # the DPO preset's reference setting; "auto" (dpo_llama2.py's default policy) keeps the
+        # activations when they fit in HBM (trainer/memory.py)
+        from distributed_lion_pytorch_amd.trainer.memory import should_checkpoint
+
+        tokens = args.micro_batch * (2 if args.task == "dpo" else 1) * args.seq_len
+        args.gradient_checkpointing = should_checkpoint(True, args.checkpointing_policy, cfg, tokens, model, ref_model)
     if args.gradient_checkpointing:
         model.gradient_checkpointing_enable()
     broadcast_parameters(model)
@@ -296,6 +308,7 @@ def main():
                 "base_weights": "nf4 (4-bit, frozen)" if args.load_in_4bit else "bf16",
                 "global_batch": world * args.grad_accum * args.micro_batch,
                 "task": args.task,
+                "gradient_checkpointing": bool(args.gradient_checkpointing),
                 "micro_batch": args.micro_batch,
                 "grad_accum": args.grad_accum,
                 "seq_len": args.seq_len,

@@ -58,6 +58,9 @@ class ScriptArguments:
     per_device_eval_batch_size: Optional[int] = field(default=1)
     gradient_accumulation_steps: Optional[int] = field(default=4)
     gradient_checkpointing: Optional[bool] = field(default=True)
+    checkpointing_policy: Optional[str] = field(default="auto", metadata={
+        "help": "auto: keep activations when policy + reference + activations fit in HBM (288 GB on MI355X), "
+                "checkpoint otherwise (trainer/memory.py); reference: --gradient_checkpointing as given"})
     lora_alpha: Optional[float] = field(default=16)
     lora_dropout: Optional[float] = field(default=0.05)
     lora_r: Optional[int] = field(default=8)
@@ -120,8 +123,14 @@ def main(argv=None):
                          bnb_4bit_compute_dtype=getattr(torch, script_args.torch_dtype))
         quantize_model(model, qc)
         quantize_model(model_ref, qc)
-    if script_args.gradient_checkpointing:
+    from distributed_lion_pytorch_amd.trainer.memory import should_checkpoint
+
+    tokens = 2 * script_args.per_device_train_batch_size * script_args.max_length  # chosen + rejected
+    if should_checkpoint(script_args.gradient_checkpointing, script_args.checkpointing_policy, config, tokens,
+                         model, model_ref):
         model.gradient_checkpointing_enable()
+    elif script_args.gradient_checkpointing:
+        logger.info("gradient checkpointing not needed: activations fit in device memory (--checkpointing_policy auto)")
 
     rows = load_pairs(script_args)
     n_eval = max(1, min(len(rows) // 20, 1000))
