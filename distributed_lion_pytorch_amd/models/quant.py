@@ -189,7 +189,9 @@ def quantize_model(model: nn.Module, config: Optional[QuantConfig] = None, **kw)
     for name, module in list(model.named_modules()):
         for child_name, child in list(module.named_children()):
             full = f"{name}.{child_name}" if name else child_name
-            if type(child) is nn.Linear and not _skipped(full, config.llm_int8_skip_modules):
+            # LoRA adapters stay trainable (quantizing an injected model keeps them as they are)
+            if (type(child) is nn.Linear and not _skipped(full, config.llm_int8_skip_modules)
+                    and child_name not in ("lora_A", "lora_B")):
                 setattr(module, child_name, Linear4bit.from_linear(child, config.bnb_4bit_quant_type,
                                                                    config.bnb_4bit_compute_dtype))
                 n += 1

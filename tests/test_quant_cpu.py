@@ -164,3 +164,15 @@ def test_linear4bit_survives_model_dtype_cast():
     assert l4.absmax.dtype == torch.float32 and l4.quant_map.dtype == torch.float32
     assert l4.qweight.dtype == torch.uint8
     assert torch.equal(l4.dequantize(torch.float32), before)
+
+
+def test_quantize_after_lora_keeps_adapters_trainable():
+    m = _tiny()
+    inject_lora(m, LoraConfig(r=8, lora_alpha=16, lora_dropout=0.0))
+    quantize_model(m, QuantConfig())
+    q = m.model.layers[0].self_attn.q_proj
+    assert isinstance(q.base_layer, Linear4bit)
+    assert type(q.lora_A) is nn.Linear and q.lora_A.weight.requires_grad
+    ids = torch.randint(0, 512, (1, 64))
+    m(input_ids=ids, labels=ids).loss.backward()
+    assert q.lora_B.weight.grad is not None
