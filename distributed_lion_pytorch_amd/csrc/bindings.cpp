@@ -10,6 +10,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "kernels.h"
@@ -378,6 +380,32 @@ Partials partials(const Tensor& part) {
   return {part.data_ptr<float>(), part.size(0), part.size(1), part.stride(0)};
 }
 
+// narrow tall stacks go through the row-split two-pass reduction (elementwise_kernels.hip);
+// returns false when the one-pass kernels are the better fit
+bool sum_partials_split(const std::vector<const float*>& ptrs, const std::vector<int64_t>& rows,
+                        const std::vector<int64_t>& lds, int64_t n, void* out, bool accumulate, const float* scale,
+                        const at::TensorOptions& opt) {
+  static const bool enabled = [] {
+    const char* e = std::getenv("DLION_SPLIT_PARTIALS");  // A/B switch: 0 = one-pass kernels only
+    return e == nullptr || std::string(e) != "0";
+  }();
+  if (!enabled) return false;
+  int64_t total = 0;
+  for (auto r : rows) total += r;
+  const int Y = dlion::sum_partials_split_factor(n, total);
+  if (Y <= 1) return false;
+  auto scratch = at::empty({Y, n}, opt.dtype(at::kFloat));
+  check_hip(dlion::launch_sum_partials_split(ptrs.data(), rows.data(), lds.data(), static_cast<int>(ptrs.size()), n, Y,
+                                             scratch.data_ptr<float>(), out, accumulate, scale, cur_stream()),
+            "sum_partials_split");
+  return true;
+}
+
+bool sum_partials_split1(const Partials& P, void* out, bool accumulate, const float* scale,
+                         const at::TensorOptions& opt) {
+  return sum_partials_split({P.ptr}, {P.S}, {P.ld}, P.n, out, accumulate, scale, opt);
+}
+
 Tensor sum_partials(const Tensor& part) {
   const auto P = partials(part);
   TORCH_CHECK(P.n % 4 == 0, "dlion: partial row length must be a multiple of 4");
@@ -385,6 +413,7 @@ Tensor sum_partials(const Tensor& part) {
   auto sizes = part.sizes().vec();
   sizes.erase(sizes.begin());
   auto out = at::empty(sizes, part.options().dtype(at::kBFloat16));
+  if (sum_partials_split1(P, out.data_ptr(), false, nullptr, part.options())) return out;
   check_hip(dlion::launch_sum_partials(P.ptr, static_cast<int>(P.S), P.n, P.ld, out.data_ptr(), false, cur_stream()),
             "sum_partials");
   return out;
@@ -398,6 +427,7 @@ void sum_partials_acc_(const Tensor& part, const Tensor& out) {
               "dlion: accumulation target must be a contiguous bf16 tensor of the partial row size");
   TORCH_CHECK(P.n % 4 == 0, "dlion: partial row length must be a multiple of 4");
   const c10::DeviceGuard g(part.device());
+  if (sum_partials_split1(P, out.data_ptr(), true, nullptr, part.options())) return;
   check_hip(dlion::launch_sum_partials(P.ptr, static_cast<int>(P.S), P.n, P.ld, out.data_ptr(), true, cur_stream()),
             "sum_partials_acc_");
 }
@@ -421,6 +451,7 @@ void sum_partials_multi_(at::TensorList parts, const Tensor& out, bool accumulat
               "dlion: target must be a contiguous bf16 tensor of the partial row size");
   TORCH_CHECK(n % 4 == 0, "dlion: partial row length must be a multiple of 4");
   const c10::DeviceGuard g(out.device());
+  if (sum_partials_split(ptrs, rows, lds, n, out.data_ptr(), accumulate, nullptr, out.options())) return;
   check_hip(dlion::launch_sum_partials_multi(ptrs.data(), rows.data(), lds.data(), static_cast<int>(parts.size()), n,
                                              out.data_ptr(), accumulate, cur_stream()),
             "sum_partials_multi_");
@@ -436,6 +467,7 @@ void sum_partials_scaled_(const Tensor& part, const Tensor& s, const Tensor& out
               "dlion: target must be a contiguous bf16 tensor of the partial row size");
   TORCH_CHECK(P.n % 4 == 0, "dlion: partial row length must be a multiple of 4");
   const c10::DeviceGuard g(part.device());
+  if (sum_partials_split1(P, out.data_ptr(), accumulate, s.data_ptr<float>(), part.options())) return;
   check_hip(dlion::launch_sum_partials(P.ptr, static_cast<int>(P.S), P.n, P.ld, out.data_ptr(), accumulate, cur_stream(),
                                        s.data_ptr<float>()),
             "sum_partials_scaled_");

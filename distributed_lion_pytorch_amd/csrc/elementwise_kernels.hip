@@ -346,6 +346,40 @@ __global__ void __launch_bounds__(kTallQ * kTallR) sum_partials_multi_kernel(con
   }
 }
 
+// Pass 1 of the row-split tall reduction: with only n/32 column blocks (GPT-2's
+// 768..3072-wide bias / norm partial stacks: 24-96 blocks, one CU each, 0.4-1.3
+// TB/s) the rows are also split over gridDim.y: block (x, y) sums the kTallR-row
+// groups y, y + Y, ... of every segment into scratch[y] (fp32); pass 2 is the
+// plain sum_partials kernel over those Y rows (fixed order: deterministic).
+__global__ void __launch_bounds__(kTallQ * kTallR) sum_partials_split_kernel(const PartSegs sg, int64_t n,
+                                                                            float* __restrict__ scratch) {
+  __shared__ float4 red[kTallR][kTallQ];
+  const int q = threadIdx.x % kTallQ, r = threadIdx.x / kTallQ;
+  const int64_t col4 = static_cast<int64_t>(blockIdx.x) * kTallQ + q;
+  const int64_t n4 = n / 4;
+  const int64_t step = static_cast<int64_t>(kTallR) * gridDim.y;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col4 < n4) {
+    for (int k = 0; k < sg.nseg; ++k) {
+      const float4* p = reinterpret_cast<const float4*>(sg.ptr[k]) + col4;
+      for (int64_t s = static_cast<int64_t>(blockIdx.y) * kTallR + r; s < sg.rows[k]; s += step) {
+        const float4 v = p[s * sg.ld4[k]];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+  }
+  red[r][q] = acc;
+  __syncthreads();
+  if (r == 0 && col4 < n4) {
+#pragma unroll 8
+    for (int i = 1; i < kTallR; ++i) {
+      const float4 v = red[i][q];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(scratch + static_cast<int64_t>(blockIdx.y) * n)[col4] = acc;
+  }
+}
+
 static inline int grid_for(int64_t work, int64_t per_block) {
   int64_t g = (work + per_block - 1) / per_block;
   if (g > 2048) g = 2048;
@@ -469,6 +503,41 @@ hipError_t launch_sum_partials_multi(const float* const* ptrs, const int64_t* ro
   auto O = static_cast<uint16_t*>(out);
   if (accumulate) hipLaunchKernelGGL(sum_partials_multi_kernel<true>, g, blk, 0, st, sg, n, O);
   else hipLaunchKernelGGL(sum_partials_multi_kernel<false>, g, blk, 0, st, sg, n, O);
+  return hipGetLastError();
+}
+
+int sum_partials_split_factor(int64_t n, int64_t total_rows) {
+  const int64_t col_blocks = (n / 4 + kTallQ - 1) / kTallQ;
+  if (col_blocks >= 256 || total_rows < 4 * kTallR) return 1;
+  int64_t y = (512 + col_blocks - 1) / col_blocks;  // ~2 blocks per CU
+  y = y < total_rows / (2 * kTallR) ? y : total_rows / (2 * kTallR);
+  y = y < 64 ? y : 64;
+  return static_cast<int>(y < 1 ? 1 : y);
+}
+
+hipError_t launch_sum_partials_split(const float* const* ptrs, const int64_t* rows, const int64_t* lds, int nseg,
+                                     int64_t n, int Y, float* scratch, void* out, bool accumulate, const float* scale,
+                                     hipStream_t st) {
+  if (nseg < 1 || nseg > kMaxPartSeg || n % 4 != 0 || Y < 1 || reinterpret_cast<uintptr_t>(scratch) % 16 != 0)
+    return hipErrorInvalidValue;
+  PartSegs sg{};
+  for (int k = 0; k < nseg; ++k) {
+    if (lds[k] % 4 != 0 || lds[k] < n || reinterpret_cast<uintptr_t>(ptrs[k]) % 16 != 0) return hipErrorInvalidValue;
+    sg.ptr[k] = ptrs[k];
+    sg.rows[k] = rows[k];
+    sg.ld4[k] = lds[k] / 4;
+  }
+  sg.nseg = nseg;
+  const int64_t blocks = (n / 4 + kTallQ - 1) / kTallQ;
+  if (blocks > 0x7fffffff || Y > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sum_partials_split_kernel, dim3(static_cast<unsigned>(blocks), static_cast<unsigned>(Y)),
+                     dim3(kTallQ * kTallR), 0, st, sg, n, scratch);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  auto O = static_cast<uint16_t*>(out);
+  const dim3 g(grid_for(n / 4, 256)), blk(256);
+  if (accumulate) hipLaunchKernelGGL(sum_partials_kernel<true>, g, blk, 0, st, scratch, Y, n, n, O, scale);
+  else hipLaunchKernelGGL(sum_partials_kernel<false>, g, blk, 0, st, scratch, Y, n, n, O, scale);
   return hipGetLastError();
 }
 

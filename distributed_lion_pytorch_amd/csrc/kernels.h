@@ -57,6 +57,12 @@ hipError_t launch_colsum(const void* x, float* part, int parts, int64_t rows, in
 // out (+)= bf16(sum over every row of up to 16 fp32 stacks [rows_k, >= n] (row stride lds_k))
 hipError_t launch_sum_partials_multi(const float* const* ptrs, const int64_t* rows, const int64_t* lds, int nseg,
                                      int64_t n, void* out, bool accumulate, hipStream_t st);
+// the same over Y row groups: pass 1 into scratch fp32 [Y, n], pass 2 out (+)= bf16(scale * sum) --
+// for narrow tall stacks (few column blocks); Y from sum_partials_split_factor (1 = not worth it)
+int sum_partials_split_factor(int64_t n, int64_t total_rows);
+hipError_t launch_sum_partials_split(const float* const* ptrs, const int64_t* rows, const int64_t* lds, int nseg,
+                                     int64_t n, int Y, float* scratch, void* out, bool accumulate, const float* scale,
+                                     hipStream_t st);
 
 // ---- bf16 GEMM C[M,N] = A[M,K] . B[N,K]^T with fused epilogue (gemm.hip)
 // epi: 0 plain, 1 + bias, 2 aux = z, C = gelu_tanh(z + bias), 3 the same with erf GELU,

@@ -269,3 +269,36 @@ def test_fused_clip_matches_prescaled_grads(dtype, cuda):
     for a, b in zip(ma_enc, ms):
         assert torch.equal(a, b)
     assert torch.equal(bits_a, bits_b)
+
+
+@pytest.mark.parametrize("n,rows,nseg", [(768, 1024, 1), (2304, 1024, 8), (3072, 256, 3), (64, 4096, 2)])
+def test_sum_partials_tall_narrow_stacks(n, rows, nseg, cuda):
+    """Narrow, tall fp32 partial stacks (bias / norm parameter gradients of a
+    fusion window) take the row-split two-pass reduction: bf16 of the fp32 sum,
+    deterministic, accumulate and scaled forms included."""
+    hip.require()
+    ops = hip.ops()
+    torch.manual_seed(0)
+    parts = [torch.randn(rows, n, device=cuda) for _ in range(nseg)]
+    ref = torch.cat(parts).double().sum(0)
+    out = torch.empty(n, device=cuda, dtype=torch.bfloat16)
+    ops.sum_partials_multi_(parts, out, False)
+    assert torch.allclose(out.double(), ref, rtol=1e-2, atol=1e-3 * ref.abs().max().item())
+    out2 = torch.empty_like(out)
+    ops.sum_partials_multi_(parts, out2, False)
+    assert torch.equal(out, out2)
+    acc = torch.ones(n, device=cuda, dtype=torch.bfloat16)
+    ops.sum_partials_multi_(parts, acc, True)
+    assert torch.allclose(acc.double(), ref + 1, rtol=1e-2, atol=1e-3 * ref.abs().max().item())
+    single = ops.sum_partials(parts[0])
+    ref0 = parts[0].double().sum(0)
+    assert torch.allclose(single.double(), ref0, rtol=1e-2, atol=1e-3 * ref0.abs().max().item())
+    s = torch.tensor([0.5], device=cuda)
+    sc = torch.zeros(n, device=cuda, dtype=torch.bfloat16)
+    ops.sum_partials_scaled_(parts[0], s, sc, False)
+    assert torch.allclose(sc.double(), 0.5 * ref0, rtol=1e-2, atol=1e-3 * ref0.abs().max().item())
+    # a row-strided slice (one of the [S, 3, C] norm parameter blocks)
+    wide = torch.randn(rows, 3 * n, device=cuda)
+    sl = wide[:, n:2 * n]
+    assert torch.allclose(ops.sum_partials(sl).double(), sl.double().sum(0), rtol=1e-2,
+                          atol=1e-3 * sl.double().sum(0).abs().max().item())
