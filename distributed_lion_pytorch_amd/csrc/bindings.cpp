@@ -964,9 +964,25 @@ void dequant4_(const Tensor& q, const Tensor& absmax, const Tensor& code, const 
                                    code.data_ptr<float>(), out.data_ptr(), n, cur_stream()),
             "dequant4");
 }
+
+// out [C, Rp] = x [R, C]^T zero-padded to Rp columns (16-bit dtypes; the per-step weight layouts)
+Tensor transpose_pad(const Tensor& x, int64_t rows_out) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1 && x.element_size() == 2,
+              "dlion transpose_pad: x must be a 2-D 16-bit GPU tensor with unit column stride");
+  const int64_t R = x.size(0), C = x.size(1);
+  const int64_t Rp = rows_out < 0 ? R : rows_out;
+  TORCH_CHECK(Rp >= R && Rp % 8 == 0 && x.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "dlion transpose_pad: needs rows_out >= rows, rows_out % 8 == 0, row stride % 8 == 0, 16-byte alignment");
+  const c10::DeviceGuard g(x.device());
+  auto out = at::empty({C, Rp}, x.options());
+  check_hip(dlion::launch_transpose_pad(x.data_ptr(), R, C, x.stride(0), out.data_ptr(), Rp, cur_stream()),
+            "transpose_pad");
+  return out;
+}
 }  // namespace
 
 TORCH_LIBRARY(dlion, m) {
+  m.def("transpose_pad(Tensor x, int rows_out=-1) -> Tensor");
   m.def("quant4(Tensor w, Tensor code) -> (Tensor, Tensor)");
   m.def("dequant4_(Tensor q, Tensor absmax, Tensor code, Tensor(a!) out) -> ()");
   m.def("gemm_tn(Tensor[] P, Tensor[] Q, int splits) -> Tensor");
@@ -1069,4 +1085,5 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("lora_cols", &lora_cols);
   m.impl("quant4", &quant4);
   m.impl("dequant4_", &dequant4_);
+  m.impl("transpose_pad", &transpose_pad);
 }

@@ -380,6 +380,50 @@ __global__ void __launch_bounds__(kTallQ * kTallR) sum_partials_split_kernel(con
   }
 }
 
+// out [C, Rp] = x[R, C]^T, columns R..Rp-1 zero (the per-step transposed / vocab-padded weight
+// copies of the GPT-2 step: ATen's strided copy ran them at 0.2-0.6 TB/s).  64 x 64 tile per
+// 256-thread block through LDS: 16-byte row loads, 2-byte LDS column reads (row pitch 66
+// elements = 33 dwords: the 8 rows a lane gathers fall in distinct banks), 16-byte stores.
+__global__ void __launch_bounds__(256) transpose_pad_kernel(const uint16_t* __restrict__ x, int64_t R, int64_t C,
+                                                            int64_t ldx, uint16_t* __restrict__ out, int64_t Rp) {
+  __shared__ uint16_t tile[64][66];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * 64, c0 = static_cast<int64_t>(blockIdx.x) * 64;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = threadIdx.x + h * 256;  // 512 chunks of 8 elements: 64 rows x 8 chunks
+    const int tr = idx >> 3, tc = (idx & 7) * 8;
+    const int64_t r = r0 + tr, c = c0 + tc;
+    uint16_t v[8];
+    if (r < R && c + 8 <= C) {
+      const uint4 w = *reinterpret_cast<const uint4*>(x + r * ldx + c);
+      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[2 * j] = static_cast<uint16_t>(ws[j] & 0xffffu);
+        v[2 * j + 1] = static_cast<uint16_t>(ws[j] >> 16);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (r < R && c + j < C) ? x[r * ldx + c + j] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[tr][tc + j] = v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = threadIdx.x + h * 256;  // out tile: 64 rows (x columns) x 8 chunks (x rows)
+    const int oc = idx >> 3, orr = (idx & 7) * 8;
+    const int64_t row = c0 + oc, col = r0 + orr;
+    if (row >= C || col >= Rp) continue;
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = static_cast<uint32_t>(tile[orr + 2 * j][oc]) | (static_cast<uint32_t>(tile[orr + 2 * j + 1][oc]) << 16);
+    *reinterpret_cast<uint4*>(out + row * Rp + col) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 static inline int grid_for(int64_t work, int64_t per_block) {
   int64_t g = (work + per_block - 1) / per_block;
   if (g > 2048) g = 2048;
@@ -503,6 +547,19 @@ hipError_t launch_sum_partials_multi(const float* const* ptrs, const int64_t* ro
   auto O = static_cast<uint16_t*>(out);
   if (accumulate) hipLaunchKernelGGL(sum_partials_multi_kernel<true>, g, blk, 0, st, sg, n, O);
   else hipLaunchKernelGGL(sum_partials_multi_kernel<false>, g, blk, 0, st, sg, n, O);
+  return hipGetLastError();
+}
+
+hipError_t launch_transpose_pad(const void* x, int64_t R, int64_t C, int64_t ldx, void* out, int64_t Rp,
+                                hipStream_t st) {
+  if (R <= 0 || C <= 0) return hipSuccess;
+  if (Rp < R || Rp % 8 != 0 || ldx % 8 != 0 || ldx < C || reinterpret_cast<uintptr_t>(x) % 16 != 0 ||
+      reinterpret_cast<uintptr_t>(out) % 16 != 0)
+    return hipErrorInvalidValue;
+  const int64_t gx = (C + 63) / 64, gy = (Rp + 63) / 64;
+  if (gx > 0x7fffffff || gy > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(transpose_pad_kernel, dim3(static_cast<unsigned>(gx), static_cast<unsigned>(gy)), dim3(256), 0, st,
+                     static_cast<const uint16_t*>(x), R, C, ldx, static_cast<uint16_t*>(out), Rp);
   return hipGetLastError();
 }
 

@@ -934,7 +934,9 @@ def _lm_dgrad(g: torch.Tensor, weight: torch.Tensor, wp: torch.Tensor) -> torch.
             and g.numel() < 2**31 and hip.available()):
         from .linear import cached_derived
 
-        wpt = cached_derived(weight, "pad_t", lambda t: _pad_rows(t).t().contiguous())
+        from .linear import fast_transpose
+
+        wpt = cached_derived(weight, "pad_t", lambda t: fast_transpose(t, vp))  # [C, Vp], zero vocab padding
         return hip.ops().gemm_nt(g, wpt, None)
     return g @ wp
 

@@ -601,9 +601,28 @@ def cached_derived(w: torch.Tensor, tag: str, fn) -> torch.Tensor:
     return out
 
 
+_FAST_T = os.environ.get("DLION_FAST_TRANSPOSE", "1") != "0"  # A/B switch
+
+
+def fast_transpose(t: torch.Tensor, rows_out: int | None = None) -> torch.Tensor:
+    """t.t().contiguous() (zero-padded to ``rows_out`` columns if given) -- the
+    LDS-tiled gfx950 kernel for 16-bit GPU matrices (ATen's strided copy ran
+    the GPT-2 per-step weight transposes at 0.2-0.6 TB/s), ATen otherwise."""
+    from . import hip
+
+    rp = t.shape[0] if rows_out is None else rows_out
+    if (_FAST_T and t.is_cuda and t.dim() == 2 and t.element_size() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0
+            and rp % 8 == 0 and t.data_ptr() % 16 == 0 and hip.available()):
+        return hip.ops().transpose_pad(t, rp)
+    out = t.t().contiguous()
+    if rp != t.shape[0]:
+        out = torch.cat([out, out.new_zeros(out.shape[0], rp - t.shape[0])], 1)
+    return out
+
+
 def transposed_weight(w: torch.Tensor) -> torch.Tensor:
     """Contiguous w.t() cached until w changes (next optimizer step)."""
-    return cached_derived(w, "t", lambda t: t.t().contiguous())
+    return cached_derived(w, "t", lambda t: fast_transpose(t))
 
 
 class _LinearKN(torch.autograd.Function):

@@ -302,3 +302,17 @@ def test_sum_partials_tall_narrow_stacks(n, rows, nseg, cuda):
     sl = wide[:, n:2 * n]
     assert torch.allclose(ops.sum_partials(sl).double(), sl.double().sum(0), rtol=1e-2,
                           atol=1e-3 * sl.double().sum(0).abs().max().item())
+
+
+@pytest.mark.parametrize("R,C,Rp,dt", [(768, 3072, 768, torch.bfloat16), (3072, 768, 3072, torch.bfloat16),
+                                        (50257, 768, 50304, torch.bfloat16), (100, 136, 104, torch.float16)])
+def test_transpose_pad(R, C, Rp, dt, cuda):
+    hip.require()
+    x = torch.randn(R, C, device=cuda).to(dt)
+    out = hip.ops().transpose_pad(x, Rp)
+    assert out.shape == (C, Rp)
+    assert torch.equal(out[:, :R], x.t())
+    assert (out[:, R:] == 0).all()
+    # row-strided input (a column slice of a wider matrix)
+    wide = torch.randn(R, C + 16, device=cuda).to(dt)
+    assert torch.equal(hip.ops().transpose_pad(wide[:, :C], Rp)[:, :R], wide[:, :C].t())
