@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.linear import _adjacent_views, autocast_inputs
+from ..ops.linear import _adjacent_views, autocast_inputs, gemm_fwd
 from ..ops.quant import BLOCK, code_tensor, dequantize_4bit, quantize_4bit
 
 
@@ -133,7 +133,7 @@ class _Linear4bitMulti(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2d, bias, *layers):
         W = _dequant_cat(layers, x2d.dtype, x2d.device)
-        y = F.linear(x2d, W, bias)
+        y = F.linear(x2d, W, bias) if bias is not None or not x2d.is_cuda else gemm_fwd(x2d, W)
         del W
         ctx.layers = layers
         ctx.sizes = [l.out_features for l in layers]

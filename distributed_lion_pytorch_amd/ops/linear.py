@@ -625,6 +625,120 @@ def transposed_weight(w: torch.Tensor) -> torch.Tensor:
     return cached_derived(w, "t", lambda t: fast_transpose(t))
 
 
+# ------------------------------------------------ per-shape GEMM choice (Llama sizes)
+# hipBLASLt's first heuristic (what ATen calls) is not the fastest option for
+# every Llama projection, and the input gradient dX = dY.W runs in the NN
+# layout, slower than the NT form against a cached W^T.  Measured at the
+# Llama-2-7B SFT micro-batch (4096 tokens, tools/bench_gemm_llama.py): q/k/v
+# forward 342 (ATen) vs 303 us (own NT), gate/up forward 644 vs 559 (own),
+# q/k/v dgrad 367 (NN) vs 258 (NT), gate/up dgrad 542 vs 471, down dgrad 362
+# vs 272 (own NT) -- ~0.4 ms per layer per micro-batch.  Large GEMMs (>= 2^34
+# FLOP) therefore time their candidates once per shape on first use and keep
+# the fastest.  The NT input-gradient forms need W^T: cached for good for a
+# frozen weight (LoRA bases), rebuilt once per optimizer step for a trainable
+# one -- whose candidates are timed with that transpose included, so they win
+# only if they pay for it within one micro-batch.  DLION_GEMM_AUTOTUNE=0 keeps
+# ATen's choice everywhere.
+_AUTOTUNE = os.environ.get("DLION_GEMM_AUTOTUNE", "1") != "0"
+_TUNE_MIN_FLOP = float(2 ** 34)
+_GEMM_PICK: dict = {}  # key -> candidate name
+
+
+def _own_nt_ok(a: torch.Tensor, b_nk: torch.Tensor) -> bool:
+    return (a.dim() == 2 and b_nk.dim() == 2 and a.shape[1] == b_nk.shape[1] and a.shape[1] % 128 == 0
+            and b_nk.shape[0] % 8 == 0 and a.stride(1) == 1 and a.stride(0) % 8 == 0 and b_nk.is_contiguous()
+            and a.data_ptr() % 16 == 0 and b_nk.data_ptr() % 16 == 0 and a.shape[0] * a.stride(0) < 2 ** 31
+            and b_nk.numel() < 2 ** 31)
+
+
+def _nt_candidates(a: torch.Tensor, b_nk: torch.Tensor, prefix: str) -> dict:
+    """a @ b_nk^T implementations (bf16, a [M, K], b_nk [N, K])."""
+    from . import hip
+
+    F = torch.nn.functional
+    c = {prefix + "aten": lambda: F.linear(a, b_nk)}
+    if _own_nt_ok(a, b_nk):
+        c[prefix + "own"] = lambda: hip.ops().gemm_nt(a, b_nk, None)
+
+    def lt():
+        out = torch.empty(a.shape[0], b_nk.shape[0], dtype=a.dtype, device=a.device)
+        if not hip.ops().lt_gemm_nt(a, b_nk, None, 0, out):
+            return F.linear(a, b_nk)
+        return out
+
+    if a.stride(1) == 1 and b_nk.is_contiguous():
+        c[prefix + "lt"] = lt
+    return c
+
+
+def _pick(key, cands: dict) -> str:
+    name = _GEMM_PICK.get(key)
+    if name is not None and name in cands:
+        return name
+    best, best_t = None, None
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for n, fn in cands.items():
+        try:
+            fn()  # warm-up (also tunes lt_gemm's algorithm for the shape)
+            ev0.record()
+            for _ in range(3):
+                fn()
+            ev1.record()
+            ev1.synchronize()
+            t = ev0.elapsed_time(ev1)
+        except RuntimeError:
+            continue
+        if best_t is None or t < best_t:
+            best, best_t = n, t
+    _GEMM_PICK[key] = best
+    return best
+
+
+def _tunable(a: torch.Tensor, M: int, N: int, K: int) -> bool:
+    from . import hip
+
+    return (_AUTOTUNE and a.is_cuda and a.dtype == torch.bfloat16 and 2.0 * M * N * K >= _TUNE_MIN_FLOP
+            and not torch.cuda.is_current_stream_capturing() and hip.available())
+
+
+def gemm_fwd(x2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """x2d @ w^T (w [N, K], nn.Linear layout): ATen, or the measured-fastest
+    of ATen / own NT / tuned hipBLASLt for large bf16 shapes."""
+    M, K = x2d.shape
+    N = w.shape[0]
+    if not (_tunable(x2d, M, N, K) and w.dtype == torch.bfloat16):
+        return torch.nn.functional.linear(x2d, w)
+    cands = _nt_candidates(x2d, w, "")
+    key = ("fwd", M, N, K, x2d.stride(0))
+    return cands[_pick(key, cands)]()
+
+
+def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, frozen: bool) -> torch.Tensor:
+    """dy @ w (w [N, K]): the NN product, or for frozen weights the measured-
+    fastest NT form against a cached w^T [K, N]."""
+    M, N = dy.shape
+    K = w.shape[1]
+    if not (_tunable(dy, M, N, K) and w.dtype == torch.bfloat16 and w.dim() == 2):
+        return dy @ w
+    key = ("dgrad", M, N, K, dy.stride(0), frozen)
+    name = _GEMM_PICK.get(key)
+    if name == "nn":
+        return dy @ w
+    if name is None:
+        # time the NT forms with the transpose included for a trainable weight (its W^T is
+        # rebuilt once per optimizer step, i.e. at most once per micro-batch)
+        timed = {"nn": lambda: dy @ w}
+        wt_t = cached_derived(w, "t", lambda t: fast_transpose(t)) if frozen else None
+        probe = _nt_candidates(dy, wt_t if frozen else fast_transpose(w), "nt_")
+        for n in probe:
+            timed[n] = probe[n] if frozen else (lambda n=n: _nt_candidates(dy, fast_transpose(w), "nt_")[n]())
+        name = _pick(key, timed)
+        if name == "nn":
+            return dy @ w
+    wt = cached_derived(w, "t", lambda t: fast_transpose(t))  # frozen: for good; trainable: per step
+    return _nt_candidates(dy, wt, "nt_")[name]()
+
+
 class _LinearKN(torch.autograd.Function):
     """y = x @ W + b with W stored [K, N] (HF Conv1D layout)."""
 
@@ -666,13 +780,16 @@ class _LinearNK(torch.autograd.Function):
         ctx.param = w if ctx.fuse else None
         ctx.fuse_b = b is not None and _fuse_target(b)
         ctx.bias = b if ctx.fuse_b else None
+        ctx.w = w  # the weight object itself (the W^T cache key; saved_tensors may be an alias)
+        if b is None:
+            return gemm_fwd(x2d, w)
         return torch.nn.functional.linear(x2d, w, b)
 
     @staticmethod
     def backward(ctx, dy):
         x2d, w = ctx.saved_tensors
         dy = dy.contiguous()
-        dx = dy @ w if ctx.needs_input_grad[0] else None
+        dx = gemm_dgrad(dy, ctx.w, not ctx.w.requires_grad) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
             if ctx.fuse:
@@ -757,8 +874,9 @@ class _LinearMultiNK(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2d, *ws):
         sizes = [w.shape[0] for w in ws]
-        y = torch.nn.functional.linear(x2d, cat_weights(ws))
+        y = gemm_fwd(x2d, cat_weights(ws))
         ctx.save_for_backward(x2d, *ws)
+        ctx.ws = ws  # the weight objects (cat / W^T cache keys; saved_tensors may be aliases)
         ctx.sizes = sizes
         ctx.fuse = [_fuse_target(w) for w in ws]
         ctx.params = [w if f else None for w, f in zip(ws, ctx.fuse)]
@@ -773,7 +891,9 @@ class _LinearMultiNK(torch.autograd.Function):
         if dy is None:
             dy = torch.cat([g.reshape(-1, g.shape[-1]) for g in grads], -1)
         dy = dy.reshape(-1, dy.shape[-1])
-        dx = dy @ cat_weights(ws) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm_dgrad(dy, cat_weights(ctx.ws), not any(w.requires_grad for w in ctx.ws))
         dws = [None] * len(ws)
         want = [ctx.needs_input_grad[1 + i] for i in range(len(ws))]
         if any(want):

@@ -211,3 +211,37 @@ def test_cat_weights_refreshes_in_place_after_step(cuda):
     L.bump_weight_generation()
     c2 = L.cat_weights(ws)
     assert c2.data_ptr() == ptr and torch.equal(c2, torch.cat([w.detach() for w in ws]))
+
+
+def test_gemm_autotune_candidates_agree(cuda):
+    """Every candidate the per-shape GEMM choice may pick (ATen NN/NT, own NT,
+    tuned hipBLASLt) computes the same product; the pick is cached per shape."""
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    torch.manual_seed(5)
+    M, N, K = 4096, 4096, 1536
+    x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=cuda) * 0.02).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    for name, fn in L._nt_candidates(x, w, "").items():
+        assert (fn().float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item(), name
+    y = L.gemm_fwd(x, w)
+    assert ("fwd", M, N, K, x.stride(0)) in L._GEMM_PICK
+    assert (y.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+    dy = torch.randn(M, N, device=cuda, dtype=torch.bfloat16)
+    dref = dy.float() @ w.float()
+    for frozen in (True, False):
+        dx = L.gemm_dgrad(dy, w, frozen)
+        assert (dx.float() - dref).abs().max().item() <= 2e-2 * dref.abs().max().item()
+    assert ("dgrad", M, N, K, dy.stride(0), False) in L._GEMM_PICK
+    # a trainable weight's W^T follows the weight across an optimizer step
+    wp = torch.nn.Parameter(w.clone())
+    L._GEMM_PICK[("dgrad", M, N, K, dy.stride(0), False)] = "nt_aten"
+    d1 = L.gemm_dgrad(dy, wp, False)
+    with torch.no_grad():
+        wp.mul_(-1.0)
+    L.bump_weight_generation()
+    d2 = L.gemm_dgrad(dy, wp, False)
+    assert (d2.float() + dref).abs().max().item() <= 2e-2 * dref.abs().max().item()  # the new weight's W^T
+    assert (d1.float() - dref).abs().max().item() <= 2e-2 * dref.abs().max().item()
