@@ -19,6 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from . import hip
+from .linear import gemm_fwd
 
 _IMPL = {"mode": os.environ.get("DLION_FUSED_IMPL", "auto")}  # auto | torch | hip
 
@@ -456,7 +457,7 @@ class _MLP(torch.autograd.Function):
         ctx.wparams = (w_fc, w_proj)
         ctx.fused_b = _fused_params(b_fc)[0]
         wp_t = transposed_weight(w_proj) if isinstance(w_proj, torch.nn.Parameter) else w_proj.t()
-        return F.linear(h, wp_t)
+        return gemm_fwd(h, wp_t)
 
     @staticmethod
     def backward(ctx, dy):
@@ -473,7 +474,7 @@ class _MLP(torch.autograd.Function):
             dz, part = hip.ops().bias_gelu_bwd(dy @ w_proj.t(), z, b_fc, ctx.exact, max(1, min(1024, z.shape[0] // 8)))
         grads = [None] * 5
         if ctx.needs_input_grad[0]:
-            grads[0] = F.linear(dz, w_fc)  # dx = dz . Wfc^T, Wfc stored [C, 4C]
+            grads[0] = gemm_fwd(dz, w_fc)  # dx = dz . Wfc^T, Wfc stored [C, 4C]
         for i, (w, a, g) in ((1, (ctx.wparams[0], x, dz)), (3, (ctx.wparams[1], h, dy))):
             if ctx.needs_input_grad[i]:
                 if ctx.fuse[(i - 1) // 2]:
@@ -651,7 +652,7 @@ class _QKVAttention(torch.autograd.Function):
         C3 = w.shape[1]
         D = C3 // (3 * H)
         wt = transposed_weight(w) if isinstance(w, torch.nn.Parameter) else w.t()
-        qkv = F.linear(x2d, wt, b).view(B, T, 3, H, D)
+        qkv = gemm_fwd(x2d, wt, b).view(B, T, 3, H, D)
         out, lse = hip.ops().attn_fwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], p, seed)
         ctx.save_for_backward(x2d, w, qkv, out, lse)
         ctx.p, ctx.seed = p, seed
@@ -672,7 +673,7 @@ class _QKVAttention(torch.autograd.Function):
         hip.ops().attn_bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], out, dout, lse, ctx.p, ctx.seed,
                            dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], part)
         g = dqkv.view(B * T, -1)
-        dx = g @ w.t() if ctx.needs_input_grad[0] else None
+        dx = gemm_fwd(g, w) if ctx.needs_input_grad[0] else None  # g @ W^T, W [C, 3C]
         dw = db = None
         if ctx.needs_input_grad[1]:
             if ctx.fuse:
@@ -972,7 +973,7 @@ class _LMHeadCE(torch.autograd.Function):
         v = weight.shape[0]
         need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         wp = _pad_rows(weight)
-        logits = h2d @ wp.t()  # [N, Vp] in the compute dtype (hipBLASLt)
+        logits = gemm_fwd(h2d, wp)  # [N, Vp] in the compute dtype
         if normalizer is None:
             n_valid = (labels1d != -100).sum().clamp_min(1).to(torch.float32)
         else:

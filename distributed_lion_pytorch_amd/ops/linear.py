@@ -651,22 +651,23 @@ def _own_nt_ok(a: torch.Tensor, b_nk: torch.Tensor) -> bool:
             and b_nk.numel() < 2 ** 31)
 
 
-def _nt_candidates(a: torch.Tensor, b_nk: torch.Tensor, prefix: str) -> dict:
-    """a @ b_nk^T implementations (bf16, a [M, K], b_nk [N, K])."""
+def _nt_candidates(a: torch.Tensor, b_nk: torch.Tensor, prefix: str, bias=None) -> dict:
+    """a @ b_nk^T (+ bias) implementations (bf16, a [M, K], b_nk [N, K])."""
     from . import hip
 
     F = torch.nn.functional
-    c = {prefix + "aten": lambda: F.linear(a, b_nk)}
-    if _own_nt_ok(a, b_nk):
-        c[prefix + "own"] = lambda: hip.ops().gemm_nt(a, b_nk, None)
+    c = {prefix + "aten": lambda: F.linear(a, b_nk, bias)}
+    bias_ok = bias is None or (bias.is_contiguous() and bias.dtype == a.dtype and bias.data_ptr() % 16 == 0)
+    if _own_nt_ok(a, b_nk) and bias_ok:
+        c[prefix + "own"] = lambda: hip.ops().gemm_nt(a, b_nk, bias)
 
     def lt():
         out = torch.empty(a.shape[0], b_nk.shape[0], dtype=a.dtype, device=a.device)
-        if not hip.ops().lt_gemm_nt(a, b_nk, None, 0, out):
-            return F.linear(a, b_nk)
+        if not hip.ops().lt_gemm_nt(a, b_nk, bias, 0 if bias is None else 1, out):
+            return F.linear(a, b_nk, bias)
         return out
 
-    if a.stride(1) == 1 and b_nk.is_contiguous():
+    if a.stride(1) == 1 and b_nk.is_contiguous() and bias_ok:
         c[prefix + "lt"] = lt
     return c
 
@@ -701,15 +702,16 @@ def _tunable(a: torch.Tensor, M: int, N: int, K: int) -> bool:
             and not torch.cuda.is_current_stream_capturing() and hip.available())
 
 
-def gemm_fwd(x2d: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """x2d @ w^T (w [N, K], nn.Linear layout): ATen, or the measured-fastest
-    of ATen / own NT / tuned hipBLASLt for large bf16 shapes."""
+def gemm_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
+    """x2d @ w^T (+ bias) (w [N, K], nn.Linear layout; also any NT product,
+    e.g. an HF Conv1D input gradient dy @ W^T): ATen, or the measured-fastest of
+    ATen / own NT / tuned hipBLASLt for large bf16 shapes."""
     M, K = x2d.shape
     N = w.shape[0]
-    if not (_tunable(x2d, M, N, K) and w.dtype == torch.bfloat16):
-        return torch.nn.functional.linear(x2d, w)
-    cands = _nt_candidates(x2d, w, "")
-    key = ("fwd", M, N, K, x2d.stride(0))
+    if not (_tunable(x2d, M, N, K) and w.dtype == torch.bfloat16 and w.dim() == 2):
+        return torch.nn.functional.linear(x2d, w, bias)
+    cands = _nt_candidates(x2d, w, "", bias)
+    key = ("fwd", M, N, K, x2d.stride(0), w.stride(0), bias is not None)
     return cands[_pick(key, cands)]()
 
 
@@ -751,14 +753,14 @@ class _LinearKN(torch.autograd.Function):
         ctx.fuse_b = b is not None and _fuse_target(b)
         ctx.bias = b if ctx.fuse_b else None
         if isinstance(w, torch.nn.Parameter) and x2d.dtype in (torch.bfloat16, torch.float16):
-            return torch.nn.functional.linear(x2d, transposed_weight(w), b)
+            return gemm_fwd(x2d, transposed_weight(w), b)
         return torch.addmm(b, x2d, w) if b is not None else x2d @ w
 
     @staticmethod
     def backward(ctx, dy):
         x2d, w = ctx.saved_tensors
         dy = dy.contiguous()
-        dx = dy @ w.t() if ctx.needs_input_grad[0] else None
+        dx = gemm_fwd(dy, w) if ctx.needs_input_grad[0] else None  # dy @ W^T, W [K, N]: an NT product
         dw = None
         if ctx.needs_input_grad[1]:
             if ctx.fuse:

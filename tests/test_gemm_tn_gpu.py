@@ -227,7 +227,7 @@ def test_gemm_autotune_candidates_agree(cuda):
     for name, fn in L._nt_candidates(x, w, "").items():
         assert (fn().float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item(), name
     y = L.gemm_fwd(x, w)
-    assert ("fwd", M, N, K, x.stride(0)) in L._GEMM_PICK
+    assert ("fwd", M, N, K, x.stride(0), w.stride(0), False) in L._GEMM_PICK
     assert (y.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
     dy = torch.randn(M, N, device=cuda, dtype=torch.bfloat16)
     dref = dy.float() @ w.float()
