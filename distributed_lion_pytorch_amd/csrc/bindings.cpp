@@ -979,9 +979,29 @@ Tensor transpose_pad(const Tensor& x, int64_t rows_out) {
             "transpose_pad");
   return out;
 }
+
+// out [K, N] (a 2-D view, unit column stride, any row stride: e.g. a column block of a
+// concatenated W^T) = W^T of the 4-bit W [N, K]
+void dequant4_t_(const Tensor& q, const Tensor& absmax, const Tensor& code, const Tensor& out) {
+  check_dev(q, "q");
+  check_dev(absmax, "absmax");
+  check_dev(code, "code");
+  TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.stride(1) == 1 && out.element_size() == 2,
+              "dlion dequant4_t: out must be a 2-D 16-bit GPU view with unit column stride");
+  const int64_t K = out.size(0), N = out.size(1);
+  TORCH_CHECK(q.scalar_type() == at::kByte && q.numel() * 2 == N * K && absmax.numel() * 64 == N * K &&
+                  code.numel() == 16 && code.scalar_type() == at::kFloat,
+              "dlion dequant4_t: q / absmax do not match out");
+  const c10::DeviceGuard g(out.device());
+  check_hip(dlion::launch_dequant4_t(dtype_code(out.scalar_type()), q.data_ptr<uint8_t>(), absmax.data_ptr<float>(),
+                                     code.data_ptr<float>(), out.data_ptr(), static_cast<int>(N), static_cast<int>(K),
+                                     out.stride(0), cur_stream()),
+            "dequant4_t");
+}
 }  // namespace
 
 TORCH_LIBRARY(dlion, m) {
+  m.def("dequant4_t_(Tensor q, Tensor absmax, Tensor code, Tensor(a!) out) -> ()");
   m.def("transpose_pad(Tensor x, int rows_out=-1) -> Tensor");
   m.def("quant4(Tensor w, Tensor code) -> (Tensor, Tensor)");
   m.def("dequant4_(Tensor q, Tensor absmax, Tensor code, Tensor(a!) out) -> ()");
@@ -1085,5 +1105,6 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("lora_cols", &lora_cols);
   m.impl("quant4", &quant4);
   m.impl("dequant4_", &dequant4_);
+  m.impl("dequant4_t_", &dequant4_t_);
   m.impl("transpose_pad", &transpose_pad);
 }

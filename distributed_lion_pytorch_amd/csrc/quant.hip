@@ -95,6 +95,57 @@ __global__ __launch_bounds__(kThreads) void dequant4_kernel(const uint32_t* __re
   }
 }
 
+// Transposed expansion for the input-gradient GEMM (dX = dY . W as the NT
+// product against W^T): out[k, n] (row stride ldo) = code[q(n, k)] * absmax,
+// for W [N, K] stored as above.  64 x 64 tile per 256-thread block: 128
+// threads each expand 16 packed bytes (32 elements of one row) into an LDS
+// tile of 16-bit values, then every thread gathers 2 x 8 tile-column values
+// into 16-byte stores of the transposed rows.  N % 64 == K % 64 == 0.
+template <int DT>
+__global__ __launch_bounds__(kThreads) void dequant4_t_kernel(const uint4* __restrict__ q,
+                                                              const float* __restrict__ absmax,
+                                                              const float* __restrict__ code,
+                                                              uint16_t* __restrict__ out, int N, int K, int64_t ldo) {
+  __shared__ float2 tab[256];
+  __shared__ uint16_t tile[64][66];
+  tab[threadIdx.x] = make_float2(code[threadIdx.x >> 4], code[threadIdx.x & 15]);
+  __syncthreads();
+  const int n0 = blockIdx.y * 64, k0 = blockIdx.x * 64;
+  if (threadIdx.x < 128) {
+    const int nl = threadIdx.x >> 1, half = threadIdx.x & 1;
+    const int64_t e = static_cast<int64_t>(n0 + nl) * K + k0 + half * 32;  // first element of the 32
+    const uint4 w = q[e / 32];
+    const float s = absmax[e / kQBlock];
+    const uint32_t words[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float2 c = tab[(words[k] >> (8 * b)) & 0xffu];
+        const int col = half * 32 + k * 8 + b * 2;
+        if constexpr (DT == kBF16) {
+          tile[nl][col] = __builtin_bit_cast(uint16_t, static_cast<__bf16>(c.x * s));
+          tile[nl][col + 1] = __builtin_bit_cast(uint16_t, static_cast<__bf16>(c.y * s));
+        } else {
+          tile[nl][col] = f32_to_f16(c.x * s);
+          tile[nl][col + 1] = f32_to_f16(c.y * s);
+        }
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = threadIdx.x + h * kThreads;  // 64 output rows (k) x 8 chunks of 8 n
+    const int kl = idx >> 3, nb = (idx & 7) * 8;
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      v[j] = static_cast<uint32_t>(tile[nb + 2 * j][kl]) | (static_cast<uint32_t>(tile[nb + 2 * j + 1][kl]) << 16);
+    *reinterpret_cast<uint4*>(out + static_cast<int64_t>(k0 + kl) * ldo + n0 + nb) = make_uint4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 // One thread per 64-element block: absmax, then the nearest codebook entry
 // per element (first minimum on ties, the torch.argmin rule of the oracle).
 template <int DT>
@@ -163,6 +214,28 @@ hipError_t launch_dequant4(int dt, const uint8_t* q, const float* absmax, const 
       break;
     case kF32:
       dequant4_kernel<kF32><<<grid, kThreads, 0, st>>>(qv, absmax, code, static_cast<float*>(out), words);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_dequant4_t(int dt, const uint8_t* q, const float* absmax, const float* code, void* out, int N, int K,
+                             int64_t ldo, hipStream_t st) {
+  if (N <= 0 || K <= 0) return hipSuccess;
+  if (N % 64 || K % 64 || ldo < N || ldo % 8 || reinterpret_cast<uintptr_t>(out) % 16 ||
+      reinterpret_cast<uintptr_t>(q) % 16)
+    return hipErrorInvalidValue;
+  const dim3 grid(K / 64, N / 64);
+  if (grid.y > 65535) return hipErrorInvalidValue;
+  const uint4* qv = reinterpret_cast<const uint4*>(q);
+  switch (dt) {
+    case kBF16:
+      dequant4_t_kernel<kBF16><<<grid, kThreads, 0, st>>>(qv, absmax, code, static_cast<uint16_t*>(out), N, K, ldo);
+      break;
+    case kF16:
+      dequant4_t_kernel<kF16><<<grid, kThreads, 0, st>>>(qv, absmax, code, static_cast<uint16_t*>(out), N, K, ldo);
       break;
     default:
       return hipErrorInvalidValue;

@@ -124,6 +124,24 @@ def _dequant_cat(layers, dtype, device) -> torch.Tensor:
     return W
 
 
+def _transposed_ok(layers, dy) -> bool:
+    return (dy.is_cuda and dy.dtype in (torch.bfloat16, torch.float16)
+            and all(l.in_features % 64 == 0 and l.out_features % 64 == 0 for l in layers))
+
+
+def _dequant_cat_t(layers, dtype, device) -> torch.Tensor:
+    """[W1; W2; ...]^T = [W1^T | W2^T | ...] ([K, sum N]) expanded from 4 bits."""
+    from ..ops import hip
+
+    K = layers[0].in_features
+    Wt = torch.empty(K, sum(l.out_features for l in layers), dtype=dtype, device=device)
+    off = 0
+    for l in layers:
+        hip.ops().dequant4_t_(l.qweight, l.absmax, l.quant_map, Wt[:, off:off + l.out_features])
+        off += l.out_features
+    return Wt
+
+
 class _Linear4bitMulti(torch.autograd.Function):
     """[y1 | y2 | ...] = x @ [W1; W2; ...]^T (+ b for one layer) with the 4-bit
     weights expanded into one transient buffer; backward re-expands it for
@@ -151,7 +169,12 @@ class _Linear4bitMulti(torch.autograd.Function):
         dy = dy.reshape(-1, dy.shape[-1])
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = dy @ _dequant_cat(ctx.layers, dy.dtype, dy.device)
+            if _transposed_ok(ctx.layers, dy):
+                # dX = dY . W as the NT product against W^T, expanded straight into the transposed
+                # layout (csrc/quant.hip dequant4_t): no NN GEMM, no transpose pass
+                dx = gemm_fwd(dy, _dequant_cat_t(ctx.layers, dy.dtype, dy.device))
+            else:
+                dx = dy @ _dequant_cat(ctx.layers, dy.dtype, dy.device)
         db = dy.sum(0) if ctx.has_bias and ctx.needs_input_grad[1] else None
         return (dx, db) + (None,) * len(ctx.layers)
 

@@ -99,3 +99,18 @@ def test_qlora_llama_gpu_matches_dequantized(cuda):
         if p.requires_grad:
             gr = byname[n].grad.float()
             assert (p.grad.float() - gr).abs().max().item() <= 5e-2 * gr.abs().max().item() + 1e-6, n
+
+
+def test_dequant4_transposed_into_column_blocks(cuda):
+    """The transposed expansion (input-gradient GEMM layout) equals the plain
+    one transposed, written into a column block of a concatenated W^T."""
+    hip.require()
+    torch.manual_seed(1)
+    code = code_tensor("nf4", cuda)
+    w = torch.randn(1024, 768, device=cuda, dtype=torch.bfloat16)
+    q, a = quantize_4bit(w, code)
+    full = dequantize_4bit(q, a, code, w.shape, torch.bfloat16)
+    big = torch.full((768, 3 * 1024), 5.0, device=cuda, dtype=torch.bfloat16)
+    hip.ops().dequant4_t_(q, a, code, big[:, 1024:2048])
+    assert torch.equal(big[:, 1024:2048], full.t())
+    assert (big[:, :1024] == 5).all() and (big[:, 2048:] == 5).all()
