@@ -24,6 +24,8 @@
 // a range of rows; the waves split the rows, batch 4 rows of loads at a time,
 // and reduce through LDS into one partial per block.  (tools/bench_lora.py
 // times each kernel.)
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dlion {
@@ -147,21 +149,29 @@ __global__ void __launch_bounds__(256) lora_up_kernel(const uint16_t* __restrict
 #pragma unroll
     for (int j = 0; j < R; j += 8) lora_ld16(b + static_cast<int64_t>(c + e) * R + j, &bp[e][j / 2]);
   for (int64_t tb = t0; tb < t1; tb += RB) {
-    float ov[RB][8];
+    // the batch's o rows stay packed bf16 (4 VGPRs a row) so that all RB
+    // 16-byte loads are in flight at once (the kernel is latency-bound: 4 rows
+    // per batch ran at 2.4 TB/s)
+    uint4 raw[RB];
 #pragma unroll
     for (int q = 0; q < RB; ++q)
-      if (tb + q < t1) Elem<kBF16>::load8(o + (tb + q) * ldo + c, ov[q]);
+      if (tb + q < t1) raw[q] = *reinterpret_cast<const uint4*>(o + (tb + q) * ldo + c);
 #pragma unroll
     for (int q = 0; q < RB; ++q) {
       const int64_t t = tb + q;
       if (t < t1) {
+        float ov[8];
+        Elem<kBF16>::load8(reinterpret_cast<const uint16_t*>(&raw[q]), ov);
         uint32_t up[R / 2];
 #pragma unroll
         for (int j = 0; j < R; j += 8) lora_ld16(u + t * R + j, &up[j / 2]);
+        lora_bf16x8 ob;
 #pragma unroll
-        for (int e = 0; e < 8; ++e)  // + the bf16 adapter output, as the unfused add sees it
-          ov[q][e] += bf16_to_f32(f32_to_bf16(lora_dot<R>(bp[e], up) * s));
-        Elem<kBF16>::store8(out + t * N + c, ov[q]);
+        for (int e = 0; e < 8; ++e) {  // + the bf16 adapter output, as the unfused add sees it
+          const float a = static_cast<float>(static_cast<__bf16>(lora_dot<R>(bp[e], up) * s));
+          ob[e] = static_cast<__bf16>(ov[e] + a);  // v_cvt_pk_bf16_f32 (RNE)
+        }
+        *reinterpret_cast<lora_bf16x8*>(out + t * N + c) = ob;
       }
     }
   }
@@ -324,9 +334,19 @@ hipError_t launch_lora_up(const void* o, int64_t ldo, const void* u, const void*
   const int rpt = 16;
   const int64_t threads = ((rows + rpt - 1) / rpt) * (N / 8);
   const dim3 grid(static_cast<unsigned>((threads + 255) / 256)), block(256);
-  LORA_R_DISPATCH(r, hipLaunchKernelGGL((lora_up_kernel<R, 4>), grid, block, 0, st, static_cast<const uint16_t*>(o), ldo,
-                                        static_cast<const uint16_t*>(u), static_cast<const uint16_t*>(b),
-                                        static_cast<uint16_t*>(out), rows, N, rpt, s));
+  static const bool shallow = [] {  // A/B switch: DLION_LORA_UP_RB=4 restores the 4-row load batches
+    const char* e = std::getenv("DLION_LORA_UP_RB");
+    return e != nullptr && e[0] == '4';
+  }();
+  if (shallow) {
+    LORA_R_DISPATCH(r, hipLaunchKernelGGL((lora_up_kernel<R, 4>), grid, block, 0, st, static_cast<const uint16_t*>(o),
+                                          ldo, static_cast<const uint16_t*>(u), static_cast<const uint16_t*>(b),
+                                          static_cast<uint16_t*>(out), rows, N, rpt, s));
+  } else {
+    LORA_R_DISPATCH(r, hipLaunchKernelGGL((lora_up_kernel<R, 8>), grid, block, 0, st, static_cast<const uint16_t*>(o),
+                                          ldo, static_cast<const uint16_t*>(u), static_cast<const uint16_t*>(b),
+                                          static_cast<uint16_t*>(out), rows, N, rpt, s));
+  }
   return hipGetLastError();
 }
 
