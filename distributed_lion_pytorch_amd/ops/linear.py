@@ -691,6 +691,8 @@ def _pick(key, cands: dict) -> str:
             continue
         if best_t is None or t < best_t:
             best, best_t = n, t
+    if best is None:  # nothing ran: the first candidate (ATen) raises its own error when called
+        best = next(iter(cands))
     _GEMM_PICK[key] = best
     return best
 
