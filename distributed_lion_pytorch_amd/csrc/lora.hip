@@ -184,13 +184,13 @@ __global__ void __launch_bounds__(256) lora_up_kernel(const uint16_t* __restrict
 // A lane owns 8 columns (16-byte loads: 8-byte lanes measured 1.6x slower); a
 // 4-wave block owns 512 columns, its waves take alternate batches of RB rows,
 // and the four partial sums meet in LDS.
-template <int R, int MODE>
+template <int R, int MODE, int RB = 4>
 __global__ void __launch_bounds__(256) lora_cols_kernel(const uint16_t* __restrict__ g, int64_t ldg,
                                                         const uint16_t* __restrict__ y, const uint16_t* __restrict__ a,
                                                         uint16_t* __restrict__ dx, float* __restrict__ part,
                                                         int64_t rows, int N, int rpp, float yscale, uint32_t seed,
                                                         uint32_t thresh16, float inv_keep) {
-  constexpr int RB = 4;  // rows per load batch
+  // RB rows per load batch per wave (packed bf16 until used)
   __shared__ float red[3][32][64];
   const int cblocks = (N + 511) / 512;
   const int p = blockIdx.x / cblocks;
@@ -256,7 +256,10 @@ __global__ void __launch_bounds__(256) lora_cols_kernel(const uint16_t* __restri
               d[e] = keep ? lora_dot<R>(yp[q], ap[e]) * inv_keep : 0.f;
               gv[e] = keep ? gv[e] * inv_keep : 0.f;
             }
-            Elem<kBF16>::store8(dx + t * N + c, d);
+            lora_bf16x8 db;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) db[e] = static_cast<__bf16>(d[e]);  // v_cvt_pk_bf16_f32 (RNE)
+            *reinterpret_cast<lora_bf16x8*>(dx + t * N + c) = db;
           }
         }
 #pragma unroll
@@ -369,7 +372,7 @@ hipError_t launch_lora_cols(const void* g, int64_t ldg, const void* y, const voi
   auto Y = static_cast<const uint16_t*>(y);
   auto A = static_cast<const uint16_t*>(a);
   auto DX = static_cast<uint16_t*>(dx);
-  if (mode == 0) {
+  if (mode == 0) {  // 8-row batches measured neutral at the SFT shape (profiles/r2/lora_up_rb_ab.txt)
     LORA_R_DISPATCH(r, hipLaunchKernelGGL((lora_cols_kernel<R, 0>), grid, block, 0, st, G, ldg, Y, A, DX, part, rows, N,
                                           rpp, yscale, seed, thresh16, inv_keep));
   } else {
