@@ -504,6 +504,32 @@ def split_k_factor(M: int, K: int, N: int) -> int:
     return s
 
 
+def _unsplit_wgrad(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool) -> None:
+    """out [K, N] bf16 (+)= a^T b unsplit: the own TN kernel's bf16 epilogue, or
+    hipBLASLt's TN GEMM (beta = 1 to accumulate) where the per-shape timing
+    (see gemm_fwd) finds it faster.  Both round the fp32 sum (+ out) once."""
+    from . import hip
+
+    M, K = a.shape
+    N = b.shape[1]
+    out2 = out.view(K, N)
+    if _tunable(a, M, N, K):
+        key = ("wgrad", M, K, N, a.stride(0), b.stride(0))
+        name = _GEMM_PICK.get(key)
+        if name is None:
+            scratch = torch.empty(K, N, dtype=out.dtype, device=out.device)
+            name = _pick(key, {"tn": lambda: hip.ops().gemm_tn_([a], [b], scratch, False),
+                               "blas": lambda: torch.mm(a.t(), b, out=scratch)})
+            del scratch
+        if name == "blas":
+            if accumulate:
+                out2.addmm_(a.t(), b)
+            else:
+                torch.mm(a.t(), b, out=out2)
+            return
+    hip.ops().gemm_tn_([a], [b], out, accumulate)
+
+
 def wgrad_into(a: torch.Tensor, b: torch.Tensor, w: torch.nn.Parameter) -> None:
     """w.grad (+)= a^T @ b, deposited in place (a [M, K], b [M, N], w [K, N])."""
     g = w.grad
@@ -524,9 +550,9 @@ def wgrad_into(a: torch.Tensor, b: torch.Tensor, w: torch.nn.Parameter) -> None:
                 # unsplit: the TN kernel writes (adds onto) the bf16 gradient itself
                 if g is None:
                     w.grad = g = torch.empty_like(w, memory_format=torch.contiguous_format)
-                    hip.ops().gemm_tn_([a], [b], g, False)
+                    _unsplit_wgrad(a, b, g, False)
                 else:
-                    hip.ops().gemm_tn_([a], [b], g, True)
+                    _unsplit_wgrad(a, b, g, True)
                 return
             if grad_ok:
                 part = wgrad_partials(a, b, s).view(s, K * N)
@@ -938,7 +964,7 @@ def _multi_wgrad_into(dy, x2d, params, sizes) -> None:
                 gs = [p.grad for p in params]
                 if all(g is None for g in gs):  # one buffer; each grad is a row block of it
                     buf = torch.empty(N, K, dtype=torch.bfloat16, device=dy.device)
-                    hip.ops().gemm_tn_([dy], [x2d], buf, False)
+                    _unsplit_wgrad(dy, x2d, buf, False)
                     off = 0
                     for p, n in zip(params, sizes):
                         p.grad = buf[off:off + n].view_as(p)
@@ -946,7 +972,7 @@ def _multi_wgrad_into(dy, x2d, params, sizes) -> None:
                     return
                 base = _adjacent_rows(gs) if all(g is not None for g in gs) else None
                 if base is not None and base.dtype == torch.bfloat16 and base.is_contiguous():
-                    hip.ops().gemm_tn_([dy], [x2d], base, True)
+                    _unsplit_wgrad(dy, x2d, base, True)
                     return
             flat = wgrad_partials(dy, x2d, s).view(s, N * K)
             off = 0

@@ -245,3 +245,23 @@ def test_gemm_autotune_candidates_agree(cuda):
     d2 = L.gemm_dgrad(dy, wp, False)
     assert (d2.float() + dref).abs().max().item() <= 2e-2 * dref.abs().max().item()  # the new weight's W^T
     assert (d1.float() - dref).abs().max().item() <= 2e-2 * dref.abs().max().item()
+
+
+@pytest.mark.parametrize("choice", ["tn", "blas"])
+def test_unsplit_wgrad_choices(cuda, choice):
+    """Both candidates of the unsplit weight gradient (own TN bf16 epilogue,
+    hipBLASLt TN with beta = 1) write and accumulate the same gradient."""
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    torch.manual_seed(6)
+    M, K, N = 2048, 2048, 4096
+    a = torch.randn(M, K, device=cuda, dtype=torch.bfloat16)
+    b = torch.randn(M, N, device=cuda, dtype=torch.bfloat16)
+    L._GEMM_PICK[("wgrad", M, K, N, a.stride(0), b.stride(0))] = choice
+    ref = a.float().t() @ b.float()
+    out = torch.empty(K, N, device=cuda, dtype=torch.bfloat16)
+    L._unsplit_wgrad(a, b, out, False)
+    assert (out.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    L._unsplit_wgrad(a, b, out, True)
+    assert (out.float() - 2 * ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
