@@ -267,9 +267,15 @@ class _AddNorm(torch.autograd.Function):
         if dh is None:
             dh = torch.zeros_like(xo)
         parts = _norm_parts(rows, C)
-        dx, dy, part = hip.ops().add_norm_bwd(dh.contiguous(), None if dxo is None else dxo.contiguous(), xo, gamma,
-                                              mean, rstd, ctx.rms, ctx.p, ctx.seed, True, parts)
         need = ctx.needs_input_grad
+        # without dropout (Llama) and with no bias gradient to sum, the branch gradient IS the
+        # residual one: return dx for both instead of writing an identical copy (one stream of
+        # the backward's five; autograd aliases grads the same way for an add)
+        alias = ctx.p == 0.0 and not (ctx.has_bias and need[2])
+        dx, dy, part = hip.ops().add_norm_bwd(dh.contiguous(), None if dxo is None else dxo.contiguous(), xo, gamma,
+                                              mean, rstd, ctx.rms, ctx.p, ctx.seed, not alias, parts)
+        if alias:
+            dy = dx
         dgamma, dbeta, dbias = _param_grads(part.view(-1, 3 * C), C, ctx.fused_params,
                                             (need[3], ctx.has_beta and need[4], ctx.has_bias and need[2]))
         return dy, dx, dbias, dgamma, dbeta, None, None, None, None
