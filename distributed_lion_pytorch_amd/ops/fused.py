@@ -735,6 +735,20 @@ def causal_attention_gqa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, drop
     return y.transpose(1, 2).reshape(B, T, H * D)
 
 
+_ROPE_MERGE = os.environ.get("DLION_ROPE_MERGE", "1") != "0"  # A/B switch: one rotation launch for q | k
+
+
+def _adjacent_heads(q: torch.Tensor, k: torch.Tensor):
+    """[B, T, Hq + Hk, D] view over q [B, T, Hq, D] and k when k's heads follow
+    q's in memory with the same token stride (the fused q|k|v output), else None."""
+    B, T, Hq, D = q.shape
+    if (k.shape[0] != B or k.shape[1] != T or k.shape[3] != D or q.stride() != k.stride() or q.stride(2) != D
+            or q.stride(3) != 1 or k.data_ptr() != q.data_ptr() + Hq * D * q.element_size()
+            or k.untyped_storage().data_ptr() != q.untyped_storage().data_ptr()):
+        return None
+    return q.as_strided((B, T, Hq + k.shape[2], D), q.stride())
+
+
 class _RopeAttention(torch.autograd.Function):
     """Llama attention core: causal GQA attention on rope(q), rope(k), v where
     q / k / v are column views of the fused q|k|v projection output.  The
@@ -747,8 +761,14 @@ class _RopeAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, cos, sin, p, seed):
         ops = hip.ops()
-        qr = ops.rope(q, cos, sin, False)
-        kr = ops.rope(k, cos, sin, False)
+        H = q.shape[2]
+        qk = _adjacent_heads(q, k) if _ROPE_MERGE else None
+        if qk is not None:  # q | k adjacent column blocks of the projection output: one rotation launch
+            r = ops.rope(qk, cos, sin, False)
+            qr, kr = r[:, :, :H], r[:, :, H:]
+        else:
+            qr = ops.rope(q, cos, sin, False)
+            kr = ops.rope(k, cos, sin, False)
         out, lse = ops.attn_fwd(qr, kr, v, p, seed)
         ctx.save_for_backward(qr, kr, v, out, lse, cos, sin)
         ctx.p, ctx.seed = p, seed
@@ -763,8 +783,11 @@ class _RopeAttention(torch.autograd.Function):
         dq, dk, dv = buf[:, :, :H], buf[:, :, H:H + Hkv], buf[:, :, H + Hkv:]
         ops = hip.ops()
         ops.attn_bwd(qr, kr, v, out, dout.contiguous(), lse, ctx.p, ctx.seed, dq, dk, dv)
-        ops.rope_(dq, cos, sin, True)
-        ops.rope_(dk, cos, sin, True)
+        if _ROPE_MERGE:
+            ops.rope_(buf[:, :, :H + Hkv], cos, sin, True)  # dq | dk: one in-place inverse rotation
+        else:
+            ops.rope_(dq, cos, sin, True)
+            ops.rope_(dk, cos, sin, True)
         return dq, dk, dv, None, None, None, None
 
 
