@@ -105,6 +105,8 @@ def parse():
     for k, v in PRESETS[a.task].items():
         if getattr(a, k, None) is None:
             setattr(a, k, v)
+    # an explicit --gradient_checkpointing is honoured; a preset's (DPO) goes through --checkpointing_policy
+    a.ckpt_explicit = bool(a.gradient_checkpointing)
     a.gradient_checkpointing = (a.gradient_checkpointing or bool(getattr(a, "grad_ckpt", False))) and \
         not a.no_gradient_checkpointing
     return a
@@ -165,7 +167,8 @@ def build_native(args, dev):
         from distributed_lion_pytorch_amd.trainer.memory import should_checkpoint
 
         tokens = args.micro_batch * (2 if args.task == "dpo" else 1) * args.seq_len
-        args.gradient_checkpointing = should_checkpoint(True, args.checkpointing_policy, cfg, tokens, model, ref_model)
+        policy = "reference" if args.ckpt_explicit else args.checkpointing_policy
+        args.gradient_checkpointing = should_checkpoint(True, policy, cfg, tokens, model, ref_model)
     if args.gradient_checkpointing:
         model.gradient_checkpointing_enable()
     broadcast_parameters(model)
