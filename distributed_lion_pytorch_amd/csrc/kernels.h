@@ -119,7 +119,7 @@ hipError_t launch_quant4(int dt, const void* w, const float* code, uint8_t* q, f
                          hipStream_t st);
 hipError_t launch_dequant4(int dt, const uint8_t* q, const float* absmax, const float* code, void* out, int64_t n,
                            hipStream_t st);
-// transposed: out [K, >= N] (row stride ldo, 16-bit dtypes) = W^T for W [N, K]; N % 64 == K % 64 == 0
+// transposed: out [K, >= N] (row stride ldo, 16-bit dtypes) = W^T for W [N, K]; N % 64 == 0, K % 128 == 0
 hipError_t launch_dequant4_t(int dt, const uint8_t* q, const float* absmax, const float* code, void* out, int N, int K,
                              int64_t ldo, hipStream_t st);
 

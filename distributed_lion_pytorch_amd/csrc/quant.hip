@@ -97,23 +97,25 @@ __global__ __launch_bounds__(kThreads) void dequant4_kernel(const uint32_t* __re
 
 // Transposed expansion for the input-gradient GEMM (dX = dY . W as the NT
 // product against W^T): out[k, n] (row stride ldo) = code[q(n, k)] * absmax,
-// for W [N, K] stored as above.  64 x 64 tile per 256-thread block: 128
-// threads each expand 16 packed bytes (32 elements of one row) into an LDS
-// tile of 16-bit values, then every thread gathers 2 x 8 tile-column values
-// into 16-byte stores of the transposed rows.  N % 64 == K % 64 == 0.
+// for W [N, K] stored as above.  64 (n) x 128 (k) tile per 256-thread block:
+// each thread expands one 16-byte load (32 elements of a row; 64 contiguous
+// packed bytes per row and tile -- a 64 x 64 tile fetched 32-byte row pieces,
+// measured 4.4x the ideal packed-weight traffic) into an LDS tile of 16-bit
+// values, then gathers tile columns into 16-byte stores of the transposed rows.
+// N % 64 == 0, K % 128 == 0.
 template <int DT>
 __global__ __launch_bounds__(kThreads) void dequant4_t_kernel(const uint4* __restrict__ q,
                                                               const float* __restrict__ absmax,
                                                               const float* __restrict__ code,
                                                               uint16_t* __restrict__ out, int N, int K, int64_t ldo) {
   __shared__ float2 tab[256];
-  __shared__ uint16_t tile[64][66];
+  __shared__ uint16_t tile[64][130];
   tab[threadIdx.x] = make_float2(code[threadIdx.x >> 4], code[threadIdx.x & 15]);
   __syncthreads();
-  const int n0 = blockIdx.y * 64, k0 = blockIdx.x * 64;
-  if (threadIdx.x < 128) {
-    const int nl = threadIdx.x >> 1, half = threadIdx.x & 1;
-    const int64_t e = static_cast<int64_t>(n0 + nl) * K + k0 + half * 32;  // first element of the 32
+  const int n0 = blockIdx.y * 64, k0 = blockIdx.x * 128;
+  {
+    const int nl = threadIdx.x >> 2, part = threadIdx.x & 3;
+    const int64_t e = static_cast<int64_t>(n0 + nl) * K + k0 + part * 32;  // first element of the 32
     const uint4 w = q[e / 32];
     const float s = absmax[e / kQBlock];
     const uint32_t words[4] = {w.x, w.y, w.z, w.w};
@@ -122,7 +124,7 @@ __global__ __launch_bounds__(kThreads) void dequant4_t_kernel(const uint4* __res
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const float2 c = tab[(words[k] >> (8 * b)) & 0xffu];
-        const int col = half * 32 + k * 8 + b * 2;
+        const int col = part * 32 + k * 8 + b * 2;
         if constexpr (DT == kBF16) {
           tile[nl][col] = __builtin_bit_cast(uint16_t, static_cast<__bf16>(c.x * s));
           tile[nl][col + 1] = __builtin_bit_cast(uint16_t, static_cast<__bf16>(c.y * s));
@@ -135,8 +137,8 @@ __global__ __launch_bounds__(kThreads) void dequant4_t_kernel(const uint4* __res
   }
   __syncthreads();
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int idx = threadIdx.x + h * kThreads;  // 64 output rows (k) x 8 chunks of 8 n
+  for (int h = 0; h < 4; ++h) {
+    const int idx = threadIdx.x + h * kThreads;  // 128 output rows (k) x 8 chunks of 8 n
     const int kl = idx >> 3, nb = (idx & 7) * 8;
     uint32_t v[4];
 #pragma unroll
@@ -224,10 +226,10 @@ hipError_t launch_dequant4(int dt, const uint8_t* q, const float* absmax, const 
 hipError_t launch_dequant4_t(int dt, const uint8_t* q, const float* absmax, const float* code, void* out, int N, int K,
                              int64_t ldo, hipStream_t st) {
   if (N <= 0 || K <= 0) return hipSuccess;
-  if (N % 64 || K % 64 || ldo < N || ldo % 8 || reinterpret_cast<uintptr_t>(out) % 16 ||
+  if (N % 64 || K % 128 || ldo < N || ldo % 8 || reinterpret_cast<uintptr_t>(out) % 16 ||
       reinterpret_cast<uintptr_t>(q) % 16)
     return hipErrorInvalidValue;
-  const dim3 grid(K / 64, N / 64);
+  const dim3 grid(K / 128, N / 64);
   if (grid.y > 65535) return hipErrorInvalidValue;
   const uint4* qv = reinterpret_cast<const uint4*>(q);
   switch (dt) {

@@ -126,7 +126,7 @@ def _dequant_cat(layers, dtype, device) -> torch.Tensor:
 
 def _transposed_ok(layers, dy) -> bool:
     return (dy.is_cuda and dy.dtype in (torch.bfloat16, torch.float16)
-            and all(l.in_features % 64 == 0 and l.out_features % 64 == 0 for l in layers))
+            and all(l.in_features % 128 == 0 and l.out_features % 64 == 0 for l in layers))
 
 
 def _dequant_cat_t(layers, dtype, device) -> torch.Tensor:
