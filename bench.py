@@ -42,6 +42,7 @@ from distributed_lion_pytorch_amd import Lion  # noqa: E402
 from distributed_lion_pytorch_amd.models.gpt2 import gpt2_config  # noqa: E402
 from distributed_lion_pytorch_amd.parallel.exchange import wire_bytes_per_step  # noqa: E402
 from distributed_lion_pytorch_amd.trainer.engine import StepTimer, TrainStep, broadcast_parameters  # noqa: E402
+from distributed_lion_pytorch_amd.utils.timing import PhaseTimer  # noqa: E402
 
 
 # reference configs: run_clm README (/root/reference/README.md:20-37) and
@@ -98,6 +99,9 @@ def parse():
                     help="frozen base weights in 4-bit NF4 (the reference's bitsandbytes base, models/quant.py)")
     ap.add_argument("--profile_dir", default=None)
     ap.add_argument("--rocm_fa", default=None, help="PyTorch SDPA flash library on ROCm: ck | aotriton")
+    ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"],
+                    help="auto: cuda when a GPU is visible (cpu + gloo: plumbing rehearsal of the multi-rank path)")
+    ap.add_argument("--no_phase_times", action="store_true", help="do not record per-phase HIP events")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend; gloo (with ranks sharing GPUs) only to rehearse the multi-rank "
                          "path on a 1-GPU box -- RCCL refuses two ranks on one device")
@@ -112,19 +116,106 @@ def parse():
     return a
 
 
+RCCL_ENV_DEFAULTS = {
+    # the host driver only supports dmabuf IPC (RCCL / cross-process CUDA tensors fail without it)
+    "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+    # RCCL's streams at high priority: the vote collectives are issued while the
+    # compute stream still has the next bucket's encode / apply queued
+    "TORCH_NCCL_HIGH_PRIORITY": "1",
+}
+_ENV_PREFIXES = ("NCCL_", "RCCL_", "TORCH_NCCL_", "HSA_", "HIP_", "GPU_MAX_HW_QUEUES", "OMP_NUM_THREADS")
+
+
+def comm_env() -> dict:
+    """The collective-relevant environment this rank ran with (reported in the JSON)."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith(_ENV_PREFIXES)}
+
+
+def _rccl_version():
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def resolve_device(args) -> str:
+    if args.device != "auto":
+        return args.device
+    return "cuda" if torch.cuda.device_count() > 0 else "cpu"
+
+
+def launch_local(args) -> int:
+    """``--gpus N`` without a launcher: start N rank processes (one per GPU,
+    127.0.0.1 rendezvous) and relay rank 0's JSON line.  This parent never
+    initialises the GPU (``device_count`` only counts devices), so no HIP
+    context is ever forked or exec'd over; the children are fresh interpreters."""
+    import socket
+    import subprocess
+
+    device = resolve_device(args)
+    if device == "cuda" and args.backend == "nccl" and torch.cuda.device_count() < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but only {torch.cuda.device_count()} GPU(s) visible; refusing to "
+              "report a smaller run", file=sys.stderr)
+        return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLION_BENCH_LAUNCHER="bench.py")
+        out = None if r == 0 else subprocess.DEVNULL
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=out))
+    rc = 0
+    pending = list(procs)
+    import time as _time
+
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr)
+                for q in pending:
+                    q.terminate()
+        _time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
 def setup_dist(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    world = int(env_world) if env_world is not None else 1
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if args.backend == "gloo":
-        local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a dp{world} run "
+                         f"as {args.gpus} GPUs")
+    device = resolve_device(args)
+    if device == "cuda":
+        n_dev = torch.cuda.device_count()
+        if args.backend == "gloo":
+            local = local % max(1, n_dev)  # gloo rehearsal: ranks may share a GPU
+        elif local >= n_dev:
+            raise SystemExit(f"bench.py: rank {rank} wants cuda:{local} but only {n_dev} GPU(s) are visible")
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        if args.backend == "nccl" and world > 1:
+            raise SystemExit("bench.py: --device cpu needs --backend gloo")
+        dev = torch.device("cpu")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if args.backend == "nccl":
+            for k, v in RCCL_ENV_DEFAULTS.items():
+                os.environ.setdefault(k, v)
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
             dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -216,6 +307,10 @@ def build_reference(args, dev):
 
 def main():
     args = parse()
+    if os.environ.get("WORLD_SIZE") is None and args.gpus > 1:
+        sys.exit(launch_local(args))  # one process per GPU, started here (no torchrun needed)
+    if resolve_device(args) == "cpu" and args.backend == "nccl":
+        args.backend = "gloo"
     world, rank, dev = setup_dist(args)
     if args.rocm_fa:
         torch.backends.cuda.preferred_rocm_fa_library(args.rocm_fa)
@@ -261,6 +356,10 @@ def main():
 
     for _ in range(args.warmup):
         step(batches())
+    if hasattr(opt, "stats"):
+        opt.stats(reset=True)  # wire counters cover the timed steps only
+    phases = None if args.no_phase_times else PhaseTimer(dev)
+    step.set_timer(phases)
     timer = StepTimer(dev)
     prof = None
     if args.profile_dir and rank == 0:
@@ -280,16 +379,27 @@ def main():
             f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=80,
                                                                           max_name_column_width=40,
                                                                           max_shapes_column_width=90))
-    elapsed = torch.tensor([timer.elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    step.set_timer(None)
+    phase_ms = phases.summary() if phases is not None else {}
+    names = sorted(phase_ms)
+    vec = torch.tensor([timer.elapsed] + [phase_ms[k] for k in names], dtype=torch.float64, device=dev)
+    if world > 1:  # slowest rank (the contract's MAX over ranks), and its phase times
+        allv = [torch.zeros_like(vec) for _ in range(world)]
+        dist.all_gather(allv, vec)
+        vec = max(allv, key=lambda v: float(v[0]))
+        per_rank_ms = [round(1000.0 * float(v[0]) / args.steps, 3) for v in allv]
+    else:
+        per_rank_ms = [round(1000.0 * timer.elapsed / args.steps, 3)]
+    elapsed = float(vec[0])
+    phase_ms = {k: round(float(vec[i + 1]), 3) for i, k in enumerate(names)}
     tokens = world * args.grad_accum * seqs_per_mb * args.seq_len * args.steps
     tps = tokens / elapsed
     ms = 1000.0 * elapsed / args.steps
     stats = opt.stats() if hasattr(opt, "stats") else {}
     exchange = args.exchange if args.impl == "native" else "ref_int64"
     wire = wire_bytes_per_step(n_train, world, exchange)
+    wire_meas = {k: stats.get(k, 0) // max(1, args.steps) for k in ("wire_bytes_sent", "wire_bytes_recv",
+                                                                       "collectives")}
     if rank == 0:
         out = {
             "metric": args.metric,
@@ -320,7 +430,16 @@ def main():
                 "exchange": exchange,
                 "impl": args.impl,
             },
-            "wire_bytes_per_step_per_rank": wire,
+            "wire_bytes_per_step_per_rank": wire_meas["wire_bytes_sent"] if world > 1 else 0,
+            "wire_bytes_per_step_per_rank_measured": wire_meas,
+            "wire_bytes_per_step_per_rank_analytic": wire,
+            "phase_ms_per_step": phase_ms,
+            "ms_per_step_per_rank": per_rank_ms,
+            "device": str(dev),
+            "backend": args.backend if world > 1 else None,
+            "launcher": os.environ.get("DLION_BENCH_LAUNCHER", "torchrun" if world > 1 else "none"),
+            "comm_env": comm_env() if world > 1 else {},
+            "rccl_version": _rccl_version() if world > 1 and args.backend == "nccl" else None,
             "bf16_allreduce_bytes_per_step_per_rank": 0 if world == 1 else int(2 * (world - 1) / world * 2 * n_train),
             "loss": round(float(loss.item()), 4),
             "optimizer_stats": stats,

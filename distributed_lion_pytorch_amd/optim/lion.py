@@ -40,6 +40,7 @@ from torch.optim.optimizer import Optimizer
 from ..ops import reference as ref
 from ..ops.linear import bump_weight_generation
 from ..parallel.exchange import canonical_strategy, make_exchange, wire_bytes_per_step
+from ..utils.timing import phase_of
 from .executors import HParams, make_executor
 from .plan import FlatPlan
 
@@ -64,7 +65,7 @@ class Lion(Optimizer):
         *,
         vote: str = "majority",
         tie_break: str = "negative",
-        exchange: str = "allgather",
+        exchange: str = "a2a",
         bucket_mb: float = 32.0,
         group=None,
         backend: str = "auto",
@@ -109,6 +110,11 @@ class Lion(Optimizer):
         self.last_world = 1
         self.elastic_timeout = elastic_timeout
         self._elastic = None
+        # optional utils.metrics.PhaseTimer: encode / exchange / apply (local_update at W=1)
+        self.phase_timer = None
+        # run the vote path (encode -> collectives -> apply) even on a 1-rank
+        # group: exercises the RCCL calls on a single GPU (tests/test_nccl_gpu.py)
+        self._force_vote = False
 
     # ------------------------------------------------------------ topology
     def _world(self):
@@ -175,7 +181,7 @@ class Lion(Optimizer):
         plan._full_key = key
         self._plan = plan
         self._executor = make_executor(plan, self.backend)
-        if world > 1:
+        if world > 1 or self._force_vote:
             if self.verify_consistency:
                 self._check_consistency(plan)
             self._exchange = make_exchange(self.exchange_name, plan, self.process_group, rank, world,
@@ -276,9 +282,10 @@ class Lion(Optimizer):
                for g in self.param_groups]
 
         gscale, self._pending_gscale = getattr(self, "_pending_gscale", None), None
-        if world == 1:
-            for b in plan.buckets:
-                ex.local(meta, b, hps[b.group], grads=grads, moms=moms, gscale=gscale)
+        if world == 1 and not self._force_vote:
+            with phase_of(self.phase_timer, "local_update"):
+                for b in plan.buckets:
+                    ex.local(meta, b, hps[b.group], grads=grads, moms=moms, gscale=gscale)
         else:
             self._distributed_step(plan, ex, meta, hps, grads, moms, world, rank, gscale)
         # the kernels wrote the weights through raw pointers (no autograd
@@ -294,19 +301,24 @@ class Lion(Optimizer):
         if self.telemetry and self._agree is None:
             self._agree = torch.zeros(1, dtype=torch.int64, device=plan.device)
         seed = (self.seed * 0x9E3779B1 + rank * 0x632BE59BD9B4E019 + 1) & 0x7FFFFFFFFFFFFFFF
+        t = self.phase_timer
         states = []
         for b in plan.buckets:  # encode bucket i, then its collective overlaps encode of i+1
             hp = hps[b.group]
             rr = (1.0 + 1.0 / hp.beta1) * self.max_grad_norm if stochastic else 0.0
-            ex.encode(meta, b, xch.send_view(b), hp, update_m=True, stochastic=stochastic, rr=rr, seed=seed,
-                      step=self._n_steps, grads=grads, moms=moms, gscale=gscale)
-            states.append(xch.launch(b, alive))
-        states = [xch.advance(b, s, alive) for b, s in zip(plan.buckets, states)]
+            with phase_of(t, "encode"):
+                ex.encode(meta, b, xch.send_view(b), hp, update_m=True, stochastic=stochastic, rr=rr, seed=seed,
+                          step=self._n_steps, grads=grads, moms=moms, gscale=gscale)
+                states.append(xch.launch(b, alive))
+        with phase_of(t, "exchange"):
+            states = [xch.advance(b, s, alive) for b, s in zip(plan.buckets, states)]
         for b, s in zip(plan.buckets, states):
-            a = xch.finish(b, s, alive)
-            ex.apply(meta, b, a.planes, a.stride, alive, a.mode, ref.TIE_CODES[self.tie_break], a.neg,
-                     hps[b.group], own=xch.send_view(b) if self.telemetry else None,
-                     agree=self._agree if self.telemetry else None)
+            with phase_of(t, "exchange"):
+                a = xch.finish(b, s, alive)
+            with phase_of(t, "apply"):
+                ex.apply(meta, b, a.planes, a.stride, alive, a.mode, ref.TIE_CODES[self.tie_break], a.neg,
+                         hps[b.group], own=xch.send_view(b) if self.telemetry else None,
+                         agree=self._agree if self.telemetry else None)
 
     # ---------------------------------------------------------- telemetry
     def stats(self, reset: bool = True) -> dict:

@@ -18,6 +18,8 @@ from typing import Callable, Iterable, Optional
 import torch
 import torch.distributed as dist
 
+from ..utils.timing import phase_of
+
 
 def broadcast_parameters(model: torch.nn.Module, src: int = 0, group=None) -> None:
     """One-time replica initialisation (what DDP's constructor broadcast did
@@ -73,26 +75,40 @@ class TrainStep:
             self._fused_ok = mine == {id(p) for p in self.params}
         return self._fused_ok
 
+    def set_timer(self, timer) -> None:
+        """Attach a :class:`~..utils.timing.PhaseTimer` (``None`` detaches):
+        phases ``fwd_bwd`` / ``clip`` / ``optimizer`` here, and the Lion
+        step's own ``encode`` / ``exchange`` / ``apply`` (or ``local_update``)."""
+        self.timer = timer
+        if hasattr(self.optimizer, "phase_timer"):
+            self.optimizer.phase_timer = timer
+
     def __call__(self, micro_batches: Iterable[dict]) -> torch.Tensor:
         from ..ops.linear import grad_accumulation_fusion
 
+        t = getattr(self, "timer", None)
         self.model.train()
         total = None
-        with grad_accumulation_fusion(self.fuse_grad_accumulation, micro_batches=self.grad_accum):
-            for batch in micro_batches:
-                loss = self.loss_fn(self.model, batch) / self.grad_accum
-                loss.backward()
-                total = loss.detach() if total is None else total + loss.detach()
+        with phase_of(t, "fwd_bwd"):
+            with grad_accumulation_fusion(self.fuse_grad_accumulation, micro_batches=self.grad_accum):
+                for batch in micro_batches:
+                    loss = self.loss_fn(self.model, batch) / self.grad_accum
+                    loss.backward()
+                    total = loss.detach() if total is None else total + loss.detach()
         if self.max_grad_norm is not None and self.max_grad_norm > 0:
-            if self._fused_clip():
-                # norm on device, scale applied inside the Lion update kernels
-                self.optimizer.clip_grad_norm_(self.max_grad_norm)
-            else:
-                torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm, foreach=True)
-        self.optimizer.step()
+            with phase_of(t, "clip"):
+                if self._fused_clip():
+                    # norm on device, scale applied inside the Lion update kernels
+                    self.optimizer.clip_grad_norm_(self.max_grad_norm)
+                else:
+                    torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm, foreach=True)
+        with phase_of(t, "optimizer"):
+            self.optimizer.step()
         if self.scheduler is not None:
             self.scheduler.step()
         self.optimizer.zero_grad(set_to_none=True)
+        if t is not None:
+            t.step()
         return total
 
 

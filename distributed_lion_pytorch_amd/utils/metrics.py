@@ -11,12 +11,16 @@ from __future__ import annotations
 import json
 import os
 import time
-from collections import defaultdict
-from contextlib import contextmanager
-from typing import Dict, Optional
+from typing import Optional
 
 import torch
-from transformers import TrainerCallback
+
+try:
+    from transformers import TrainerCallback
+except ImportError:  # pragma: no cover - the engine/bench path does not need HF
+    TrainerCallback = object
+
+from .timing import PhaseTimer, phase_of  # noqa: F401  (re-export)
 
 
 def is_rank0() -> bool:
@@ -54,33 +58,3 @@ class JsonlMetricsCallback(TrainerCallback):
         os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
         with open(self.path, "a") as f:
             f.write(json.dumps(rec, default=float) + "\n")
-
-
-class PhaseTimer:
-    """Per-phase GPU time with HIP events (no host sync until :meth:`summary`)."""
-
-    def __init__(self, enabled: bool = True):
-        self.enabled = enabled and torch.cuda.is_available()
-        self._events = defaultdict(list)
-
-    @contextmanager
-    def phase(self, name: str):
-        if not self.enabled:
-            yield
-            return
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        try:
-            yield
-        finally:
-            e.record()
-            self._events[name].append((s, e))
-
-    def summary(self, reset: bool = True) -> Dict[str, float]:
-        if not self.enabled:
-            return {}
-        torch.cuda.synchronize()
-        out = {k: sum(s.elapsed_time(e) for s, e in v) for k, v in self._events.items()}
-        if reset:
-            self._events.clear()
-        return out

@@ -1,0 +1,59 @@
+"""bench.py launch contract on the CPU: ``--gpus N`` without torchrun starts N
+real ranks (never a silent dp1), a WORLD_SIZE that disagrees with ``--gpus``
+or too few devices is a hard error, and the JSON carries the measured wire
+bytes and the per-phase breakdown of the step."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TINY = ["--model", "gpt2-tiny", "--micro_batch", "2", "--grad_accum", "2", "--seq_len", "64", "--steps", "2",
+        "--warmup", "1"]
+
+
+def _run(args, env=None, timeout=300):
+    e = dict(os.environ, OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, "bench.py"] + args, cwd=ROOT, capture_output=True, text=True,
+                          timeout=timeout, env=e)
+
+
+def test_gpus3_without_torchrun_spawns_three_ranks():
+    r = _run(["--gpus", "3", "--backend", "gloo", "--device", "cpu"] + TINY)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    out = lines[0]
+    assert out["n_gpus"] == 3 and out["config"]["parallelism"] == "dp3"
+    assert out["launcher"] == "bench.py" and len(out["ms_per_step_per_rank"]) == 3
+    meas = out["wire_bytes_per_step_per_rank_measured"]
+    assert meas["wire_bytes_sent"] > 0 and meas["wire_bytes_recv"] > 0 and meas["collectives"] == 2  # a2a + AG
+    assert out["wire_bytes_per_step_per_rank"] == meas["wire_bytes_sent"]
+    # 1-bit vote-RS/AG: 2(W-1)/W * N/8 analytic, measured adds only the 256*W-byte bucket padding
+    assert out["wire_bytes_per_step_per_rank_analytic"] <= meas["wire_bytes_sent"] < 2 * out[
+        "wire_bytes_per_step_per_rank_analytic"]
+    ph = out["phase_ms_per_step"]
+    assert {"fwd_bwd", "clip", "optimizer", "encode", "exchange", "apply"} <= set(ph)
+    assert all(v >= 0 for v in ph.values())
+    assert ph["optimizer"] >= ph["encode"] and out["ms_per_step"] >= ph["fwd_bwd"]
+    assert abs(out["value"] - 3 * 2 * 2 * 64 * 2 / (out["ms_per_step"] * 2 / 1000)) / out["value"] < 0.01
+
+
+def test_world_size_mismatch_is_an_error():
+    r = _run(["--gpus", "2", "--device", "cpu", "--backend", "gloo"] + TINY,
+             env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE=1" in r.stderr
+
+
+@pytest.mark.skipif(torch.cuda.device_count() >= 2, reason="needs a host with fewer than 2 GPUs")
+def test_too_few_gpus_is_an_error():
+    r = _run(["--gpus", "2", "--device", "cuda"] + TINY)
+    assert r.returncode != 0
+    assert "GPU(s) visible" in r.stderr

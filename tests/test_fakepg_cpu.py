@@ -25,8 +25,9 @@ def _fake_world(q, world, rank, exchange, bucket_mb, steps):
         cfg = gpt2_config("gpt2-tiny")
         torch.manual_seed(0)
         model = GPT2LMHeadModel(cfg)
-        opt = Lion(model.parameters(), lr=1e-3, weight_decay=0.1, exchange=exchange, bucket_mb=bucket_mb,
-                   backend="torch", verify_consistency=False)
+        kw = {} if exchange is None else {"exchange": exchange}  # None: the constructor default
+        opt = Lion(model.parameters(), lr=1e-3, weight_decay=0.1, bucket_mb=bucket_mb, backend="torch",
+                   verify_consistency=False, **kw)
         ids = torch.randint(0, cfg.vocab_size, (2, 16))
         per_step = []
         for _ in range(steps):
@@ -40,7 +41,7 @@ def _fake_world(q, world, rank, exchange, bucket_mb, steps):
             "bucket_bytes": [b.nbytes for b in plan.buckets],
             "total_bytes": plan.total_bytes,
             "numel": sum(s.numel for s in plan.segments),
-            "analytic": wire_bytes_per_step(sum(s.numel for s in plan.segments), world, exchange),
+            "analytic": wire_bytes_per_step(sum(s.numel for s in plan.segments), world, opt.exchange_name),
             "finite": all(torch.isfinite(p).all().item() for p in model.parameters()),
             "exchange_cls": type(opt._exchange).__name__,
         }
@@ -87,6 +88,15 @@ def test_a2a_shards_align_and_wire_bytes(world, rank):
         # reference wire: 1 byte per parameter per peer; here >= 4x less even with a
         # tiny model's per-tensor padding
         assert 4 * s["wire_bytes_recv"] < (world - 1) * out["numel"]
+
+
+def test_reference_signature_defaults_to_a2a():
+    """``Lion(model.parameters(), lr=...)`` -- exactly the reference usage
+    (/root/reference/README.md:8-15) -- gets the vote-RS/AG exchange, not the
+    4x-more-bytes all-gather."""
+    out = run_fake(4, 1, None, steps=1)
+    assert out["exchange_cls"] == "AllToAllExchange"
+    assert out["stats"][0]["wire_bytes_recv"] == 2 * 3 * out["total_bytes"] // 4
 
 
 @pytest.mark.parametrize("exchange", ["allgather", "ref_int64"])
