@@ -147,47 +147,20 @@ def resolve_device(args) -> str:
 
 def launch_local(args) -> int:
     """``--gpus N`` without a launcher: start N rank processes (one per GPU,
-    127.0.0.1 rendezvous) and relay rank 0's JSON line.  This parent never
-    initialises the GPU (``device_count`` only counts devices), so no HIP
-    context is ever forked or exec'd over; the children are fresh interpreters."""
-    import socket
-    import subprocess
+    127.0.0.1 rendezvous, store hosted by this parent) and relay rank 0's JSON
+    line; any rank failing fails the run.  This parent never initialises the
+    GPU (``device_count`` only counts devices), so no HIP context is ever
+    forked or exec'd over; the children are fresh interpreters."""
+    from distributed_lion_pytorch_amd.launch import run
 
     device = resolve_device(args)
     if device == "cuda" and args.backend == "nccl" and torch.cuda.device_count() < args.gpus:
         print(f"bench.py: --gpus {args.gpus} but only {torch.cuda.device_count()} GPU(s) visible; refusing to "
               "report a smaller run", file=sys.stderr)
         return 2
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    procs = []
-    for r in range(args.gpus):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLION_BENCH_LAUNCHER="bench.py")
-        out = None if r == 0 else subprocess.DEVNULL
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=out))
-    rc = 0
-    pending = list(procs)
-    import time as _time
-
-    while pending:
-        for p in list(pending):
-            code = p.poll()
-            if code is None:
-                continue
-            pending.remove(p)
-            if code != 0 and rc == 0:
-                rc = code
-                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
-                      file=sys.stderr)
-                for q in pending:
-                    q.terminate()
-        _time.sleep(0.05)
-    for p in procs:
-        p.wait()
-    return rc
+    env = dict(os.environ, DLION_BENCH_LAUNCHER="bench.py")
+    return run([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus, max_failures=0,
+               quiet_ranks=True, env=env)
 
 
 def setup_dist(args):
@@ -380,6 +353,9 @@ def main():
                                                                           max_name_column_width=40,
                                                                           max_shapes_column_width=90))
     step.set_timer(None)
+    from distributed_lion_pytorch_amd.ops.fused import check_index_errors
+
+    check_index_errors(blocking=True)
     phase_ms = phases.summary() if phases is not None else {}
     names = sorted(phase_ms)
     vec = torch.tensor([timer.elapsed] + [phase_ms[k] for k in names], dtype=torch.float64, device=dev)

@@ -690,7 +690,25 @@ void check_bf16_contig(const Tensor& t, const char* name) {
 }
 
 // out [B, T, C] = dropout(wte[ids] + wpe[t]) for ids [B, T]
-Tensor embed_fwd(const Tensor& ids, const Tensor& wte, const Tensor& wpe, double p, int64_t seed) {
+int32_t* err_ptr(const std::optional<Tensor>& err, const Tensor& like) {
+  if (!err.has_value()) return nullptr;
+  TORCH_CHECK(err->scalar_type() == at::kInt && err->numel() >= 1 && err->device() == like.device(),
+              "dlion: the index-error flag must be an int32 tensor on the ids' device");
+  return err->data_ptr<int32_t>();
+}
+
+// err[0] |= code when any of ids is outside [0, hi) and != ignore
+void index_check_(const Tensor& ids, int64_t hi, int64_t ignore, const Tensor& err, int64_t code) {
+  check_dev(ids, "ids");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous(), "dlion index_check: ids must be contiguous int64");
+  const c10::DeviceGuard g(ids.device());
+  check_hip(dlion::launch_index_check(ids.data_ptr<int64_t>(), ids.numel(), hi, ignore, err_ptr(err, ids),
+                                      static_cast<int>(code), cur_stream()),
+            "index_check");
+}
+
+Tensor embed_fwd(const Tensor& ids, const Tensor& wte, const Tensor& wpe, double p, int64_t seed,
+                 const std::optional<Tensor>& err) {
   check_dev(ids, "ids");
   TORCH_CHECK(ids.scalar_type() == at::kLong && ids.dim() == 2, "dlion embed: ids must be int64 [B, T]");
   check_bf16_contig(wte, "wte");
@@ -703,7 +721,7 @@ Tensor embed_fwd(const Tensor& ids, const Tensor& wte, const Tensor& wpe, double
   const auto dp = drop_params(p);
   check_hip(dlion::launch_embed_fwd(ids.data_ptr<int64_t>(), wte.data_ptr(), wpe.data_ptr(), out.data_ptr(), ids.numel(),
                                     static_cast<int>(C), static_cast<int>(T), wte.size(0), static_cast<uint32_t>(seed),
-                                    dp.first, dp.second, cur_stream()),
+                                    dp.first, dp.second, err_ptr(err, ids), cur_stream()),
             "embed_fwd");
   return out;
 }
@@ -1014,7 +1032,8 @@ TORCH_LIBRARY(dlion, m) {
   m.def("gemm_nt_gelu_d(Tensor a, Tensor b, Tensor bias, bool exact) -> (Tensor, Tensor)");
   m.def("gemm_nt_dmul(Tensor a, Tensor b, Tensor d) -> (Tensor, Tensor)");
   m.def("gemm_nt_stamped(Tensor a, Tensor b, Tensor(a!) stamps) -> Tensor");
-  m.def("embed_fwd(Tensor ids, Tensor wte, Tensor wpe, float p, int seed) -> Tensor");
+  m.def("embed_fwd(Tensor ids, Tensor wte, Tensor wpe, float p, int seed, Tensor(a!)? err=None) -> Tensor");
+  m.def("index_check_(Tensor ids, int hi, int ignore, Tensor(a!) err, int code) -> ()");
   m.def(
       "embed_bwd_(Tensor dx, Tensor? sid, Tensor? perm, Tensor(a!)? dwte, Tensor(b!)? dwpe, int T, bool pos_accumulate,"
       " float p, int seed) -> ()");
@@ -1095,6 +1114,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("gemm_nt_dmul", &gemm_nt_dmul);
   m.impl("gemm_nt_stamped", &gemm_nt_stamped);
   m.impl("embed_fwd", &embed_fwd);
+  m.impl("index_check_", &index_check_);
   m.impl("embed_bwd_", &embed_bwd_);
   m.impl("scale_acc_", &scale_acc_);
   m.impl("lt_gemm_nt", &lt_gemm_nt);

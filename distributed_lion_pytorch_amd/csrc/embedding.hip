@@ -15,6 +15,7 @@
 // batch for each position.  The dropout keep-mask is keep4() of the flat
 // element index (common.h), regenerated in the backward.
 #include "common.h"
+#include "kernels.h"
 
 namespace dlion {
 
@@ -27,7 +28,7 @@ __device__ __forceinline__ void drop8(float (&v)[8], uint32_t kp, float inv_keep
 __global__ void __launch_bounds__(256) embed_fwd_kernel(const int64_t* __restrict__ ids, const uint16_t* __restrict__ wte,
                                                         const uint16_t* __restrict__ wpe, uint16_t* __restrict__ out,
                                                         int64_t n, int C, int T, int64_t V, uint32_t seed,
-                                                        uint32_t thresh16, float inv_keep) {
+                                                        uint32_t thresh16, float inv_keep, int32_t* __restrict__ err) {
   const int cpr = C / 8;
   const int64_t total = n * cpr;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total;
@@ -35,7 +36,10 @@ __global__ void __launch_bounds__(256) embed_fwd_kernel(const int64_t* __restric
     const int64_t row = i / cpr;
     const int c = static_cast<int>(i - row * cpr) * 8;
     int64_t id = ids[row];
-    id = id < 0 ? 0 : (id >= V ? V - 1 : id);  // out-of-range ids are clamped, never read out of bounds
+    if (id < 0 || id >= V) {  // an error (flag checked once per step, ops/fused.py), never an out-of-bounds read
+      if (err != nullptr) atomicOr(err, kIndexErrEmbed);
+      id = id < 0 ? 0 : V - 1;
+    }
     float a[8], b[8];
     Elem<kBF16>::load8(wte + id * C + c, a);
     Elem<kBF16>::load8(wpe + static_cast<int64_t>(row % T) * C + c, b);
@@ -146,13 +150,33 @@ static inline unsigned grid_for(int64_t work, int64_t cap = 4096) {
   return static_cast<unsigned>(g < 1 ? 1 : (g > cap ? cap : g));
 }
 
+// err[0] |= code for every id outside [0, hi) other than `ignore` (labels: -100)
+__global__ void __launch_bounds__(256) index_check_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t hi,
+                                                          int64_t ignore, int32_t* __restrict__ err, int code) {
+  bool bad = false;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t v = ids[i];
+    bad |= (v < 0 || v >= hi) && v != ignore;
+  }
+  if (bad) atomicOr(err, code);
+}
+
+hipError_t launch_index_check(const int64_t* ids, int64_t n, int64_t hi, int64_t ignore, int32_t* err, int code,
+                              hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(index_check_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, ids, n, hi, ignore, err, code);
+  return hipGetLastError();
+}
+
 hipError_t launch_embed_fwd(const int64_t* ids, const void* wte, const void* wpe, void* out, int64_t n, int C, int T,
-                            int64_t V, uint32_t seed, uint32_t thresh16, float inv_keep, hipStream_t st) {
+                            int64_t V, uint32_t seed, uint32_t thresh16, float inv_keep, int32_t* err,
+                            hipStream_t st) {
   if (n == 0) return hipSuccess;
   if (C % 8 != 0 || T <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_for(n * (C / 8))), dim3(256), 0, st, ids,
                      static_cast<const uint16_t*>(wte), static_cast<const uint16_t*>(wpe), static_cast<uint16_t*>(out),
-                     n, C, T, V, seed, thresh16, inv_keep);
+                     n, C, T, V, seed, thresh16, inv_keep, err);
   return hipGetLastError();
 }
 

@@ -79,7 +79,11 @@ hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* 
 
 // ---- token + position embedding with dropout, scaled gradient accumulation (embedding.hip)
 hipError_t launch_embed_fwd(const int64_t* ids, const void* wte, const void* wpe, void* out, int64_t n, int C, int T,
-                            int64_t V, uint32_t seed, uint32_t thresh16, float inv_keep, hipStream_t st);
+                            int64_t V, uint32_t seed, uint32_t thresh16, float inv_keep, int32_t* err, hipStream_t st);
+// error-flag bits (index_check / embed_fwd): OR-ed into err[0]
+constexpr int kIndexErrEmbed = 1, kIndexErrLabel = 2;
+hipError_t launch_index_check(const int64_t* ids, int64_t n, int64_t hi, int64_t ignore, int32_t* err, int code,
+                              hipStream_t st);
 // dwte / dwpe nullable; sid / perm = stably sorted ids and their positions (needed with dwte)
 hipError_t launch_embed_bwd(const void* dx, const int64_t* sid, const int64_t* perm, void* dwte, void* dwpe, int64_t n,
                             int C, int T, int64_t V, int pos_accumulate, uint32_t seed, uint32_t thresh16,

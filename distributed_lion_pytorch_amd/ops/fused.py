@@ -513,6 +513,68 @@ def mlp_gelu(x: torch.Tensor, w_fc: torch.Tensor, b_fc: torch.Tensor, w_proj: to
     return (h @ w_proj).view(shp)
 
 
+# ------------------------------------------------------------ index errors
+# Out-of-range token ids / labels are an error, as in ATen's embedding and
+# cross-entropy, not a silent clamp: the embedding kernel and a label check
+# OR a bit into a per-device int32 flag, which check_index_errors() reads
+# once per optimizer step without stalling the stream (one step late) or, at
+# the end of a run, synchronously.
+_IDX_EMBED, _IDX_LABEL = 1, 2
+_IDX_FLAGS: dict = {}  # device -> [flag int32[1] (device), pinned host mirror, copy-done event]
+
+
+def _index_flag(dev: torch.device) -> torch.Tensor:
+    st = _IDX_FLAGS.get(dev)
+    if st is None:
+        st = _IDX_FLAGS[dev] = [torch.zeros(1, dtype=torch.int32, device=dev),
+                                torch.zeros(1, dtype=torch.int32).pin_memory(), None]
+    return st[0]
+
+
+def _index_error(code: int, where: str):
+    msgs = []
+    if code & _IDX_EMBED:
+        msgs.append("a token id is outside the embedding table [0, vocab_size) -- is the tokenizer larger than "
+                    "the model vocabulary? (run_clm resizes the embeddings for that)")
+    if code & _IDX_LABEL:
+        msgs.append("a label is outside [0, vocab_size) and is not the ignore index -100")
+    return ValueError(f"dlion ({where}): " + "; ".join(msgs))
+
+
+def check_labels(labels1d: torch.Tensor, v: int) -> None:
+    """Labels must be in [0, v) or -100 (ATen cross-entropy's contract)."""
+    if labels1d.is_cuda and hip.available():
+        hip.ops().index_check_(labels1d.contiguous(), int(v), -100, _index_flag(labels1d.device), _IDX_LABEL)
+    elif not labels1d.is_cuda:
+        bad = ((labels1d < 0) & (labels1d != -100)) | (labels1d >= v)
+        if bool(bad.any()):
+            raise _index_error(_IDX_LABEL, "labels")
+
+
+def check_index_errors(blocking: bool = False) -> None:
+    """Raise ValueError if a kernel flagged an out-of-range id or label.
+    Non-blocking (the per-step call): reads the flag copied at the previous
+    call if that copy has landed, then starts the next asynchronous copy.
+    ``blocking``: reads the flag now (end of a run, tests)."""
+    for dev, st in _IDX_FLAGS.items():
+        flag, host, ev = st
+        if blocking:
+            code = int(flag.item())
+        else:
+            code = 0
+            if ev is not None:
+                if not ev.query():
+                    continue  # the previous copy is still in flight
+                code = int(host[0])
+            host.copy_(flag, non_blocking=True)
+            st[2] = torch.cuda.Event()
+            st[2].record()
+        if code:
+            flag.zero_()
+            st[2] = None
+            raise _index_error(code, str(dev))
+
+
 # ------------------------------------------------------------ token embedding
 class _Embed(torch.autograd.Function):
     """x = dropout(wte[ids] + wpe[t]) for ids [B, T] (csrc/embedding.hip).
@@ -525,7 +587,7 @@ class _Embed(torch.autograd.Function):
     def forward(ctx, ids, wte, wpe, p, seed):
         from .linear import _fuse_target
 
-        out = hip.ops().embed_fwd(ids, wte, wpe, p, seed)
+        out = hip.ops().embed_fwd(ids, wte, wpe, p, seed, _index_flag(ids.device))
         ctx.save_for_backward(ids)
         ctx.p, ctx.seed = p, seed
         ctx.wte = wte if _fuse_target(wte) else None
@@ -1007,6 +1069,7 @@ class _LMHeadCE(torch.autograd.Function):
             n_valid = (labels1d != -100).sum().clamp_min(1).to(torch.float32)
         else:
             n_valid = torch.as_tensor(normalizer, dtype=torch.float32, device=h2d.device).clamp_min(1)
+        check_labels(labels1d, v)
         if _use_hip(logits):
             row_loss = hip.ops().softmax_xent_(logits, labels1d, v)  # logits <- softmax - onehot (in place)
         else:
@@ -1103,6 +1166,7 @@ class _TokenLogp(torch.autograd.Function):
         v = weight.shape[0]
         wp = _pad_rows(weight)
         logits = h2d @ wp.t()
+        check_labels(labels1d, v)
         if _use_hip(logits):
             row_loss = hip.ops().softmax_xent_(logits, labels1d, v)
         else:

@@ -39,7 +39,8 @@ from torch.optim.optimizer import Optimizer
 
 from ..ops import reference as ref
 from ..ops.linear import bump_weight_generation
-from ..parallel.exchange import canonical_strategy, make_exchange, wire_bytes_per_step
+from ..parallel.exchange import WireCounter, canonical_strategy, make_exchange, wire_bytes_per_step
+from ..parallel.elastic import inject as inject_fault
 from ..utils.timing import phase_of
 from .executors import HParams, make_executor
 from .plan import FlatPlan
@@ -115,6 +116,7 @@ class Lion(Optimizer):
         # run the vote path (encode -> collectives -> apply) even on a 1-rank
         # group: exercises the RCCL calls on a single GPU (tests/test_nccl_gpu.py)
         self._force_vote = False
+        self._wire_carry = WireCounter()  # counts of exchanges replaced after a regroup
 
     # ------------------------------------------------------------ topology
     def _world(self):
@@ -157,20 +159,32 @@ class Lion(Optimizer):
             self._alive_host = host
         return self._alive_dev
 
-    def _elastic_check(self) -> None:
-        """Real dropout: heartbeat before the vote; on a drop, switch to the
-        survivors' group (the plan is rebuilt below because the world changed)."""
+    def _elastic_setup(self) -> None:
+        """Real dropout (``elastic_timeout``): every vote runs as a guarded,
+        store-committed collective on the default group (parallel/elastic.py);
+        after a regroup the plan is rebuilt for the survivors' world."""
         if self.elastic_timeout is None or not (dist.is_available() and dist.is_initialized()):
             return
-        if self._elastic is None:
-            from ..parallel.elastic import ElasticMembership
+        from ..parallel.elastic import ElasticGroup
 
-            self._elastic = ElasticMembership(self.elastic_timeout, group=self.process_group)
-        grp = self._elastic.check(self._n_steps)
-        if grp is not None:
-            self.process_group = grp
-            self._dropped.clear()  # simulated-dropout ranks were numbered in the old group
-            self._alive_dev = None
+        if self.process_group is not None:
+            raise ValueError("elastic_timeout works on the default process group (group=None)")
+        if self.exchange_name == "ref_int64":
+            raise ValueError("the ref_int64 wire issues blocking per-tensor collectives; it cannot be "
+                             "elastic -- use exchange='a2a' or 'allgather'")
+        el = ElasticGroup.get(self.elastic_timeout)
+        if self._elastic is not el:
+            self._elastic = el
+            el.on_regroup(self._on_regroup)
+
+    def _on_regroup(self, el) -> None:
+        if self._exchange is not None:  # keep the wire counts of the abandoned exchange
+            w = self._exchange.wire
+            self._wire_carry.add(w.sent, w.recv, w.calls)
+        self._plan = None  # re-planned for the new world at the next step
+        self._exchange = None
+        self._dropped.clear()  # simulated-dropout ranks were numbered in the old group
+        self._alive_dev = None
 
     # --------------------------------------------------------------- plan
     def _get_plan(self, entries, world: int, rank: int):
@@ -203,7 +217,10 @@ class Lion(Optimizer):
         v = int.from_bytes(h.digest()[:7], "little")
         dev = plan.device if dist.get_backend(self.process_group) == "nccl" else torch.device("cpu")
         t = torch.tensor([v, -v], dtype=torch.int64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.process_group)
+        if self._elastic is not None:
+            self._elastic.all_reduce(t, op=dist.ReduceOp.MAX)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.process_group)
         if int(t[0]) != v or int(t[1]) != -v:
             raise RuntimeError(
                 "dlion Lion: parameter/gradient layout differs across ranks (different params have grads?); "
@@ -272,7 +289,8 @@ class Lion(Optimizer):
         if not entries:
             return loss
 
-        self._elastic_check()
+        inject_fault("before_step", self._n_steps)
+        self._elastic_setup()
         world, rank = self._world()
         self.last_world = world
         plan = self._get_plan(entries, world, rank)
@@ -295,21 +313,14 @@ class Lion(Optimizer):
         return loss
 
     def _distributed_step(self, plan, ex, meta, hps, grads, moms, world, rank, gscale=None):
-        xch = self._exchange
+        if self._elastic is not None:
+            return self._elastic_step(plan, ex, meta, hps, grads, moms, world, rank, gscale)
+        xch, t = self._exchange, self.phase_timer
         alive = self._alive(world, plan.device)
-        stochastic = self.max_grad_norm is not None
         if self.telemetry and self._agree is None:
             self._agree = torch.zeros(1, dtype=torch.int64, device=plan.device)
-        seed = (self.seed * 0x9E3779B1 + rank * 0x632BE59BD9B4E019 + 1) & 0x7FFFFFFFFFFFFFFF
-        t = self.phase_timer
-        states = []
-        for b in plan.buckets:  # encode bucket i, then its collective overlaps encode of i+1
-            hp = hps[b.group]
-            rr = (1.0 + 1.0 / hp.beta1) * self.max_grad_norm if stochastic else 0.0
-            with phase_of(t, "encode"):
-                ex.encode(meta, b, xch.send_view(b), hp, update_m=True, stochastic=stochastic, rr=rr, seed=seed,
-                          step=self._n_steps, grads=grads, moms=moms, gscale=gscale)
-                states.append(xch.launch(b, alive))
+        # encode bucket i, then its collective overlaps the encode of i+1
+        states = self._encode_launch(plan, ex, meta, hps, grads, moms, rank, gscale, alive)
         with phase_of(t, "exchange"):
             states = [xch.advance(b, s, alive) for b, s in zip(plan.buckets, states)]
         for b, s in zip(plan.buckets, states):
@@ -320,22 +331,109 @@ class Lion(Optimizer):
                          hps[b.group], own=xch.send_view(b) if self.telemetry else None,
                          agree=self._agree if self.telemetry else None)
 
+    def _encode_launch(self, plan, ex, meta, hps, grads, moms, rank, gscale, alive):
+        xch, stochastic, t = self._exchange, self.max_grad_norm is not None, self.phase_timer
+        seed = (self.seed * 0x9E3779B1 + rank * 0x632BE59BD9B4E019 + 1) & 0x7FFFFFFFFFFFFFFF
+        states = []
+        for b in plan.buckets:
+            hp = hps[b.group]
+            rr = (1.0 + 1.0 / hp.beta1) * self.max_grad_norm if stochastic else 0.0
+            with phase_of(t, "encode"):
+                ex.encode(meta, b, xch.send_view(b), hp, update_m=True, stochastic=stochastic, rr=rr, seed=seed,
+                          step=self._n_steps, grads=grads, moms=moms, gscale=gscale)
+                states.append(xch.launch(b, alive))
+            if b.index == 0:
+                inject_fault("after_launch", self._n_steps)
+        return states
+
+    def _elastic_step(self, plan, ex, meta, hps, grads, moms, world, rank, gscale=None):
+        """The vote as guarded collectives: the host polls each phase to
+        completion (bounded by ``elastic_timeout``) before anything on the
+        compute stream depends on it, and applies the step only after the
+        store-arbitrated commit.  On a failure the survivors regroup and vote
+        again from the intact encoded planes (the momentum was already
+        advanced by the encode, exactly once) with a 1-bit all-gather over
+        the new group, on the old plan's layout."""
+        from ..parallel.elastic import flatten_works
+
+        el, xch, t = self._elastic, self._exchange, self.phase_timer
+        alive = self._alive(world, plan.device)
+        if self.telemetry and self._agree is None:
+            self._agree = torch.zeros(1, dtype=torch.int64, device=plan.device)
+        tie = ref.TIE_CODES[self.tie_break]
+        ok = True
+        try:
+            states = self._encode_launch(plan, ex, meta, hps, grads, moms, rank, gscale, alive)
+            with phase_of(t, "exchange"):
+                ok = el.wait_works(flatten_works(states))
+                if ok:
+                    states = [xch.advance(b, s, alive) for b, s in zip(plan.buckets, states)]
+                    inject_fault("in_allgather", self._n_steps)
+                    ok = el.wait_works(flatten_works(states))
+        except Exception as e:  # noqa: BLE001 - gloo reports a dead peer at issue time
+            import logging
+
+            logging.getLogger(__name__).warning("dlion: vote collective failed: %s", str(e)[:200])
+            ok = False
+        with phase_of(t, "exchange"):
+            committed = el.commit(ok)
+        if committed:
+            for b, s in zip(plan.buckets, states):
+                a = xch.finish(b, s, alive)
+                with phase_of(t, "apply"):
+                    ex.apply(meta, b, a.planes, a.stride, alive, a.mode, tie, a.neg, hps[b.group],
+                             own=xch.send_view(b) if self.telemetry else None,
+                             agree=self._agree if self.telemetry else None)
+            inject_fault("after_vote", self._n_steps)
+            return
+        # ---- somebody failed: regroup, then vote again among the survivors
+        from ..parallel.exchange import AllGatherExchange
+
+        send = xch.send
+        while True:
+            el.regroup({"step": self._n_steps, "where": "vote"})
+            w2, r2 = el.world, el.rank
+            if w2 == 1:  # the last one standing votes alone: its own signs
+                rex, alive2 = None, torch.ones(1, dtype=torch.uint8, device=plan.device)
+                break
+            alive2 = torch.ones(w2, dtype=torch.uint8, device=plan.device)
+            rex = AllGatherExchange(plan, None, r2, w2, ex, tie, ref.VOTE_CODES[self.vote], send=send)
+            try:
+                works = [rex.launch(b, alive2) for b in plan.buckets]
+                ok = el.wait_works(works)
+            except Exception:  # noqa: BLE001
+                ok = False
+            if el.commit(ok):
+                break
+        for b in plan.buckets:
+            if rex is None:
+                planes, stride, mode = send[b.byte_off:b.byte_off + b.nbytes], b.nbytes, ref.VOTE_CODES[self.vote]
+            else:
+                a = rex.finish(b, None, alive2)
+                planes, stride, mode = a.planes, a.stride, a.mode
+            ex.apply(meta, b, planes, stride, alive2, mode, tie, None, hps[b.group])
+        if rex is not None:
+            self._wire_carry.add(rex.wire.sent, rex.wire.recv, rex.wire.calls)
+
     # ---------------------------------------------------------- telemetry
     def stats(self, reset: bool = True) -> dict:
         """Wire counters and (telemetry=True) vote agreement since last reset.
         Reading the agreement count synchronises with the device."""
         out = {"world": self.last_world, "exchange": self.exchange_name, "steps": self._n_steps}
-        if self._exchange is not None:
-            out.update(self._exchange.wire.snapshot())
-            if reset:
-                self._exchange.wire.reset()
+        if self._exchange is not None or self._wire_carry.calls:
+            tot = WireCounter()
+            for w in (self._wire_carry, getattr(self._exchange, "wire", None)):
+                if w is not None:
+                    tot.add(w.sent, w.recv, w.calls)
+                    if reset:
+                        w.reset()
+            out.update(tot.snapshot())
         if self._plan is not None:
             out["numel"] = sum(s.numel for s in self._plan.segments)
             out["n_buckets"] = len(self._plan.buckets)
             out["wire_bytes_analytic"] = wire_bytes_per_step(out["numel"], self.last_world, self.exchange_name)
         if self._elastic is not None:
-            out["live_ranks"] = list(self._elastic.members)
-            out["dropout_events"] = list(self._elastic.events)
+            out.update(self._elastic.stats())
         if self._agree is not None:
             out["vote_agree"] = int(self._agree.item())
             if reset:

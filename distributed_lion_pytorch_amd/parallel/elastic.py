@@ -1,42 +1,64 @@
-"""Real worker dropout: detect dead ranks between optimizer steps and keep
-training on the survivors.
+"""Worker dropout at any instant: bounded-time collectives, a store-arbitrated
+commit per collective, and regrouping of the survivors into a fresh default
+process group.
 
 The reference claims robustness to worker drop-out (/root/reference/README.md:2)
 but its blocking per-tensor ``dist.all_gather`` (distributed_lion.py:81) hangs
 every survivor until the c10d watchdog kills the job.  Majority
 vote over the *live* voters is still a valid Distributed Lion step, so a dead
-rank only has to be detected and cut out of the vote group:
+worker only has to be detected and cut out -- wherever it died: in backward,
+between the launch of the vote all-to-all and its completion, inside the
+1-bit all-gather, or between steps.
 
-1. **Heartbeat.**  Before its vote collectives, every member publishes
-   ``<prefix>/<gen>/<step>/hb/<rank>`` to the rendezvous store and waits (with
-   ``timeout_s``) for all members' keys.  No collective is entered with a
-   rank that has not checked in, so nothing can hang on it.
-2. **Agreement.**  On timeout each survivor proposes the members whose keys it
-   sees; the first proposal written with ``compare_set`` is the decision for
-   everybody, so all survivors adopt the identical member list even when a
-   slow rank checks in during the race.  A rank left out of the decision
-   (it was only late) raises :class:`WorkerExcluded` instead of voting on.
-3. **Regroup.**  Survivors build a new process group over themselves only
-   (``new_group(..., use_local_synchronization=True)``: the dead rank never has
-   to call it) and the optimizer re-plans for the new world size on the same
-   step.  Parameters stay identical on the survivors because they were
-   identical before and every survivor applies the same vote.
+Protocol (all ranks run the same sequence of *guarded* collectives):
 
-Granularity is one optimizer step: a rank that dies *inside* a collective is
-still caught by the backend's own timeout.  The store must outlive the dead
-rank -- torchrun's agent-hosted store does; with a rank-0-hosted TCPStore,
-rank 0 cannot be the one that drops.
+1. **Bounded wait.**  A guarded collective is issued asynchronously and its
+   works are polled on the host (``is_completed``) against a deadline of
+   ``timeout_s``.  Nothing on the compute stream ever waits on a work that has
+   not completed, so a collective stuck on a dead peer can be abandoned (gloo
+   reports a closed peer at once; RCCL kernels spin until aborted).
+2. **Commit.**  Completing locally does not mean every peer completed (a ring
+   or all-to-all can finish on some ranks only).  So no rank *uses* a result
+   before the rendezvous store -- which outlives the workers: torchrun's agent
+   or :mod:`..launch` hosts it -- has recorded the outcome: each rank adds
+   itself to ``<gen>/<seq>/ok`` or proposes ``fail``; the last of the W adders
+   writes ``all``.  ``compare_set`` makes the first written decision final, so
+   every survivor acts on the same outcome (apply the step, or regroup).
+3. **Membership.**  After a ``fail`` every live rank checks in under
+   ``<gen>/members``; after ``grace_s`` the first proposal of the ranks seen is
+   the new member list for everybody.  A rank left out (it was only late)
+   raises :class:`WorkerExcluded`.
+4. **Regroup.**  Every process group of the process is aborted
+   (``ncclCommAbort`` under RCCL -- it stops the spinning kernels; gloo's abort
+   runs off-thread because it waits for a hung, not dead, peer) and the
+   survivors initialise a *new default* group over the same store with dense
+   ranks.  Everything that resolves the group at call time -- Lion, HF /
+   accelerate collectives (their cached process counts are updated by a
+   listener, trainer/async_trainer.py) -- then runs on the survivors.  The
+   failed collective is re-issued on the new group; Lion re-votes the step
+   from its intact encoded sign planes (optim/lion.py).
+
+Cost while nobody fails: one host wait for the collective plus three store
+round trips per guarded collective (one per optimizer step); measured in
+profiles/stress.  A rank's identity across regroups is its *original* global
+rank (``ElasticGroup.me``).
 """
 from __future__ import annotations
 
 import datetime
 import json
 import logging
-from typing import List, Optional
+import os
+import threading
+import time
+from typing import Callable, List, Optional
 
+import torch
 import torch.distributed as dist
 
 log = logging.getLogger(__name__)
+
+DEFAULT_GRACE_S = 5.0
 
 
 class WorkerExcluded(RuntimeError):
@@ -49,70 +71,330 @@ def _default_store():
     return c10d._get_default_store()
 
 
-class ElasticMembership:
-    """Tracks the live members of a vote group across optimizer steps.
+_GRAVEYARD: list = []  # aborted gloo groups: keep them referenced so no destructor blocks the caller
 
-    ``check(step)`` returns ``None`` while everybody is alive, or the new
-    process group over the survivors after a drop (also kept in ``.group``).
-    """
 
-    def __init__(self, timeout_s: float = 60.0, group=None, store=None, prefix: str = "dlion/elastic"):
+def _quiet_abort(pg) -> None:
+    try:
+        pg.abort()
+    except Exception:  # noqa: BLE001 - best effort on a broken group
+        pass
+
+
+def discard_process_groups(backend: str) -> None:
+    """Abort and forget every process group of this process so a new default
+    group can be initialised.  RCCL: ``_abort_process_group()`` (all
+    communicators aborted inside one group call, kernels stop spinning).
+    gloo: its ``abort()`` blocks until a hung peer's pending op ends, so it runs
+    on a daemon thread and the bookkeeping that ``_abort_process_group`` would
+    do is done here directly."""
+    from torch.distributed import distributed_c10d as c10d
+
+    if not dist.is_initialized():
+        return
+    if backend == "nccl":
+        c10d._abort_process_group()
+        return
+    w = c10d._world
+    for pg in list(w.pg_names):
+        _GRAVEYARD.append(pg)
+        threading.Thread(target=_quiet_abort, args=(pg,), daemon=True).start()
+    c10d._update_default_pg(None)
+    for m in (w.pg_map, w.pg_names, w.pg_group_ranks, w.pg_backend_config, w.pg_to_tag, w.tags_to_pg,
+              w.pg_coalesce_state):
+        m.clear()
+    c10d._unregister_all_process_groups()
+    w.group_count = 0
+
+
+class ElasticGroup:
+    """Process-wide membership of the data-parallel group, and guarded
+    collectives on it (see module docstring).  One instance per process
+    (:meth:`get`); it always works on the *default* process group."""
+
+    _current: Optional["ElasticGroup"] = None
+
+    def __init__(self, timeout_s: float = 60.0, grace_s: Optional[float] = None, store=None,
+                 poll_s: float = 2e-4):
         if not (dist.is_available() and dist.is_initialized()):
-            raise RuntimeError("ElasticMembership needs an initialised torch.distributed process group")
-        self.timeout = datetime.timedelta(seconds=float(timeout_s))
-        self.group = group
-        self.store = store if store is not None else _default_store()
-        self.prefix = prefix
-        self.me = dist.get_rank()
-        self.members: List[int] = sorted(dist.get_process_group_ranks(group)) if group is not None else list(
-            range(dist.get_world_size()))
+            raise RuntimeError("ElasticGroup needs an initialised torch.distributed default group")
+        from torch.distributed import PrefixStore
+
+        self.backend = dist.get_backend()
+        self.timeout = float(timeout_s)
+        self._grace_fixed = float(grace_s) if grace_s is not None else None
+        self.store = PrefixStore("dlion/elastic", store if store is not None else _default_store())
+        self.me = dist.get_rank()  # stable identity: the original global rank
+        self.members: List[int] = list(range(dist.get_world_size()))
         self.gen = 0
+        self.seq = 0
         self.events: List[dict] = []
-        self._last_step: Optional[int] = None
+        self.stall_s = 0.0
+        self.commits = 0
+        self._poll = float(poll_s)
+        self._last_commit_t: Optional[float] = None
+        self._intervals: List[float] = []  # recent times between commits (~ the step time)
+        self._listeners: List[Callable[["ElasticGroup"], None]] = []
+        # the backend's own timeout must never fire before ours (RCCL's watchdog
+        # would tear the process down)
+        self.pg_timeout = datetime.timedelta(seconds=max(600.0, 10.0 * self.timeout))
+        self.device = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else None
+        self._pg = dist.group.WORLD
 
-    # ------------------------------------------------------------------ keys
-    def _hb(self, step: int, r: int) -> str:
-        return f"{self.prefix}/{self.gen}/{step}/hb/{r}"
+    @classmethod
+    def get(cls, timeout_s: float = 60.0, **kw) -> "ElasticGroup":
+        cur = cls._current
+        if cur is None or not dist.is_initialized() or (dist.group.WORLD is not cur._pg):
+            cur = cls._current = cls(timeout_s, **kw)
+        return cur
 
-    def _decision(self, step: int) -> str:
-        return f"{self.prefix}/{self.gen}/{step}/decision"
+    @classmethod
+    def active(cls) -> Optional["ElasticGroup"]:
+        cur = cls._current
+        if cur is not None and dist.is_initialized() and dist.group.WORLD is cur._pg:
+            return cur
+        return None
 
-    def _cleanup(self, step: int) -> None:
-        # keys of two steps ago can go: every member has passed that heartbeat
-        for r in self.members:
-            try:
-                self.store.delete_key(self._hb(step - 2, r))
-            except Exception:  # noqa: BLE001 - best effort (older stores lack delete_key)
-                return
-
-    # ----------------------------------------------------------------- check
-    def check(self, step: int):
-        if len(self.members) <= 1:
-            return None
-        self.store.set(self._hb(step, self.me), "1")
-        keys = [self._hb(step, r) for r in self.members]
-        try:
-            self.store.wait(keys, self.timeout)
-            self._cleanup(step)
-            return None
-        except Exception:  # noqa: BLE001 - DistStoreError / RuntimeError on timeout
-            pass
-        seen = [r for r in self.members if self.store.check([self._hb(step, r)])]
-        decided = self.store.compare_set(self._decision(step), "", json.dumps(seen))
-        survivors = sorted(json.loads(decided))
-        dropped = sorted(set(self.members) - set(survivors))
-        if self.me not in survivors:
-            raise WorkerExcluded(f"rank {self.me} was excluded from the vote group at step {step} "
-                                 f"(survivors {survivors})")
-        if not dropped:  # everybody made it in the end
-            return None
-        log.warning("dlion elastic: step %d: ranks %s dropped; continuing on %s", step, dropped, survivors)
-        self.events.append({"step": step, "dropped": dropped, "survivors": survivors})
-        self.members = survivors
-        self.gen += 1
-        self.group = dist.new_group(ranks=survivors, use_local_synchronization=True)
-        return self.group
-
+    # ------------------------------------------------------------- topology
     @property
     def world(self) -> int:
         return len(self.members)
+
+    @property
+    def rank(self) -> int:
+        return self.members.index(self.me)
+
+    @property
+    def grace(self) -> float:
+        """Membership check-in window after a failure.  Live ranks arrive within
+        the skew between ranks (a fraction of a step), so by default it is 3x
+        the longest of the last 8 intervals between commits, at least 1 s and at
+        most ``timeout`` (5 s before any history)."""
+        if self._grace_fixed is not None:
+            return self._grace_fixed
+        if not self._intervals:
+            return min(self.timeout, DEFAULT_GRACE_S)
+        return min(self.timeout, max(1.0, 3.0 * max(self._intervals)))
+
+    def on_regroup(self, fn: Callable[["ElasticGroup"], None]) -> None:
+        if fn not in self._listeners:
+            self._listeners.append(fn)
+
+    # ------------------------------------------------------ bounded waiting
+    def wait_works(self, works) -> bool:
+        """True when every work completed without error before the deadline.
+        Only then is ``work.wait()`` called (it is what makes the compute
+        stream depend on the collective)."""
+        start = time.monotonic()
+        deadline = start + self.timeout
+        next_check = start + 0.02
+        dec = f"{self.gen}/{self.seq}/decision"
+        for w in works:
+            if w is None:
+                continue
+            try:
+                while not w.is_completed():
+                    now = time.monotonic()
+                    if now > deadline:
+                        return False
+                    if now > next_check:  # a peer already declared this collective failed
+                        next_check = now + 0.02
+                        if self.store.check([dec]):
+                            return False
+                    time.sleep(self._poll)
+                w.wait()
+            except Exception as e:  # noqa: BLE001 - a failed collective is what this detects
+                log.warning("dlion elastic: collective failed on rank %d: %s", self.me, str(e)[:200])
+                return False
+        return True
+
+    # --------------------------------------------------------------- commit
+    def commit(self, ok: bool) -> bool:
+        """Store-arbitrated outcome of the current guarded collective: True
+        when every member completed it (the result may be used), False when
+        the survivors must regroup.  Identical on every surviving rank."""
+        key = f"{self.gen}/{self.seq}"
+        self.seq += 1
+        self.commits += 1
+        dec = key + "/decision"
+        now = time.monotonic()
+        if self._last_commit_t is not None:
+            self._intervals = (self._intervals + [now - self._last_commit_t])[-8:]
+        self._last_commit_t = now
+        if ok:
+            if self.store.add(key + "/ok", 1) == self.world:
+                val = self.store.compare_set(dec, "", "all")
+                if val == b"all" and self.seq > 2:  # everybody is past seq-2: drop its keys
+                    old = f"{self.gen}/{self.seq - 3}"
+                    for k in ("/ok", "/decision"):
+                        try:
+                            self.store.delete_key(old + k)
+                        except Exception:  # noqa: BLE001 - best effort
+                            pass
+                return val == b"all"
+        else:
+            self.store.compare_set(dec, "", "fail")
+        try:
+            self.store.wait([dec], datetime.timedelta(seconds=self.timeout + self.grace))
+            val = self.store.get(dec)
+        except Exception:  # noqa: BLE001 - no decision in time: somebody is gone
+            val = self.store.compare_set(dec, "", "fail")
+        return val == b"all"
+
+    # --------------------------------------------------------------- regroup
+    def regroup(self, tag: Optional[dict] = None) -> None:
+        """Agree on the survivors, abort every group, initialise the new default
+        group over them, notify listeners."""
+        t0 = time.monotonic()
+        ns = f"{self.gen}/members"
+        self.store.set(f"{ns}/alive/{self.me}", "1")
+        keys = [f"{ns}/alive/{r}" for r in self.members]
+        try:
+            self.store.wait(keys, datetime.timedelta(seconds=self.grace))
+        except Exception:  # noqa: BLE001 - somebody did not check in
+            pass
+        seen = [r for r in self.members if self.store.check([f"{ns}/alive/{r}"])]
+        survivors = sorted(json.loads(self.store.compare_set(f"{ns}/decision", "", json.dumps(seen))))
+        discard_process_groups(self.backend)
+        if self.me not in survivors:
+            raise WorkerExcluded(f"rank {self.me} was excluded from the group in generation {self.gen} "
+                                 f"(survivors {survivors})")
+        dropped = sorted(set(self.members) - set(survivors))
+        self.gen += 1
+        self.seq = 0
+        self.members = survivors
+        self._last_commit_t = None
+        from torch.distributed import PrefixStore
+
+        kw = dict(backend=self.backend, store=PrefixStore(f"pg/{self.gen}", self.store), rank=self.rank,
+                  world_size=self.world, timeout=self.pg_timeout)
+        if self.device is not None:
+            kw["device_id"] = self.device
+        dist.init_process_group(**kw)
+        self._pg = dist.group.WORLD
+        stall = time.monotonic() - t0
+        self.stall_s += stall
+        ev = dict(tag or {})
+        ev.update({"generation": self.gen, "dropped": dropped, "survivors": survivors,
+                   "regroup_s": round(stall, 3)})
+        self.events.append(ev)
+        log.warning("dlion elastic: ranks %s dropped; continuing on %s (new rank %d of %d)", dropped, survivors,
+                    self.rank, self.world)
+        for fn in list(self._listeners):
+            fn(self)
+
+    # ----------------------------------------------------- guarded execution
+    def run(self, issue: Callable[[], tuple], tag: Optional[dict] = None):
+        """``issue()`` launches async collectives on the *current* default
+        group and returns ``(works, result)``.  Returns ``result`` once every
+        member completed; on failure regroups and issues again."""
+        while True:
+            t0 = time.monotonic()
+            try:
+                works, result = issue()
+                ok = self.wait_works(works)
+            except WorkerExcluded:
+                raise
+            except Exception as e:  # noqa: BLE001 - issuing on a broken group
+                log.warning("dlion elastic: issuing a collective failed: %s", str(e)[:200])
+                ok = False
+            if self.commit(ok):
+                return result
+            self.stall_s += time.monotonic() - t0
+            self.regroup(tag)
+
+    # ---------------------------------------------- guarded collective helpers
+    def _dev(self, t: torch.Tensor) -> torch.Tensor:
+        return t.to(self.device) if self.device is not None and t.device != self.device else t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenation along dim 0 of every member's ``t`` (``t`` 0-dim ->
+        1-element rows), on ``t``'s device."""
+        src = self._dev(t.reshape(1) if t.dim() == 0 else t).contiguous()
+
+        def issue():
+            outs = [torch.empty_like(src) for _ in range(self.world)]
+            return [dist.all_gather(outs, src, async_op=True)], outs
+
+        outs = self.run(issue, {"where": "all_gather"})
+        return torch.cat(outs, dim=0).to(t.device)
+
+    def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+        """In-place all-reduce of ``t`` over the members (re-done from ``t``'s
+        value at the call after a regroup)."""
+        orig = t.detach().clone()
+        buf = self._dev(t)
+
+        def issue():
+            buf.copy_(self._dev(orig))
+            return [dist.all_reduce(buf, op=op, async_op=True)], buf
+
+        self.run(issue, {"where": "all_reduce"})
+        if buf is not t:
+            t.copy_(buf)
+        return t
+
+    def barrier(self) -> None:
+        self.all_reduce(torch.zeros(1, device=self.device or "cpu"))
+
+    def stats(self) -> dict:
+        return {"live_ranks": list(self.members), "dropout_events": list(self.events),
+                "elastic_generation": self.gen, "elastic_commits": self.commits,
+                "elastic_stall_s": round(self.stall_s, 3)}
+
+
+def flatten_works(states) -> list:
+    """Works out of the exchange's per-bucket states (a work, a list, or None)."""
+    out = []
+    for s in states:
+        if isinstance(s, (list, tuple)):
+            out.extend(x for x in s if x is not None)
+        elif s is not None:
+            out.append(s)
+    return out
+
+
+# ---------------------------------------------------------------- fault injection
+_FAULT_PHASES = ("before_step", "backward", "after_launch", "in_allgather", "after_vote")
+
+
+def parse_fault(spec: Optional[str]) -> list:
+    """``"rank:step:phase[,rank:step:phase...]"`` (``DLION_FAULT``): the process
+    of original global rank ``rank`` kills itself (SIGKILL: no teardown,
+    sockets just close) at optimizer step ``step`` in ``phase`` -- one of
+    before_step, backward (inside autograd), after_launch (vote all-to-all
+    issued, not completed), in_allgather (vote all-gather issued), after_vote
+    (step applied)."""
+    out = []
+    for item in (spec or "").split(","):
+        if not item.strip():
+            continue
+        r, s, ph = item.strip().split(":")
+        if ph not in _FAULT_PHASES:
+            raise ValueError(f"DLION_FAULT phase must be one of {_FAULT_PHASES}, got {ph!r}")
+        out.append((int(r), int(s), ph))
+    return out
+
+
+_FAULT_CACHE: list = []
+
+
+def fault_spec() -> list:
+    if not _FAULT_CACHE:
+        _FAULT_CACHE.append(parse_fault(os.environ.get("DLION_FAULT")))
+    return _FAULT_CACHE[0]
+
+
+def inject(phase: str, step: int) -> None:
+    """Die here if ``DLION_FAULT`` names this rank, step and phase."""
+    faults = fault_spec()
+    if not faults or not (dist.is_available() and dist.is_initialized()):
+        return
+    eg = ElasticGroup.active()
+    me = eg.me if eg is not None else dist.get_rank()
+    if (me, step, phase) in faults:
+        import signal
+        import sys
+
+        print(json.dumps({"rank": me, "event": "fault", "step": step, "phase": phase}), file=sys.stderr, flush=True)
+        os.kill(os.getpid(), signal.SIGKILL)

@@ -77,13 +77,15 @@ class WireCounter:
 
 
 class VoteExchange:
-    def __init__(self, plan: FlatPlan, group, rank: int, world: int, executor, tie: int, mode: int):
+    def __init__(self, plan: FlatPlan, group, rank: int, world: int, executor, tie: int, mode: int,
+                 send: Optional[torch.Tensor] = None):
         self.plan, self.group, self.rank, self.world = plan, group, rank, world
         self.executor = executor
         self.tie, self.mode = tie, mode
         self.wire = WireCounter()
-        dev = plan.device
-        self.send = torch.zeros(plan.total_bytes, dtype=torch.uint8, device=dev)
+        # ``send``: reuse already-encoded planes (the elastic re-vote after a regroup)
+        self.send = send if send is not None else torch.zeros(plan.total_bytes, dtype=torch.uint8,
+                                                              device=plan.device)
 
     def send_view(self, b: Bucket) -> torch.Tensor:
         return self.send[b.byte_off:b.byte_off + b.nbytes]
@@ -115,7 +117,8 @@ class AllGatherExchange(VoteExchange):
         return work
 
     def finish(self, b, work, alive):
-        work.wait()
+        if work is not None:
+            work.wait()
         return ApplyArgs(planes=self.recv_view(b), stride=b.nbytes, mode=self.mode)
 
 

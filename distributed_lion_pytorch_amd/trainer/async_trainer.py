@@ -142,6 +142,64 @@ class AsyncMixin:
             loss = torch.where(torch.isfinite(loss), loss, avg.to(loss.dtype))
         return loss
 
+    # ------------------------------------------------------ worker dropout (HF path)
+    def _elastic(self):
+        """With ``--lion_elastic_timeout`` on a multi-rank run, the process-wide
+        :class:`ElasticGroup`: Lion's vote is guarded by it, and so are the
+        collectives HF / accelerate issue on their own -- the per-step
+        ``num_items_in_batch`` gather, the logging loss gather, evaluation
+        gathers -- so a worker dying anywhere leaves the survivors a
+        regrouped default group instead of a hang (parallel/elastic.py)."""
+        t = getattr(self.args, "lion_elastic_timeout", None)
+        if t is None or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return None
+        from ..parallel.elastic import ElasticGroup
+
+        el = ElasticGroup.active()
+        if el is None or getattr(self, "_dlion_elastic", None) is not el:
+            el = ElasticGroup.get(t)
+            self._dlion_elastic = el
+            el.on_regroup(self._on_regroup)
+            _install_guarded_gathers(self, el)
+        return el
+
+    def _on_regroup(self, el) -> None:
+        """accelerate caches the world in its shared state: point it at the
+        survivors (new default group, dense ranks)."""
+        from accelerate.state import AcceleratorState, PartialState
+
+        for shared in (PartialState._shared_state, AcceleratorState._shared_state):
+            if "num_processes" in shared:
+                shared["num_processes"] = el.world
+            if "process_index" in shared:
+                shared["process_index"] = el.rank
+        self.state.is_world_process_zero = el.rank == 0
+        # the dead rank's data shard is simply not consumed any more; the
+        # survivors keep their own shards (BatchSamplerShard is per process)
+
+    def compute_loss(self, model, inputs, *a, **kw):
+        loss = super().compute_loss(model, inputs, *a, **kw)
+        from ..parallel.elastic import fault_spec, inject
+
+        if fault_spec():  # DLION_FAULT=rank:step:backward -- die inside autograd
+            t = loss[0] if isinstance(loss, tuple) else loss
+            if isinstance(t, torch.Tensor) and t.requires_grad:
+                n = self.state.global_step
+                t.register_hook(lambda g, n=n: inject("backward", n))
+        return loss
+
+    def train(self, *a, **kw):
+        if getattr(self.args, "lion_elastic_timeout", None) is not None:
+            # no forward-time buffer broadcast on DDP's (possibly stale) group;
+            # buffers are deterministic and every rank builds them identically
+            self.args.ddp_broadcast_buffers = False
+            self._elastic()
+        out = super().train(*a, **kw)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            same = replicas_identical(self.model, self._elastic())
+            self.log({"replicas_identical": float(same), "world_end": float(dist.get_world_size())})
+        return out
+
     def _training_step(self, model, inputs, num_items_in_batch=None):
         from ..ops.linear import begin_fusion_window, end_fusion_window
 
@@ -157,6 +215,10 @@ class AsyncMixin:
             raise
         if fuse and self.accelerator.sync_gradients:
             end_fusion_window()  # last micro-batch of the step: every gradient is in param.grad now
+        if self.accelerator.sync_gradients:
+            from ..ops.fused import check_index_errors
+
+            check_index_errors()  # out-of-range ids / labels flagged by the kernels (no stall)
         return loss
 
     def _prepare_input(self, data):
@@ -254,6 +316,48 @@ class AsyncMixin:
             state = torch.load(path, map_location="cpu", weights_only=True)
             self.optimizer.load_state_dict(state)
             logger.info("restored per-rank optimizer state from %s", path)
+
+
+def replicas_identical(model: torch.nn.Module, elastic=None) -> bool:
+    """Do all ranks hold bit-identical parameters?  (an int64 digest per rank,
+    gathered -- guarded when ``elastic`` is given)."""
+    import hashlib
+
+    inner = getattr(model, "module", model)
+    h = hashlib.sha256()
+    for p in inner.parameters():
+        h.update(p.detach().float().cpu().numpy().tobytes())
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    d = torch.tensor([int.from_bytes(h.digest()[:7], "little")], dtype=torch.int64, device=dev)
+    if elastic is not None:
+        allv = elastic.all_gather(d)
+    else:
+        parts = [torch.empty_like(d) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, d)
+        allv = torch.cat(parts)
+    return len(set(allv.tolist())) == 1
+
+
+def _install_guarded_gathers(trainer, el) -> None:
+    """Route HF's own collectives through ``el``: ``transformers.trainer.nested_gather``
+    (the logging loss gather) and this trainer's ``accelerator.gather`` (the
+    ``num_items_in_batch`` sum, ``gather_for_metrics`` in evaluation)."""
+    import transformers.trainer as hf_trainer
+    from accelerate.utils import recursively_apply
+
+    def gather_one(t):
+        return el.all_gather(t.reshape(1) if t.dim() == 0 else t)
+
+    def guarded_gather(tensor):
+        return recursively_apply(gather_one, tensor, error_on_other_type=True)
+
+    def guarded_nested_gather(tensors, parallel_mode=None, name=None):
+        if tensors is None:
+            return None
+        return recursively_apply(gather_one, tensors, error_on_other_type=True)
+
+    trainer.accelerator.gather = guarded_gather
+    hf_trainer.nested_gather = guarded_nested_gather
 
 
 class AsyncTrainer(AsyncMixin, Trainer):

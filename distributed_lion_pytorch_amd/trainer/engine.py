@@ -18,6 +18,8 @@ from typing import Callable, Iterable, Optional
 import torch
 import torch.distributed as dist
 
+from ..parallel.elastic import fault_spec
+from ..parallel.elastic import inject as inject_fault
 from ..utils.timing import phase_of
 
 
@@ -93,6 +95,9 @@ class TrainStep:
             with grad_accumulation_fusion(self.fuse_grad_accumulation, micro_batches=self.grad_accum):
                 for batch in micro_batches:
                     loss = self.loss_fn(self.model, batch) / self.grad_accum
+                    if fault_spec() and loss.requires_grad:  # DLION_FAULT=rank:step:backward
+                        n = getattr(self.optimizer, "_n_steps", 0)
+                        loss.register_hook(lambda g, n=n: inject_fault("backward", n))
                     loss.backward()
                     total = loss.detach() if total is None else total + loss.detach()
         if self.max_grad_norm is not None and self.max_grad_norm > 0:
@@ -109,6 +114,9 @@ class TrainStep:
         self.optimizer.zero_grad(set_to_none=True)
         if t is not None:
             t.step()
+        from ..ops.fused import check_index_errors
+
+        check_index_errors()  # out-of-range token ids / labels flagged by the kernels (one step late, no stall)
         return total
 
 

@@ -3,18 +3,28 @@
 Lion async worker-dropout stress, 1 rank drops mid-run").
 
 Every rank trains its own replica on its own synthetic data through the
-native engine (no gradient all-reduce, Lion vote sync).  At ``--drop_step``
-rank ``--drop_rank`` dies without warning (``os._exit``: no teardown, no
-goodbye).  With ``--elastic_timeout`` the survivors detect it at the next
-vote heartbeat, regroup and carry on (parallel/elastic.py); the run then
-checks that the survivors' parameters are still bit-identical and reports
-tokens/s before and after the drop.  Without ``--elastic_timeout`` the
-survivors hang in the collective exactly like the reference does
-(/root/reference/distributed_lion.py:81) -- do not run that on shared boxes.
+native engine (no gradient all-reduce, Lion vote sync).  At optimizer step
+``--drop_step`` the process of rank ``--drop_rank`` kills itself (SIGKILL: no
+teardown, no goodbye) at ``--drop_phase``:
 
-  torchrun --nproc-per-node 8 --master-addr 127.0.0.1 dropout_stress.py \
+  before_step   between steps
+  backward      inside autograd (the survivors are already in their vote)
+  after_launch  after issuing the vote all-to-all, before it completed
+  in_allgather  after issuing the vote's 1-bit all-gather
+  after_vote    right after applying the step
+
+With ``--elastic_timeout`` the survivors detect it (bounded wait on the vote
+collectives), agree on the outcome through the rendezvous store, regroup,
+re-vote that step among themselves and carry on (parallel/elastic.py); the run
+then checks that the survivors' parameters are bit-identical and reports
+tokens/s before and after the drop plus the regroup stall.
+
+Launch it with the failure-tolerant launcher (torchrun stops every worker
+when one dies; this launcher hosts the store itself, so even rank 0 may drop):
+
+  python -m distributed_lion_pytorch_amd.launch --nproc 8 --max_failures 1 dropout_stress.py \
       --model llama-3-8b --micro_batch 1 --seq_len 2048 --steps 20 --drop_rank 5 --drop_step 8
-  # CPU smoke (gloo): --model llama-tiny / gpt2-tiny --device cpu
+  # CPU rehearsal (gloo): --model llama-tiny / gpt2-tiny --device cpu
 """
 from __future__ import annotations
 
@@ -32,6 +42,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from distributed_lion_pytorch_amd import Lion  # noqa: E402
 from distributed_lion_pytorch_amd.models.registry import build_model, load_config  # noqa: E402
+from distributed_lion_pytorch_amd.parallel.elastic import ElasticGroup  # noqa: E402
 from distributed_lion_pytorch_amd.trainer.engine import TrainStep, broadcast_parameters  # noqa: E402
 
 
@@ -45,7 +56,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--drop_rank", type=int, default=1)
     ap.add_argument("--drop_step", type=int, default=8)
+    ap.add_argument("--drop_phase", default="backward",
+                    choices=["before_step", "backward", "after_launch", "in_allgather", "after_vote"])
     ap.add_argument("--elastic_timeout", type=float, default=30.0)
+    ap.add_argument("--elastic_grace", type=float, default=None,
+                    help="membership check-in window after a failure (default min(timeout, 5 s))")
     ap.add_argument("--exchange", default="a2a")
     ap.add_argument("--lr", type=float, default=1e-5)
     ap.add_argument("--weight_decay", type=float, default=0.0)
@@ -57,6 +72,8 @@ def parse():
 
 def main():
     a = parse()
+    if a.drop_rank >= 0:
+        os.environ["DLION_FAULT"] = f"{a.drop_rank}:{a.drop_step}:{a.drop_phase}"
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -66,6 +83,9 @@ def main():
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         if a.backend == "nccl":
+            # the elastic path aborts communicators itself; the watchdog must not kill the process first
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
+            os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
@@ -74,8 +94,9 @@ def main():
         dev = torch.device("cpu")
         dist.init_process_group("gloo")
         dtype = torch.float32
-    if a.drop_rank == 0:
-        raise SystemExit("--drop_rank 0: rank 0 may host the rendezvous store; drop another rank")
+    if a.drop_rank == 0 and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") != "True":
+        raise SystemExit("--drop_rank 0 needs a launcher-hosted store (python -m distributed_lion_pytorch_amd.launch "
+                         "or torchrun); with a rank-0-hosted store drop another rank")
     cfg = load_config(a.model)
     torch.manual_seed(0)
     with torch.device(dev):  # materialise on the device (8B: no 32 GB host copy per rank)
@@ -83,6 +104,7 @@ def main():
     if a.gradient_checkpointing:
         model.gradient_checkpointing_enable()
     broadcast_parameters(model)
+    el = ElasticGroup.get(a.elastic_timeout, grace_s=a.elastic_grace)
     opt = Lion([p for p in model.parameters() if p.requires_grad], lr=a.lr, weight_decay=a.weight_decay,
                exchange=a.exchange, elastic_timeout=a.elastic_timeout)
     step_fn = TrainStep(model, opt, grad_accum=a.grad_accum, max_grad_norm=1.0)
@@ -95,34 +117,33 @@ def main():
 
     log = []
     for s in range(a.steps):
-        if rank == a.drop_rank and s == a.drop_step:
-            print(json.dumps({"rank": rank, "event": "dying", "step": s}), flush=True)
-            os._exit(0)
         t0 = time.perf_counter()
         loss = step_fn(batches())
         if dev.type == "cuda":
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        w = opt.last_world
-        log.append({"step": s, "world": w, "loss": float(loss), "s": dt,
+        w = el.world
+        log.append({"step": s, "world": w, "loss": float(loss), "s": round(dt, 4),
                     "tokens_per_s": w * a.grad_accum * a.micro_batch * a.seq_len / dt})
-        if rank == 0:
+        if el.rank == 0:
             print(json.dumps({"progress": log[-1]}), file=sys.stderr, flush=True)
-    # survivors: compare replicas inside the shrunken group
+    # survivors: compare replicas over the (possibly regrouped) default group
     h = hashlib.sha256()
     for p in model.parameters():
         h.update(p.detach().float().cpu().numpy().tobytes())
     d = torch.tensor([int.from_bytes(h.digest()[:7], "little")], dtype=torch.int64, device=dev)
-    lo, hi = d.clone(), d.clone()
-    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=opt.process_group)
-    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=opt.process_group)
+    digests = el.all_gather(d).tolist()
     st = opt.stats()
-    if dist.get_rank(opt.process_group) == 0:
-        pre = [r["tokens_per_s"] for r in log if r["step"] < a.drop_step and r["step"] > 0]
-        post = [r["tokens_per_s"] for r in log if r["step"] > a.drop_step + 1]
+    if el.rank == 0:
+        ev = st.get("dropout_events") or []
+        first = ev[0]["step"] if ev else a.steps
+        pre = [r["tokens_per_s"] for r in log if 0 < r["step"] < first]
+        post = [r["tokens_per_s"] for r in log if r["step"] > first + 1]
         print(json.dumps({
-            "metric": "worker-dropout stress", "model": a.model, "world_start": world, "world_end": st["world"],
-            "dropout_events": st.get("dropout_events"), "replicas_identical": bool(int(lo) == int(hi)),
+            "metric": "worker-dropout stress", "model": a.model, "world_start": world, "world_end": el.world,
+            "fault": os.environ.get("DLION_FAULT"), "dropout_events": ev, "survivors": el.members,
+            "replicas_identical": len(set(digests)) == 1, "elastic_stall_s": st.get("elastic_stall_s"),
+            "elastic_commits": st.get("elastic_commits"),
             "tokens_per_s_before": sum(pre) / max(1, len(pre)), "tokens_per_s_after": sum(post) / max(1, len(post)),
             "final_loss": log[-1]["loss"], "steps": log}), flush=True)
     dist.destroy_process_group()

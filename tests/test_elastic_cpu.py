@@ -1,110 +1,133 @@
-"""Real worker dropout (gloo, CPU): a rank process exits mid-run, the survivors
-detect it at the next step's heartbeat, regroup and keep identical replicas."""
-import hashlib
-import os
+"""Real worker dropout at any instant (gloo, CPU).
 
+A rank process SIGKILLs itself at a chosen optimizer step and phase
+(DLION_FAULT=rank:step:phase, parallel/elastic.py): inside backward, after
+the vote all-to-all was issued but before it completed, inside the 1-bit
+all-gather, after the step was applied, or between steps.  The survivors must
+detect it within the bounded wait, agree on the outcome through the store,
+regroup into a new default group, re-vote the interrupted step among
+themselves and keep bit-identical replicas -- in the native loop
+(dropout_stress.py) and in the HF path (run_clm.py --lion_elastic_timeout).
+Runs go through the failure-tolerant launcher (distributed_lion_pytorch_amd.launch),
+whose store outlives any rank, rank 0 included."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
 import torch
 import torch.distributed as dist
 
 from distributed_lion_pytorch_amd import Lion
 from tests.dist_utils import run_world
 
-
-def _digest(t):
-    return hashlib.sha256(t.detach().float().numpy().tobytes()).hexdigest()
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _train(rank, world, exchange, drop_rank, drop_step, steps):
+def _launch(nproc, script_args, max_failures=1, env_extra=None, timeout=300):
+    cmd = [sys.executable, "-m", "distributed_lion_pytorch_amd.launch", "--nproc", str(nproc), "--max_failures",
+           str(max_failures)] + script_args
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.update(env_extra or {})
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+
+
+def _stress(nproc, fault_args, steps=5):
+    r = _launch(nproc, ["dropout_stress.py", "--model", "gpt2-tiny", "--device", "cpu", "--seq_len", "32",
+                        "--micro_batch", "2", "--steps", str(steps), "--elastic_timeout", "20"] + fault_args,
+                max_failures=2)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-2000:] + r.stderr[-3000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("phase,victim,nproc", [
+    ("backward", 1, 3),
+    ("after_launch", 2, 3),
+    ("in_allgather", 1, 4),
+    ("after_vote", 0, 3),  # rank 0 too: the store lives in the launcher
+    ("before_step", 3, 4),
+])
+def test_dropout_at_phase(phase, victim, nproc):
+    res = _stress(nproc, ["--drop_rank", str(victim), "--drop_step", "2", "--drop_phase", phase])
+    survivors = [r for r in range(nproc) if r != victim]
+    assert res["world_start"] == nproc and res["world_end"] == nproc - 1
+    assert res["survivors"] == survivors and res["replicas_identical"], res
+    ev = res["dropout_events"]
+    assert len(ev) == 1 and ev[0]["dropped"] == [victim] and ev[0]["survivors"] == survivors
+    # a death after the step-2 vote is applied is noticed in step 3's vote
+    assert ev[0]["step"] == (3 if phase == "after_vote" else 2)
+    assert [s["world"] for s in res["steps"]][-1] == nproc - 1 and len(res["steps"]) == 5
+    assert res["elastic_stall_s"] < 15.0  # bounded: well under the 20 s collective deadline
+
+
+def test_two_workers_drop_at_different_steps():
+    r = _launch(4, ["dropout_stress.py", "--model", "gpt2-tiny", "--device", "cpu", "--seq_len", "32",
+                    "--micro_batch", "2", "--steps", "6", "--elastic_timeout", "20", "--drop_rank", "-1"],
+                max_failures=2, env_extra={"DLION_FAULT": "1:2:after_launch,3:4:backward"})
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][0])
+    assert res["world_end"] == 2 and res["survivors"] == [0, 2] and res["replicas_identical"]
+    assert [e["dropped"] for e in res["dropout_events"]] == [[1], [3]]
+    assert [e["step"] for e in res["dropout_events"]] == [2, 4]
+
+
+def test_run_clm_survives_a_dropout(tmp_path):
+    """HF path: the AsyncTrainer guards HF's own collectives (num_items gather,
+    logging loss gather) and Lion's vote; a rank dying in backward leaves the
+    survivors training, checkpointing and evaluating on the regrouped group."""
+    out = str(tmp_path / "clm")
+    args = ["run_clm.py", "--synthetic_data", "--synthetic_samples", "96", "--block_size", "32",
+            "--per_device_train_batch_size", "2", "--gradient_accumulation_steps", "2", "--warmup_steps", "1",
+            "--learning_rate", "1e-3", "--report_to", "none", "--use_cpu", "--logging_steps", "1",
+            "--config_name", "gpt2-tiny", "--lion", "--async_grad", "--do_train", "--max_steps", "5",
+            "--output_dir", out, "--ddp_backend", "gloo", "--lion_elastic_timeout", "20", "--save_steps", "4"]
+    r = _launch(3, args, env_extra={"DLION_FAULT": "1:2:backward"})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-4000:]
+    recs = [json.loads(x) for x in open(os.path.join(out, "metrics.jsonl"))]
+    last = [x for x in recs if "replicas_identical" in x]
+    assert last and last[-1]["replicas_identical"] == 1.0 and last[-1]["world_end"] == 2.0
+    steps = [x["step"] for x in recs if "loss" in x]
+    assert max(steps) == 5
+    lion = [x["lion"] for x in recs if "lion" in x]
+    assert lion[-1]["world"] == 2 and lion[-1]["dropout_events"][0]["dropped"] == [1]
+    ck = os.path.join(out, "checkpoint-4")
+    files = set(os.listdir(ck))
+    # per-rank momentum files are named in the regrouped world (dense ranks 0, 1 of 2)
+    assert {"rank0-of-2-optimizer.pt", "rank1-of-2-optimizer.pt", "model.safetensors"} <= files
+    assert os.path.isfile(os.path.join(out, "model.safetensors"))
+
+
+# ------------------------------------------------------- no failure: transparent
+def _train(rank, world, exchange, steps):
     torch.manual_seed(0)
     model = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 4))
-    opt = Lion(model.parameters(), lr=1e-2, weight_decay=0.1, exchange=exchange, elastic_timeout=3.0,
+    opt = Lion(model.parameters(), lr=1e-2, weight_decay=0.1, exchange=exchange, elastic_timeout=10.0,
                backend="torch")
     gen = torch.Generator().manual_seed(100 + rank)
-    for step in range(steps):
-        if rank == drop_rank and step == drop_step:
-            # the worker dies: no goodbye, no collective, no process-group teardown
-            os._exit(0)
+    m2 = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 4))
+    m2.load_state_dict(model.state_dict())
+    ref = Lion(m2.parameters(), lr=1e-2, weight_decay=0.1, exchange=exchange, backend="torch")
+    for _ in range(steps):
         x = torch.randn(8, 16, generator=gen)
-        loss = model(x).pow(2).mean()
-        opt.zero_grad()
-        loss.backward()
-        opt.step()
+        for m, o in ((model, opt), (m2, ref)):
+            o.zero_grad()
+            m(x).pow(2).mean().backward()
+            o.step()
     st = opt.stats()
-    params = torch.cat([p.detach().flatten() for p in model.parameters()])
-    # survivors can still talk to each other in the shrunken group
+    same = all(torch.equal(a, b) for a, b in zip(model.parameters(), m2.parameters()))
     t = torch.tensor([float(rank)])
-    dist.all_reduce(t, group=opt.process_group)
-    return {"digest": _digest(params), "world": st["world"], "live": st.get("live_ranks"),
-            "events": st.get("dropout_events"), "sum": float(t)}
+    dist.all_reduce(t)
+    return {"same_as_plain": same, "events": st["dropout_events"], "world": st["world"], "commits": st["elastic_commits"],
+            "sum": float(t)}
 
 
-def _run(world, exchange, drop_rank, drop_step, steps=5):
-    import torch.multiprocessing as mp
-
-    from tests import dist_utils
-
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = dist_utils.free_port()
-    procs = [ctx.Process(target=dist_utils._entry,
-                         args=(r, world, port, _train, (exchange, drop_rank, drop_step, steps), q))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    out = {}
-    try:
-        for _ in range(world - 1):
-            r, status, res = q.get(timeout=180)
-            assert status == "ok", res
-            out[r] = res
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
-    return out
-
-
-def test_real_dropout_allgather():
-    out = _run(3, "allgather", drop_rank=2, drop_step=2)
-    assert sorted(out) == [0, 1]
-    assert out[0]["digest"] == out[1]["digest"]
-    assert out[0]["world"] == 2 and out[0]["live"] == [0, 1]
-    assert out[0]["events"] == [{"step": 2, "dropped": [2], "survivors": [0, 1]}]
-    assert out[0]["sum"] == 1.0
-
-
-def test_real_dropout_a2a_w4():
-    out = _run(4, "a2a", drop_rank=1, drop_step=3)
-    assert sorted(out) == [0, 2, 3]
-    assert len({o["digest"] for o in out.values()}) == 1
-    assert all(o["world"] == 3 and o["live"] == [0, 2, 3] for o in out.values())
-    assert out[2]["sum"] == 5.0
-
-
-def test_no_dropout_heartbeat_is_transparent():
-    res = run_world(_train, 2, "allgather", -1, -1, 4)
-    assert res[0]["digest"] == res[1]["digest"]
-    assert res[0]["events"] == [] and res[0]["world"] == 2
-
-
-def test_dropout_stress_entrypoint_torchrun():
-    """dropout_stress.py (BASELINE config #5 harness) under torchrun, 3 gloo ranks."""
-    import json
-    import subprocess
-    import sys
-
-    from tests.dist_utils import free_port
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "3",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(root, "dropout_stress.py"),
-           "--model", "gpt2-tiny", "--device", "cpu", "--seq_len", "32", "--micro_batch", "2", "--steps", "5",
-           "--drop_rank", "1", "--drop_step", "2", "--elastic_timeout", "5"]
-    env = dict(os.environ, OMP_NUM_THREADS="1")
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=root)
-    assert p.returncode == 0, p.stderr[-3000:]
-    line = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')][-1]
-    res = json.loads(line)
-    assert res["world_start"] == 3 and res["world_end"] == 2 and res["replicas_identical"]
-    assert res["dropout_events"] == [{"step": 2, "dropped": [1], "survivors": [0, 2]}]
+@pytest.mark.parametrize("exchange", ["a2a", "allgather"])
+def test_no_dropout_elastic_equals_plain(exchange):
+    res = run_world(_train, 3, exchange, 4)
+    for r in res:
+        assert r["same_as_plain"], "guarded vote must give the plain vote's result bit for bit"
+        assert r["events"] == [] and r["world"] == 3 and r["commits"] >= 4
+    assert res[0]["sum"] == 3.0

@@ -112,7 +112,7 @@ def test_lion_vote_step_over_rccl_hip_equals_torch(exchange):
             cfg = gpt2_config("gpt2-tiny")
             model = GPT2LMHeadModel(cfg).to(device=dev, dtype=torch.bfloat16)
             opt = Lion(model.parameters(), lr=1e-3, weight_decay=0.1, exchange="{exchange}", backend=backend,
-                       bucket_mb=0.05)
+                       bucket_mb=0.004)
             opt._force_vote = True
             g = torch.Generator(device=dev).manual_seed(3)
             for _ in range(3):
@@ -147,3 +147,46 @@ def test_subgroup_local_sync_then_destroy():
         out["default_ok"] = bool(t2.sum().item() == 2)
     """)
     assert out == {"sub_ok": True, "default_ok": True}
+
+
+def test_elastic_abort_and_reinit_under_rccl():
+    """The regroup path of parallel/elastic.py under RCCL: guarded collectives,
+    then ``_abort_process_group`` (ncclCommAbort of every communicator) and a
+    fresh default ``nccl`` group over the survivors' store prefix, then the
+    Lion vote (guarded, store-committed) on the new group."""
+    out = _run("""
+        os.environ["TORCH_NCCL_ASYNC_ERROR_HANDLING"] = "0"
+        from distributed_lion_pytorch_amd import Lion
+        from distributed_lion_pytorch_amd.models.gpt2 import GPT2LMHeadModel, gpt2_config
+        from distributed_lion_pytorch_amd.parallel.elastic import ElasticGroup
+        el = ElasticGroup.get(30.0, grace_s=0.5)
+        out["gather"] = el.all_gather(torch.arange(4, device=dev, dtype=torch.float32)).tolist()
+        torch.manual_seed(0)
+        cfg = gpt2_config("gpt2-tiny")
+        model = GPT2LMHeadModel(cfg).to(device=dev, dtype=torch.bfloat16)
+        opt = Lion(model.parameters(), lr=1e-3, weight_decay=0.1, elastic_timeout=30.0, bucket_mb=0.004)
+        opt._force_vote = True
+        ids = torch.randint(0, cfg.vocab_size, (2, 64), device=dev)
+        for i in range(3):
+            model(ids, labels=ids)["loss"].backward()
+            opt.step()
+            opt.zero_grad()
+            if i == 0:
+                old = dist.group.WORLD
+                el.regroup({"where": "test"})  # abort every communicator, re-init the default group
+                out["new_group"] = dist.group.WORLD is not old
+                out["after"] = [dist.get_world_size(), dist.get_rank(), dist.get_backend()]
+        x = torch.ones(3, device=dev)
+        el.all_reduce(x)
+        out["allreduce"] = x.tolist()
+        torch.cuda.synchronize()
+        out["finite"] = all(bool(torch.isfinite(p).all()) for p in model.parameters())
+        st = opt.stats()
+        out["events"] = len(st["dropout_events"])
+        out["commits"] = st["elastic_commits"] >= 3
+        out["executor"] = type(opt._executor).__name__
+    """)
+    assert out["gather"] == [0.0, 1.0, 2.0, 3.0]
+    assert out["new_group"] and out["after"] == [1, 0, "nccl"]
+    assert out["allreduce"] == [1.0, 1.0, 1.0] and out["finite"]
+    assert out["events"] == 1 and out["commits"] and out["executor"] == "HipExecutor"
