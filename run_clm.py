@@ -81,34 +81,70 @@ def _read_text(path: str, keep_linebreaks: bool):
     return [ln for ln in lines if ln.strip()]
 
 
+def split_train_validation(texts, pct: int):
+    """The reference's split when a corpus has no validation part
+    (/root/reference/run_clm.py:326-341, 364-380): ``validation = train[:pct%]``,
+    ``train = train[pct%:]`` -- disjoint, validation taken from the front (HF
+    percent slicing rounds the boundary to the closest row)."""
+    n_val = int(round(len(texts) * pct / 100.0))
+    return texts[n_val:], texts[:n_val]
+
+
+def _blocks(texts, tokenizer, block_size):
+    return BlockDataset([tokenizer(t)["input_ids"] for t in texts], block_size, eos=tokenizer.eos_token_id)
+
+
+def _cap(ds, n: Optional[int]):
+    """``max_train_samples`` / ``max_eval_samples``: the first n blocks
+    (reference run_clm.py:550-560 ``select(range(n))``)."""
+    if n is None or ds is None or len(ds) <= n:
+        return ds
+    return torch.utils.data.Subset(ds, range(n))
+
+
 def build_datasets(data_args, train_args, tokenizer, vocab_size, block_size):
+    pct = data_args.validation_split_percentage if data_args.validation_split_percentage is not None else 5
     if data_args.dataset_name and not train_args.synthetic_data:
         try:
             import datasets
 
-            raw = datasets.load_dataset(data_args.dataset_name, data_args.dataset_config_name)
+            if os.path.isdir(data_args.dataset_name):
+                raw = datasets.load_from_disk(data_args.dataset_name)
+            else:
+                raw = datasets.load_dataset(data_args.dataset_name, data_args.dataset_config_name)
             col = "text" if "text" in raw["train"].column_names else raw["train"].column_names[0]
-            toks = [tokenizer(t)["input_ids"] for t in raw["train"][col]]
-            train = BlockDataset(toks, block_size, eos=tokenizer.eos_token_id)
-            n_val = max(1, len(train) * (data_args.validation_split_percentage or 5) // 100)
-            return train, torch.utils.data.Subset(train, range(n_val))
+            if "validation" in raw:  # the dataset's own validation split
+                tr, va = list(raw["train"][col]), list(raw["validation"][col])
+            else:
+                tr, va = split_train_validation(list(raw["train"][col]), pct)
+            return (_cap(_blocks(tr, tokenizer, block_size), data_args.max_train_samples),
+                    _cap(_blocks(va, tokenizer, block_size), data_args.max_eval_samples))
         except Exception as e:  # offline: no hub datasets
             logger.warning("dataset %s unavailable offline (%s); falling back to synthetic data",
                            data_args.dataset_name, e)
     if data_args.train_file and not train_args.synthetic_data:
-        toks = [tokenizer(t)["input_ids"] for t in _read_text(data_args.train_file, data_args.keep_linebreaks)]
-        train = BlockDataset(toks, block_size, eos=tokenizer.eos_token_id)
+        tr = _read_text(data_args.train_file, data_args.keep_linebreaks)
         if data_args.validation_file:
-            vt = [tokenizer(t)["input_ids"] for t in _read_text(data_args.validation_file, data_args.keep_linebreaks)]
-            val = BlockDataset(vt, block_size, eos=tokenizer.eos_token_id)
+            va = _read_text(data_args.validation_file, data_args.keep_linebreaks)
         else:
-            n_val = max(1, len(train) * (data_args.validation_split_percentage or 5) // 100)
-            val = torch.utils.data.Subset(train, range(n_val))
-        return train, val
+            tr, va = split_train_validation(tr, pct)
+        return (_cap(_blocks(tr, tokenizer, block_size), data_args.max_train_samples),
+                _cap(_blocks(va, tokenizer, block_size), data_args.max_eval_samples))
     n_train = data_args.max_train_samples or data_args.synthetic_samples
     n_eval = data_args.max_eval_samples or max(8, n_train // 20)
+    # disjoint by construction: the eval set is drawn from a different seed
     return (SyntheticCLMDataset(n_train, block_size, vocab_size, seed=train_args.seed),
             SyntheticCLMDataset(n_eval, block_size, vocab_size, seed=train_args.seed + 1))
+
+
+def resize_embeddings_for(model, tokenizer) -> bool:
+    """Grow the embedding (and tied LM head) when the tokenizer has more ids
+    than the model (/root/reference/run_clm.py:446-450).  Returns True if resized."""
+    emb = model.get_input_embeddings().weight.shape[0]
+    if len(tokenizer) > emb:
+        model.resize_token_embeddings(len(tokenizer))
+        return True
+    return False
 
 
 def main(argv=None):
@@ -117,6 +153,12 @@ def main(argv=None):
         model_args, data_args, training_args = parser.parse_json_file(json_file=os.path.abspath(sys.argv[1]))
     else:
         model_args, data_args, training_args = parser.parse_args_into_dataclasses(args=argv)
+
+    if data_args.streaming:
+        # the reference streams hub datasets (run_clm.py:323); there is no hub here and the
+        # local paths are map-style -- refuse instead of silently loading everything
+        raise ValueError("--streaming is not supported: datasets are read from local files / synthetic data "
+                         "(no network); drop the flag")
 
     logging.basicConfig(format="%(asctime)s - %(levelname)s - %(name)s - %(message)s", datefmt="%m/%d/%Y %H:%M:%S",
                         handlers=[logging.StreamHandler(sys.stdout)])
@@ -139,12 +181,14 @@ def main(argv=None):
     tokenizer = load_tokenizer(model_args.tokenizer_name or model_args.model_name_or_path)
     model = build_model(config, model_name_or_path=model_args.model_name_or_path, native=model_args.native_model,
                         torch_dtype=model_args.torch_dtype)
+    if resize_embeddings_for(model, tokenizer):
+        logger.warning(f"resized the token embeddings to the tokenizer's {len(tokenizer)} ids")
     n_params = sum({p.data_ptr(): p.numel() for p in model.parameters()}.values())
     logger.info(f"model {config.model_type}: {n_params / 2 ** 20:.2f}M params")
 
     max_pos = getattr(config, "n_positions", None) or getattr(config, "max_position_embeddings", 1024)
     block_size = min(data_args.block_size or 1024, max_pos)
-    train_ds, eval_ds = build_datasets(data_args, training_args, tokenizer, config.vocab_size, block_size)
+    train_ds, eval_ds = build_datasets(data_args, training_args, tokenizer, model.config.vocab_size, block_size)
 
     def preprocess_logits_for_metrics(logits, labels):
         if isinstance(logits, tuple):
@@ -207,6 +251,18 @@ def main(argv=None):
             metrics["perplexity"] = float("inf")
         trainer.log_metrics("eval", metrics)
         trainer.save_metrics("eval", metrics)
+
+    # model card (reference run_clm.py:641-653); offline, so nothing is pushed
+    kwargs = {"finetuned_from": model_args.model_name_or_path, "tasks": "text-generation"}
+    if data_args.dataset_name:
+        kwargs["dataset_tags"] = data_args.dataset_name
+        kwargs["dataset"] = data_args.dataset_name if not data_args.dataset_config_name else \
+            f"{data_args.dataset_name} {data_args.dataset_config_name}"
+    if training_args.do_train and trainer.is_world_process_zero():
+        try:
+            trainer.create_model_card(**kwargs)
+        except Exception as e:  # noqa: BLE001 - the card is documentation, never fail a run on it
+            logger.warning("model card not written: %s", e)
     return trainer
 
 
