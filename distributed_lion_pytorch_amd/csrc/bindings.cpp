@@ -954,6 +954,8 @@ std::tuple<Tensor, Tensor> quant4(const Tensor& w, const Tensor& code) {
   TORCH_CHECK(code.scalar_type() == at::kFloat && code.numel() == 16, "dlion quant4: code must be float32[16]");
   const int64_t n = w.numel();
   TORCH_CHECK(n % 64 == 0, "dlion quant4: numel must be a multiple of 64, got ", n);
+  TORCH_CHECK(w.is_contiguous() && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "dlion quant4: w must be contiguous and 16-byte aligned (the kernel reads it as flat vectors)");
   const c10::DeviceGuard g(w.device());
   auto q = at::empty({n / 2}, w.options().dtype(at::kByte));
   auto absmax = at::empty({n / 64}, w.options().dtype(at::kFloat));
@@ -977,6 +979,8 @@ void dequant4_(const Tensor& q, const Tensor& absmax, const Tensor& code, const 
               "dlion dequant4: out numel ", n, " does not match q ", q.numel(), " / absmax ", absmax.numel());
   TORCH_CHECK(reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
               "dlion dequant4: q and out must be 16-byte aligned");
+  TORCH_CHECK(out.is_contiguous() && q.is_contiguous() && absmax.is_contiguous(),
+              "dlion dequant4: q, absmax and out must be contiguous (out is written linearly)");
   const c10::DeviceGuard g(out.device());
   check_hip(dlion::launch_dequant4(dtype_code(out.scalar_type()), q.data_ptr<uint8_t>(), absmax.data_ptr<float>(),
                                    code.data_ptr<float>(), out.data_ptr(), n, cur_stream()),

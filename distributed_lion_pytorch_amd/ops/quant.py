@@ -82,6 +82,8 @@ def dequantize_4bit(q: torch.Tensor, absmax: torch.Tensor, code: torch.Tensor, s
     """The compute-dtype weight of ``shape``; written into ``out`` (a
     contiguous tensor, e.g. a row block of a concatenated weight) if given."""
     n = 2 * q.numel()
+    if out is not None and not out.is_contiguous():
+        raise ValueError("dequantize_4bit: out must be contiguous (it is written linearly)")
     if q.is_cuda:
         if out is None:
             out = torch.empty(shape, dtype=dtype, device=q.device)

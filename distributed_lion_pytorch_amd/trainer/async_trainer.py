@@ -252,7 +252,8 @@ class AsyncMixin:
         # blocking .to(device) -- a stream synchronise at every optimizer step.
         # Same count, pinned + non-blocking copy; the cross-rank sum (HF's
         # average_tokens_across_devices) stays a device collective.
-        if getattr(device, "type", None) != "cuda":
+        if getattr(device, "type", None) != "cuda" or self.args.n_gpu > 1:
+            # (n_gpu > 1: single-process DataParallel -- HF's own branch order and normaliser)
             return super()._get_num_items_in_batch(batch_samples, device)
         avg = self.args.average_tokens_across_devices and self.args.world_size > 1
         prev = self.args.average_tokens_across_devices

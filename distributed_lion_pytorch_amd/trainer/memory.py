@@ -49,10 +49,24 @@ def model_bytes(*models) -> int:
     return n
 
 
+def engine_reserve_bytes() -> int:
+    """Device memory the gradient-accumulation fusion window may hold on top
+    of weights and activations when activations are kept (ops/linear.py): the
+    deferred weight-gradient operands (``DLION_WGRAD_DEFER_GB``, default a
+    quarter of HBM) and the fp32 split-K accumulators (8 GB budget)."""
+    from ..ops import linear
+
+    n = linear._ACC_BUDGET
+    if linear._WDEFER_ON:
+        n += linear._wdefer_budget()
+    return n
+
+
 def should_checkpoint(requested: bool, policy: str, config, tokens_per_micro_batch: int, *models,
                       device=None) -> bool:
     """``policy``: ``"reference"`` honours ``requested`` as given; ``"auto"``
-    checkpoints only if ``requested`` and the estimate does not fit in
+    checkpoints only if ``requested`` and the estimate -- weights, gradients,
+    momentum, activations and the fusion window's reserve -- does not fit in
     HEADROOM of the device memory (no GPU: as requested)."""
     if not requested or policy == "reference":
         return bool(requested)
@@ -62,5 +76,5 @@ def should_checkpoint(requested: bool, policy: str, config, tokens_per_micro_bat
         return True
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     total = torch.cuda.get_device_properties(dev).total_memory
-    need = model_bytes(*models) + activation_bytes(config, tokens_per_micro_batch)
+    need = model_bytes(*models) + activation_bytes(config, tokens_per_micro_batch) + engine_reserve_bytes()
     return need > HEADROOM * total

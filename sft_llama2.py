@@ -33,7 +33,7 @@ from transformers import HfArgumentParser, TrainingArguments
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from distributed_lion_pytorch_amd.models.lora import (LoraConfig, merge_and_unload,  # noqa: E402
+from distributed_lion_pytorch_amd.models.lora import (LoraConfig, load_adapter, merge_and_unload,  # noqa: E402
                                                       print_trainable_parameters, save_adapter)
 from distributed_lion_pytorch_amd.models.registry import build_model, load_config  # noqa: E402
 from distributed_lion_pytorch_amd.trainer.async_trainer import build_lion, warn_unsynced  # noqa: E402
@@ -73,6 +73,16 @@ class ScriptArguments:
     bnb_4bit_quant_type: Optional[str] = field(default="nf4", metadata={"help": "nf4 | fp4"})
 
 
+def build_base(script_args, seed):
+    """The compute-dtype base model: loaded from ``model_name`` when it is a
+    local checkpoint, else randomly initialised from the seed -- so calling it
+    again with the same seed rebuilds exactly the same weights (the 4-bit
+    merge below relies on that)."""
+    transformers.set_seed(seed)
+    config = load_config(script_args.model_name, overrides=script_args.model_overrides)
+    return build_model(config, model_name_or_path=script_args.model_name, torch_dtype=script_args.torch_dtype)
+
+
 def load_samples(script_args, seed):
     path = script_args.dataset_name
     if path and os.path.isfile(path):
@@ -107,8 +117,7 @@ def main(argv=None):
     transformers.set_seed(training_args.seed)
 
     tokenizer = load_tokenizer(script_args.model_name)
-    config = load_config(script_args.model_name, overrides=script_args.model_overrides)
-    model = build_model(config, model_name_or_path=script_args.model_name, torch_dtype=script_args.torch_dtype)
+    model = build_base(script_args, training_args.seed)
     if script_args.load_in_4bit:
         from distributed_lion_pytorch_amd.models.quant import QuantConfig, quantize_model
 
@@ -148,11 +157,13 @@ def main(argv=None):
         out = os.path.join(training_args.output_dir, "final_checkpoint")
         if script_args.use_lora:
             save_adapter(trainer.model, out)
-            from distributed_lion_pytorch_amd.models.quant import dequantize_model
-
-            # like the reference (sft_llama2.py:195-199: base reloaded in bf16, adapters merged), the
-            # merged checkpoint is a plain compute-dtype model even when training ran on a 4-bit base
-            merged = merge_and_unload(dequantize_model(trainer.accelerator.unwrap_model(trainer.model)))
+            if script_args.load_in_4bit:
+                # like the reference (sft_llama2.py:195-196: AutoPeftModelForCausalLM reloads the base in
+                # the compute dtype), the adapters are merged into the ORIGINAL weights, not into
+                # dequant(quant(W)): the merged model carries no 4-bit rounding error
+                merged = merge_and_unload(load_adapter(build_base(script_args, training_args.seed), out))
+            else:
+                merged = merge_and_unload(trainer.accelerator.unwrap_model(trainer.model))
             merged.save_pretrained(os.path.join(training_args.output_dir, "final_merged_checkpoint"),
                                    safe_serialization=True)
         else:

@@ -80,3 +80,32 @@ def test_gpt2_fused_embedding_and_lm_head_grads_match_autograd(cuda):
     for n in grads[False]:
         a, b = grads[True][n], grads[False][n]
         assert (a - b).abs().max().item() < 2e-2 * b.abs().max().item() + 1e-6, n
+
+
+def test_out_of_range_ids_and_labels_are_errors(cuda):
+    """ATen's embedding / cross-entropy raise on an id >= V; the fused kernels
+    flag it on the device (no clamp-and-continue) and check_index_errors()
+    raises -- a step late in the non-blocking per-step form, at once blocking."""
+    hip.require()
+    V, C, P = 1000, 128, 256
+    wte = torch.randn(V, C, device=cuda, dtype=torch.bfloat16)
+    wpe = torch.randn(P, C, device=cuda, dtype=torch.bfloat16)
+    ok = torch.randint(0, V, (2, 64), device=cuda)
+    fused.embed(ok, wte, wpe, 0.0)
+    fused.check_index_errors(blocking=True)  # clean
+    bad = ok.clone()
+    bad[1, 7] = V  # one id past the table
+    fused.embed(bad, wte, wpe, 0.0)
+    fused.check_index_errors()  # starts the async copy of the flag
+    torch.cuda.synchronize()
+    with pytest.raises(ValueError, match="embedding table"):
+        fused.check_index_errors()  # the landed copy shows the error
+    fused.check_index_errors(blocking=True)  # the flag was reset
+    labels = torch.randint(0, V, (128,), device=cuda)
+    labels[3] = -100  # the ignore index is fine
+    fused.check_labels(labels, V)
+    fused.check_index_errors(blocking=True)
+    labels[5] = V + 3
+    fused.check_labels(labels, V)
+    with pytest.raises(ValueError, match="label"):
+        fused.check_index_errors(blocking=True)

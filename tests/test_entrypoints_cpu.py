@@ -103,3 +103,34 @@ def test_sft_and_dpo_entrypoints(tmp_path):
                           "--warmup_steps", "1", "--logging_steps", "1"])
     assert tr.state.global_step == 2
     assert os.path.isfile(os.path.join(dpo_out, "final_checkpoint", "adapter_config.json"))
+
+
+def test_sft_4bit_merge_uses_original_weights(tmp_path):
+    """--load_in_4bit: the merged checkpoint is W + B@A*scaling on the ORIGINAL
+    compute-dtype base (reference sft_llama2.py:195-196 reloads it), not
+    dequant(quant(W)) + delta."""
+    from safetensors.torch import load_file
+
+    import sft_llama2
+    from distributed_lion_pytorch_amd.models.quant import QuantConfig, quantize_model
+
+    out = str(tmp_path / "qsft")
+    args = ["--model_name", "llama-tiny", "--synthetic_samples", "60", "--seq_length", "64", "--output_dir", out,
+            "--max_steps", "2", "--per_device_train_batch_size", "2", "--learning_rate", "1e-2", "--lion",
+            "--async_grad", "--report_to", "none", "--use_cpu", "--torch_dtype", "float32", "--load_in_4bit"]
+    sft_llama2.main(args)
+    merged = load_file(os.path.join(out, "final_merged_checkpoint", "model.safetensors"))
+    adapter = load_file(os.path.join(out, "final_checkpoint", "adapter_model.safetensors"))
+    sa = sft_llama2.HfArgumentParser((sft_llama2.ScriptArguments, sft_llama2.TrainingArguments)) \
+        .parse_args_into_dataclasses(args=args)[0]
+    base = sft_llama2.build_base(sa, 42).state_dict()  # HF TrainingArguments default seed
+    key = "model.layers.0.self_attn.q_proj.weight"
+    a = adapter["base_model.model.model.layers.0.self_attn.q_proj.lora_A.weight"]
+    b = adapter["base_model.model.model.layers.0.self_attn.q_proj.lora_B.weight"]
+    assert b.abs().max() > 0, "the adapter must have trained"
+    expect = base[key] + (b @ a) * (16 / 8)
+    assert torch.allclose(merged[key], expect, atol=1e-6, rtol=0)
+    # and it is NOT the 4-bit-rounded base
+    q = quantize_model(sft_llama2.build_base(sa, 42), QuantConfig(bnb_4bit_compute_dtype=torch.float32))
+    deq = q.model.layers[0].self_attn.q_proj.dequantize(torch.float32)
+    assert not torch.allclose(merged[key], deq + (b @ a) * 2.0, atol=1e-4)

@@ -26,3 +26,19 @@ def test_policy(monkeypatch):
     assert memory.should_checkpoint(True, "auto", cfg, tokens, m) is False
     _fake_device(monkeypatch, 40 << 30)
     assert memory.should_checkpoint(True, "auto", cfg, tokens, m) is True
+
+
+def test_policy_counts_the_fusion_window_reserve(monkeypatch):
+    """Keeping activations turns on deferred weight gradients: their operand
+    budget (a quarter of HBM by default) and the 8 GB split-K accumulators are
+    part of the fit check (they were invisible to it)."""
+    cfg = load_config("llama-2-7b")
+    tokens = 2 * 4 * 1024
+    m = torch.nn.Linear(8, 8)
+    _fake_device(monkeypatch, 288 << 30)
+    assert memory.engine_reserve_bytes() == (8 << 30) + (72 << 30)
+    # 96 GB: activations alone (~30 GB) fit 0.6 x 96 = 58 GB, with the 8 + 24 GB reserve they do not
+    _fake_device(monkeypatch, 96 << 30)
+    assert memory.should_checkpoint(True, "auto", cfg, tokens, m) is True
+    monkeypatch.setenv("DLION_WGRAD_DEFER_GB", "1")
+    assert memory.should_checkpoint(True, "auto", cfg, tokens, m) is False
