@@ -102,6 +102,10 @@ def parse():
     ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"],
                     help="auto: cuda when a GPU is visible (cpu + gloo: plumbing rehearsal of the multi-rank path)")
     ap.add_argument("--no_phase_times", action="store_true", help="do not record per-phase HIP events")
+    ap.add_argument("--data", default="random", choices=["random", "markov"],
+                    help="random token ids (throughput) | a learnable Markov-chain corpus (learning curves)")
+    ap.add_argument("--loss_log", default=None,
+                    help="learning-curve mode: run --steps steps untimed, rank 0 writes one JSON line per step here")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend; gloo (with ranks sharing GPUs) only to rehearse the multi-rank "
                          "path on a 1-GPU box -- RCCL refuses two ranks on one device")
@@ -250,8 +254,18 @@ def build_reference(args, dev):
     from distributed_lion_pytorch_amd.ops import reference as ref
 
     cfg = gpt2_config(args.model)
+    if args.dropout is not None:
+        cfg.resid_pdrop = cfg.embd_pdrop = cfg.attn_pdrop = args.dropout
+    # the same initial weights as the native run (same seed, same builder; HF checkpoint layout)
+    from distributed_lion_pytorch_amd.models.registry import build_model
+
     torch.manual_seed(0)
+    with torch.device(dev):
+        init = build_model(cfg, native=True).to(dtype=torch.bfloat16).state_dict()
     model = transformers.GPT2LMHeadModel(cfg).to(device=dev, dtype=torch.bfloat16)
+    missing = model.load_state_dict(init, strict=False)
+    assert not [k for k in missing.missing_keys if "attn.bias" not in k and "masked_bias" not in k], missing
+    del init
     broadcast_parameters(model)
 
     class RefLion(torch.optim.Optimizer):
@@ -318,15 +332,50 @@ def main():
 
     seqs_per_mb = args.micro_batch * (2 if args.task == "dpo" else 1)  # DPO: chosen + rejected
 
+    if args.data == "markov":
+        # learnable synthetic corpus (the loss can fall well below ln V): every
+        # token is followed by succ[token] with probability 0.75, else by a
+        # uniformly random token; the table is the same on every rank
+        mk = torch.Generator(device=dev).manual_seed(99)
+        succ = torch.randperm(cfg.vocab_size, device=dev, generator=mk)
+
+    def sample_ids():
+        if args.data != "markov":
+            return torch.randint(0, cfg.vocab_size, (seqs_per_mb, args.seq_len), device=dev, generator=gen)
+        rnd = torch.randint(0, cfg.vocab_size, (seqs_per_mb, args.seq_len), device=dev, generator=gen)
+        follow = torch.rand(seqs_per_mb, args.seq_len, device=dev, generator=gen) < 0.75
+        out = rnd.clone()
+        for t in range(1, args.seq_len):
+            out[:, t] = torch.where(follow[:, t], succ[out[:, t - 1]], rnd[:, t])
+        return out
+
     def batches():
         for _ in range(args.grad_accum):
-            ids = torch.randint(0, cfg.vocab_size, (seqs_per_mb, args.seq_len), device=dev, generator=gen)
+            ids = sample_ids()
             labels = ids
             if args.task == "dpo":  # prompt half masked out of the log-likelihood, as the DPO collator does
                 labels = ids.clone()
                 labels[:, : args.seq_len // 2] = -100
             yield {"input_ids": ids, "labels": labels}
 
+    loss_log = open(args.loss_log, "w") if args.loss_log and rank == 0 else None
+    if loss_log is not None:  # learning-curve mode: data is generated before timing
+        for i in range(args.steps):
+            data = list(batches())
+            loss = step(iter(data))
+            loss_log.write(json.dumps({"step": i, "loss": float(loss), "world": world, "impl": args.impl}) + "\n")
+            loss_log.flush()
+        loss_log.close()
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    if args.loss_log:  # other ranks in learning-curve mode: same steps, no log
+        for _ in range(args.steps):
+            step(iter(list(batches())))
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     for _ in range(args.warmup):
         step(batches())
     if hasattr(opt, "stats"):

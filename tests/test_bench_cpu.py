@@ -57,3 +57,20 @@ def test_too_few_gpus_is_an_error():
     r = _run(["--gpus", "2", "--device", "cuda"] + TINY)
     assert r.returncode != 0
     assert "GPU(s) visible" in r.stderr
+
+
+def test_learning_curves_native_vs_reference_track(tmp_path):
+    """bench.py learning-curve mode on the learnable Markov corpus: the native
+    engine and the reference algorithm (HF model + per-tensor int64 all_gather
+    Lion) start from the same weights and their losses track step by step."""
+    curves = {}
+    for impl in ("native", "reference"):
+        log = str(tmp_path / f"{impl}.jsonl")
+        r = _run(["--device", "cpu", "--model", "gpt2-tiny", "--micro_batch", "4", "--grad_accum", "2", "--seq_len",
+                  "64", "--steps", "20", "--data", "markov", "--loss_log", log, "--lr", "1e-3", "--impl", impl])
+        assert r.returncode == 0, r.stderr[-3000:]
+        curves[impl] = [json.loads(x)["loss"] for x in open(log)]
+    a, b = curves["native"], curves["reference"]
+    assert len(a) == len(b) == 20
+    assert a[-1] < a[0] - 0.5  # it learns
+    assert max(abs(x - y) for x, y in zip(a, b)) < 0.05
