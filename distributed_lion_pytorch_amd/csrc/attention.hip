@@ -187,19 +187,36 @@ struct DmaTile {
   static constexpr int CPR = D / 8, PPW = D / 64;  // 16-byte chunks per row, 1 KiB pieces per wave
   static_assert(D == 64 || D == 128, "head dim");
   int off0, off1, lds;  // source element offsets (tile-relative) of the lane's chunks; wave's LDS byte offset
+  int r0, r1, c0, c1, st;  // the lane's tile rows / swizzled chunk offsets, for partial (tail) tiles
   __device__ __forceinline__ DmaTile(int64_t stride) {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int p0 = 64 * PPW * w + lane, p1 = p0 + 64;
-    off0 = static_cast<int>((p0 / CPR) * stride) + 8 * swz_chunk<D>(p0 / CPR, p0 % CPR);
-    off1 = static_cast<int>((p1 / CPR) * stride) + 8 * swz_chunk<D>(p1 / CPR, p1 % CPR);
+    r0 = p0 / CPR;
+    r1 = p1 / CPR;
+    c0 = 8 * swz_chunk<D>(r0, p0 % CPR);
+    c1 = 8 * swz_chunk<D>(r1, p1 % CPR);
+    st = static_cast<int>(stride);
+    off0 = r0 * st + c0;
+    off1 = r1 * st + c1;
     lds = 1024 * PPW * w;
   }
-  __device__ __forceinline__ void issue(const __bf16* tile, LdsTile<D>& t) const {
+  // `valid` = rows of the sequence left from this tile's first row: a tail
+  // tile (valid < 32) re-reads row valid-1 for its missing rows -- memory
+  // that exists; those rows are masked or dropped by every consumer
+  __device__ __forceinline__ void issue(const __bf16* tile, LdsTile<D>& t, int valid = 32) const {
     char* dst = reinterpret_cast<char*>(&t[0]) + lds;
-    glds16(tile + off0, dst);
-    if constexpr (PPW == 2) glds16(tile + off1, dst + 1024);
+    if (valid >= 32) {  // block-uniform
+      glds16(tile + off0, dst);
+      if constexpr (PPW == 2) glds16(tile + off1, dst + 1024);
+    } else {
+      glds16(tile + min(r0, valid - 1) * st + c0, dst);
+      if constexpr (PPW == 2) glds16(tile + min(r1, valid - 1) * st + c1, dst + 1024);
+    }
   }
 };
+
+// 32-row tiles covering T (the last one may be partial)
+__device__ __forceinline__ int ntiles32(int T) { return (T + 31) >> 5; }
 
 // query-side blocks (fwd, dQ): heads fastest, heavy (late) query groups first
 struct QBlock {
@@ -225,14 +242,17 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[2][NT];
   __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[2][NT];
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
-  const QBlock blk(a.B * a.H, a.T >> 5);
+  const QBlock blk(a.B * a.H, ntiles32(a.T));
   const int bh = blk.bh, qtile = blk.qtile, last = blk.last;
   const int b = bh / a.H, h = bh % a.H, hk = h / (a.H / a.Hkv);
   const int q = qtile * 32 + r;
+  // rows past T (tail tile): computed on a copy of row T-1, never stored; keys
+  // past T are behind every valid query, so the causal mask already drops them
+  const int qc = min(q, a.T - 1);
 
   bf16x8 qf[D / 16];
   if (blk.active) {
-    const __bf16* qp = a.q + b * a.q_sb + static_cast<int64_t>(q) * a.q_st + h * a.q_sh + 8 * hf;
+    const __bf16* qp = a.q + b * a.q_sb + static_cast<int64_t>(qc) * a.q_st + h * a.q_sh + 8 * hf;
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) qf[s] = ld8(qp + 16 * s);
   }
@@ -251,9 +271,9 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   auto stage = [&](int first, int buf) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      const int64_t row = static_cast<int64_t>(min(first + j, last) * 32);
-      kd.issue(kg + row * a.k_st, ks_[buf][j]);
-      vd.issue(vg + row * a.v_st, vs_[buf][j]);
+      const int row = min(first + j, last) * 32;
+      kd.issue(kg + static_cast<int64_t>(row) * a.k_st, ks_[buf][j], a.T - row);
+      vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[buf][j], a.T - row);
     }
   };
   stage(0, 0);
@@ -332,7 +352,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     vm_wait0();  // this wave's pieces of the next tiles have landed
     __syncthreads();
   }
-  if (!blk.active) return;
+  if (!blk.active || q >= a.T) return;
   const float inv_l = (DROP ? a.inv_keep : 1.f) / l;
   __bf16* op = a.out + b * a.o_sb + static_cast<int64_t>(q) * a.o_st + h * a.o_sh;
 #pragma unroll
@@ -357,27 +377,29 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[2];
   __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[2];
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
-  const QBlock blk(a.B * a.H, a.T >> 5);
+  const int nt = ntiles32(a.T);
+  const QBlock blk(a.B * a.H, nt);
   const int bh = blk.bh, qtile = blk.qtile, last = blk.last;
   const int b = bh / a.H, h = bh % a.H, hk = h / (a.H / a.Hkv);
   const int q = qtile * 32 + r;
+  const int qc = min(q, a.T - 1);  // tail rows: a copy of row T-1, never stored (see the forward)
 
   bf16x8 qf[D / 16], dof[D / 16];
   float lse2 = 0.f, dlt = 0.f;
   if (blk.active) {
-    const __bf16* qp = a.q + b * a.q_sb + static_cast<int64_t>(q) * a.q_st + h * a.q_sh + 8 * hf;
-    const __bf16* dop = a.dout + b * a.o_sb + static_cast<int64_t>(q) * a.o_st + h * a.o_sh + 8 * hf;
+    const __bf16* qp = a.q + b * a.q_sb + static_cast<int64_t>(qc) * a.q_st + h * a.q_sh + 8 * hf;
+    const __bf16* dop = a.dout + b * a.o_sb + static_cast<int64_t>(qc) * a.o_st + h * a.o_sh + 8 * hf;
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
       qf[s] = ld8(qp + 16 * s);
       dof[s] = ld8(dop + 16 * s);
     }
-    lse2 = a.lse[static_cast<int64_t>(bh) * a.T + q];
+    lse2 = a.lse[static_cast<int64_t>(bh) * a.T + qc];
     // delta = rowsum(dO * O) for this wave's 32 rows, computed here (the dQ
     // kernel already holds the dO rows) and published for the dKV kernel that
     // runs next -- instead of a separate pass over O and dO.  Lanes r and r+32
     // hold the two halves of row q.
-    const __bf16* op = a.o + b * a.o_sb + static_cast<int64_t>(q) * a.o_st + h * a.o_sh + 8 * hf;
+    const __bf16* op = a.o + b * a.o_sb + static_cast<int64_t>(qc) * a.o_st + h * a.o_sh + 8 * hf;
     float part = 0.f;
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
@@ -387,7 +409,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
     }
     dlt = xsum32(part);
     if (a.thresh16) dlt /= a.inv_keep;  // delta * (1-p), see the forward's lse note
-    if (hf == 0) const_cast<float*>(a.delta)[static_cast<int64_t>(bh) * a.T + q] = dlt;
+    if (hf == 0 && q < a.T) const_cast<float*>(a.delta)[static_cast<int64_t>(bh) * a.T + q] = dlt;
   }
   const uint32_t thr_hi = a.thresh16 << 16;
   const uint32_t arow = drop_row(a.seed, bh, q);
@@ -397,16 +419,16 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
   const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
   const DmaTile<D> kd(a.k_st), vd(a.v_st);
-  kd.issue(kg, ks_[0]);
-  vd.issue(vg, vs_[0]);
+  kd.issue(kg, ks_[0], a.T);
+  vd.issue(vg, vs_[0], a.T);
   vm_wait0();
   __syncthreads();
   for (int kt = 0; kt <= last; ++kt) {
     const int buf = kt & 1;
     if (kt < last) {  // next tile into the other buffer (last read before the previous barrier)
-      const int64_t nxt = static_cast<int64_t>((kt + 1) * 32);
-      kd.issue(kg + nxt * a.k_st, ks_[buf ^ 1]);
-      vd.issue(vg + nxt * a.v_st, vs_[buf ^ 1]);
+      const int nxt = (kt + 1) * 32;
+      kd.issue(kg + static_cast<int64_t>(nxt) * a.k_st, ks_[buf ^ 1], a.T - nxt);
+      vd.issue(vg + static_cast<int64_t>(nxt) * a.v_st, vs_[buf ^ 1], a.T - nxt);
     }
     if (blk.active && kt <= qtile) {
       const int kb = kt * 32;
@@ -453,17 +475,18 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int qq = qtile * 32 + acc_row(reg, hf);
-      base[static_cast<int64_t>(qq) * a.dq_st + 32 * t + r] = static_cast<__bf16>(dq[t][reg] * a.scale);
+      if (qq < a.T) base[static_cast<int64_t>(qq) * a.dq_st + 32 * t + r] = static_cast<__bf16>(dq[t][reg] * a.scale);
     }
   if (a.colsum != nullptr) {
     // the c_attn bias gradient's partials: column sums of the stored (bf16) dq
-    // over this wave's 32 rows; lanes r and r+32 hold the two row halves
-    float* cs = a.colsum + static_cast<int64_t>(b * (a.T >> 5) + qtile) * (3 * a.H * D) + h * D;
+    // over this wave's 32 rows (valid ones); lanes r and r+32 hold the two row halves
+    float* cs = a.colsum + static_cast<int64_t>(b * nt + qtile) * (3 * a.H * D) + h * D;
 #pragma unroll
     for (int t = 0; t < D / 32; ++t) {
       float sum = 0.f;
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) sum += static_cast<float>(static_cast<__bf16>(dq[t][reg] * a.scale));
+      for (int reg = 0; reg < 16; ++reg)
+        if (qtile * 32 + acc_row(reg, hf) < a.T) sum += static_cast<float>(static_cast<__bf16>(dq[t][reg] * a.scale));
       sum = xsum32(sum);
       if (hf == 0) cs[32 * t + r] = sum;
     }
@@ -480,7 +503,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[2];
   __shared__ __attribute__((aligned(16))) float ls_[2][3][32];  // [buf][lse | delta | drop row key][row]
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ntiles = a.T >> 5, nbhk = a.B * a.Hkv;
+  const int ntiles = ntiles32(a.T), nbhk = a.B * a.Hkv;
   const int bhk = static_cast<int>(blockIdx.x % nbhk);
   const int grp = static_cast<int>(blockIdx.x / nbhk);
   const int ktile = grp * 4 + w;
@@ -488,11 +511,12 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
   const int first = grp * 4;  // the block's first query tile = its lowest key tile
   const int b = bhk / a.Hkv, hk = bhk % a.Hkv, group = a.H / a.Hkv;
   const int kb = ktile * 32, key = kb + r;
+  const int kc = min(key, a.T - 1);  // tail keys: a copy of key T-1, never stored
 
   bf16x8 kf[D / 16], vf[D / 16];
   if (active) {
-    const __bf16* kp = a.k + b * a.k_sb + static_cast<int64_t>(key) * a.k_st + hk * a.k_sh + 8 * hf;
-    const __bf16* vp = a.v + b * a.v_sb + static_cast<int64_t>(key) * a.v_st + hk * a.v_sh + 8 * hf;
+    const __bf16* kp = a.k + b * a.k_sb + static_cast<int64_t>(kc) * a.k_st + hk * a.k_sh + 8 * hf;
+    const __bf16* vp = a.v + b * a.v_sb + static_cast<int64_t>(kc) * a.v_st + hk * a.v_sh + 8 * hf;
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
       kf[s] = ld8(kp + 16 * s);
@@ -515,11 +539,12 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
   auto stage = [&](int i, int buf) {
     const int gh = i / nq, qt = first + i % nq;
     const int h = hk * group + gh, bh = b * a.H + h;
-    const int64_t qrow = static_cast<int64_t>(qt * 32);
-    qd.issue(a.q + b * a.q_sb + h * a.q_sh + qrow * a.q_st, qs_[buf]);
-    dd.issue(a.dout + b * a.o_sb + h * a.o_sh + qrow * a.o_st, ds_[buf]);
+    const int qrow = qt * 32;
+    qd.issue(a.q + b * a.q_sb + h * a.q_sh + static_cast<int64_t>(qrow) * a.q_st, qs_[buf], a.T - qrow);
+    dd.issue(a.dout + b * a.o_sb + h * a.o_sh + static_cast<int64_t>(qrow) * a.o_st, ds_[buf], a.T - qrow);
     if (w == 0) {
-      const float* src = (lane < 32 ? a.lse : a.delta) + static_cast<int64_t>(bh) * a.T + qt * 32 + (lane & 31);
+      const float* src = (lane < 32 ? a.lse : a.delta) + static_cast<int64_t>(bh) * a.T +
+                         min(qrow + (lane & 31), a.T - 1);
       glds4(src, &ls_[buf][0][0]);
     } else if (DROP && w == 1 && lane < 32) {
       ls_[buf][2][lane] = __uint_as_float(drop_row(a.seed, bh, qt * 32 + lane));
@@ -561,6 +586,11 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
         for (int reg = 0; reg < 16; ++reg)
           if (key > qb + acc_row(reg, hf)) s[reg] = -INFINITY;
       }
+      if (qb + 32 > a.T) {  // tail query tile: rows past T contribute nothing (p = 0, dS = 0)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+          if (qb + acc_row(reg, hf) >= a.T) s[reg] = -INFINITY;
+      }
       f32x16 pd;
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
@@ -598,6 +628,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
   for (int t = 0; t < D / 32; ++t)
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
+      if (kb + acc_row(reg, hf) >= a.T) continue;
       const int64_t off = static_cast<int64_t>(kb + acc_row(reg, hf)) * a.dk_st + 32 * t + r;
       dkb[off] = static_cast<__bf16>(dk[t][reg] * a.scale);
       dvb[off] = static_cast<__bf16>(dv[t][reg]);
@@ -609,6 +640,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
       float sk = 0.f, sv = 0.f;
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
+        if (kb + acc_row(reg, hf) >= a.T) continue;
         sk += static_cast<float>(static_cast<__bf16>(dk[t][reg] * a.scale));
         sv += static_cast<float>(static_cast<__bf16>(dv[t][reg]));
       }
@@ -624,7 +656,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
 
 // ------------------------------------------------------------------ launchers
 // ceil(tiles / 4) blocks of 4 waves per head
-static inline int64_t tile_blocks(int64_t nbh, int T) { return nbh * (((T >> 5) + 3) >> 2); }
+static inline int64_t tile_blocks(int64_t nbh, int T) { return nbh * ((((T + 31) >> 5) + 3) >> 2); }
 
 hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) {
   const dim3 grid(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T))), block(256);

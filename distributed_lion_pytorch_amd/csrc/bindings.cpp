@@ -122,7 +122,8 @@ void lion_vote_apply(const Tensor& meta, int64_t seg_off, int64_t chunk_off, int
     check_dev(*own, "own");
     ownp = own->data_ptr<uint8_t>();
     check_dev(*agree, "agree");
-    TORCH_CHECK(agree->scalar_type() == at::kLong, "dlion: agree must be int64");
+    TORCH_CHECK(agree->scalar_type() == at::kLong && agree->numel() >= 2,
+                "dlion: agree must be int64 [agreements, ties]");
     agp = reinterpret_cast<unsigned long long*>(agree->data_ptr<int64_t>());
   }
   const c10::DeviceGuard g(meta.device());
@@ -137,7 +138,7 @@ void lion_vote_apply(const Tensor& meta, int64_t seg_off, int64_t chunk_off, int
 }
 
 void vote_reduce(const Tensor& recv, int64_t nbytes, const Tensor& alive, int64_t tie, const Tensor& out,
-                 const std::optional<Tensor>& neg_out) {
+                 const std::optional<Tensor>& neg_out, const std::optional<Tensor>& ties) {
   check_dev(recv, "recv");
   check_dev(alive, "alive");
   check_dev(out, "out");
@@ -149,10 +150,16 @@ void vote_reduce(const Tensor& recv, int64_t nbytes, const Tensor& alive, int64_
     check_dev(*neg_out, "neg_out");
     negp = neg_out->data_ptr<uint8_t>();
   }
+  unsigned long long* tp = nullptr;
+  if (ties.has_value()) {
+    check_dev(*ties, "ties");
+    TORCH_CHECK(ties->scalar_type() == at::kLong && ties->numel() >= 1, "dlion: ties must be int64");
+    tp = reinterpret_cast<unsigned long long*>(ties->data_ptr<int64_t>());
+  }
   const c10::DeviceGuard g(recv.device());
   check_hip(dlion::launch_vote_reduce(recv.data_ptr<uint8_t>(), nbytes, alive.data_ptr<uint8_t>(),
                                       static_cast<int>(alive.numel()), static_cast<int>(tie),
-                                      out.data_ptr<uint8_t>(), negp, cur_stream()),
+                                      out.data_ptr<uint8_t>(), negp, tp, cur_stream()),
             "vote_reduce");
 }
 
@@ -198,7 +205,7 @@ dlion::AttnArgs attn_args(const Tensor& q, const Tensor& k, const Tensor& v, dou
   const int64_t B = q.size(0), T = q.size(1), H = q.size(2), D = q.size(3), Hkv = k.size(2);
   TORCH_CHECK(k.size(0) == B && k.size(1) == T && k.size(3) == D && v.sizes() == k.sizes(), "dlion attn: shape mismatch");
   TORCH_CHECK(H % Hkv == 0, "dlion attn: H must be a multiple of Hkv");
-  TORCH_CHECK(T % 64 == 0 && (D == 64 || D == 128), "dlion attn: need T % 64 == 0 and D in {64, 128}");
+  TORCH_CHECK(T >= 1 && (D == 64 || D == 128), "dlion attn: need T >= 1 and D in {64, 128}");
   TORCH_CHECK(p >= 0.0 && p < 1.0, "dlion attn: dropout must be in [0, 1)");
   dlion::AttnArgs a{};
   a.q = static_cast<const __bf16*>(q.data_ptr());
@@ -258,9 +265,9 @@ void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
   if (colsum.has_value()) {
     TORCH_CHECK(a.H == a.Hkv, "dlion attn: bias-gradient partials need H == Hkv");
     TORCH_CHECK(colsum->is_cuda() && colsum->scalar_type() == at::kFloat && colsum->is_contiguous() &&
-                    colsum->dim() == 2 && colsum->size(0) == q.size(0) * (q.size(1) / 32) &&
+                    colsum->dim() == 2 && colsum->size(0) == q.size(0) * ((q.size(1) + 31) / 32) &&
                     colsum->size(1) == 3 * q.size(2) * q.size(3),
-                "dlion attn: colsum must be fp32 [B * T / 32, 3 * H * D]");
+                "dlion attn: colsum must be fp32 [B * ceil(T / 32), 3 * H * D]");
     a.colsum = colsum->data_ptr<float>();
   }
   check_hip(dlion::launch_attn_bwd(a, static_cast<int>(q.size(3)), a.thresh16 > 0, cur_stream()), "attn_bwd");
@@ -1083,7 +1090,8 @@ TORCH_LIBRARY(dlion, m) {
       "lion_vote_apply(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, Tensor planes,"
       " int plane_stride, Tensor alive, int mode, int tie, Tensor? neg, float decay, float neg_lr,"
       " Tensor? own, Tensor(b!)? agree) -> ()");
-  m.def("vote_reduce(Tensor recv, int nbytes, Tensor alive, int tie, Tensor(a!) out, Tensor(b!)? neg_out) -> ()");
+  m.def("vote_reduce(Tensor recv, int nbytes, Tensor alive, int tie, Tensor(a!) out, Tensor(b!)? neg_out,"
+        " Tensor(c!)? ties=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dlion, CUDA, m) {

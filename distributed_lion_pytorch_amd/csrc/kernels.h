@@ -23,7 +23,7 @@ hipError_t launch_lion_vote_apply(int dt, const int64_t* seg, const int64_t* chu
                                   int mode, int tie, const uint8_t* neg, float decay, float neg_lr, const uint8_t* own,
                                   unsigned long long* agree, hipStream_t st);
 hipError_t launch_vote_reduce(const uint8_t* recv, int64_t nbytes, const uint8_t* alive, int world, int tie,
-                              uint8_t* out, uint8_t* neg_out, hipStream_t st);
+                              uint8_t* out, uint8_t* neg_out, unsigned long long* ties, hipStream_t st);
 
 // ---- flash attention (attention.hip)
 hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st);

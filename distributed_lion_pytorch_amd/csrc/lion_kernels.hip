@@ -56,6 +56,37 @@ __device__ __forceinline__ float sgn(float x) {  // ATen sign: NaN -> 0, +-0 -> 
   return static_cast<float>((x > 0.f) - (x < 0.f));
 }
 
+// Raw 8-element vectors for the full-chunk fast paths: every load of a
+// block's 4 iterations is issued before the first use (a chunk that lies
+// wholly inside a 16-byte-aligned tensor -- all but the last chunk of a
+// tensor).  In the general loop below the per-iteration bounds test keeps
+// hipcc from hoisting iteration i+1's loads above iteration i's stores, so
+// each lane had one load in flight at a time: K2 reached 68 % of HBM against
+// K0's 89 % (profiles/lion/bench_lion_roofline.txt).
+template <int DT>
+struct Raw8 {
+  static constexpr int N = DT == kF32 ? 2 : 1;  // uint4 per 8 elements
+  uint4 v[N];
+  __device__ __forceinline__ void load(const typename Elem<DT>::S* p) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = reinterpret_cast<const uint4*>(p)[i];
+  }
+  __device__ __forceinline__ void unpack(float (&o)[8]) const {
+    if constexpr (DT == kF32) {
+      const uint32_t w[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = __uint_as_float(w[j]);
+    } else {
+      const uint32_t w[4] = {v[0].x, v[0].y, v[0].z, v[0].w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        o[2 * i] = Elem<DT>::to_f(static_cast<uint16_t>(w[i] & 0xffffu));
+        o[2 * i + 1] = Elem<DT>::to_f(static_cast<uint16_t>(w[i] >> 16));
+      }
+    }
+  }
+};
+
 // Fused gradient clipping: g <- round(g * coef) in the parameter dtype, i.e.
 // what clip_grad_norm_'s in-place _foreach_mul_ would have stored, applied on
 // load instead of as a separate read+write pass over every gradient.
@@ -79,6 +110,35 @@ lion_local_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ c
   S* p = const_cast<S*>(static_cast<const S*>(r.p));
   const S* g = static_cast<const S*>(r.g);
   S* m = const_cast<S*>(static_cast<const S*>(r.m));
+  if (r.vec && start + kChunk <= r.n) {  // block-uniform: all loads first
+    Raw8<DT> rp[kIters], rg[kIters], rm[kIters];
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int64_t e = start + it * kSpan + threadIdx.x * 8;
+      rp[it].load(p + e);
+      rg[it].load(g + e);
+      rm[it].load(m + e);
+    }
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int64_t e = start + it * kSpan + threadIdx.x * 8;
+      float pv[8], gv[8], mv[8];
+      rp[it].unpack(pv);
+      rg[it].unpack(gv);
+      rm[it].unpack(mv);
+      if (gscale != nullptr) clip8<DT>(gv, cs);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float pw = E::rnd(pv[j] * decay);
+        const float u = E::rnd(__fmaf_rn(gv[j], omb1, E::rnd(mv[j] * b1)));
+        pv[j] = __fmaf_rn(neg_lr, sgn(u), pw);
+        mv[j] = __fmaf_rn(gv[j], omb2, E::rnd(mv[j] * b2));
+      }
+      E::store8(p + e, pv);
+      E::store8(m + e, mv);
+    }
+    return;
+  }
 #pragma unroll
   for (int it = 0; it < kIters; ++it) {
     const int64_t e = start + it * kSpan + threadIdx.x * 8;
@@ -118,6 +178,34 @@ lion_encode_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ 
   const S* g = static_cast<const S*>(r.g);
   S* m = const_cast<S*>(static_cast<const S*>(r.m));
   const int64_t region = (r.n + kSpan - 1) / kSpan * kSpan;
+  if (!STOC && r.vec && start + kChunk <= r.n) {  // block-uniform: all loads first
+    Raw8<DT> rg[kIters], rm[kIters];
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int64_t e = start + it * kSpan + threadIdx.x * 8;
+      rg[it].load(g + e);
+      rm[it].load(m + e);
+    }
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int64_t e = start + it * kSpan + threadIdx.x * 8;
+      float gv[8], mv[8];
+      rg[it].unpack(gv);
+      rm[it].unpack(mv);
+      if (gscale != nullptr) clip8<DT>(gv, cs);
+      uint32_t byte = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        byte |= static_cast<uint32_t>(E::rnd(__fmaf_rn(gv[j], omb1, E::rnd(mv[j] * b1))) > 0.f) << j;
+      if (update_m) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mv[j] = __fmaf_rn(gv[j], omb2, E::rnd(mv[j] * b2));
+        E::store8(m + e, mv);
+      }
+      bits[(r.bit_off + e) >> 3] = static_cast<uint8_t>(byte);
+    }
+    return;
+  }
 #pragma unroll
   for (int it = 0; it < kIters; ++it) {
     const int64_t e = start + it * kSpan + threadIdx.x * 8;
@@ -188,7 +276,7 @@ lion_vote_apply_kernel(const int64_t* __restrict__ seg, const int64_t* __restric
   int n_live = 0;  // liveness is a device vector: no host sync to learn who voted
   for (int k = 0; k < world; ++k) n_live += alive[k] != 0;
   const float inv_n = n_live > 0 ? 1.f / static_cast<float>(n_live) : 0.f;
-  uint32_t n_agree = 0;
+  uint32_t n_agree = 0, n_tie = 0;
 #pragma unroll
   for (int it = 0; it < kIters; ++it) {
     const int64_t e = start + it * kSpan + threadIdx.x * 8;
@@ -214,6 +302,7 @@ lion_vote_apply_kernel(const int64_t* __restrict__ seg, const int64_t* __restric
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int twice = 2 * static_cast<int>(cnt[j]);
+        if (agree != nullptr && n_live > 0 && twice == n_live && e + j < r.n) ++n_tie;
         if (n_live == 0)
           delta[j] = 0.f;  // nobody voted: weight decay only
         else if (mode == 1)
@@ -236,8 +325,14 @@ lion_vote_apply_kernel(const int64_t* __restrict__ seg, const int64_t* __restric
   }
   if (agree != nullptr) {
     // wave reduce then one atomic per wave (Guideline 12)
-    for (int off = 32; off > 0; off >>= 1) n_agree += __shfl_xor(n_agree, off);
-    if ((threadIdx.x & 63) == 0) atomicAdd(agree, static_cast<unsigned long long>(n_agree));
+    for (int off = 32; off > 0; off >>= 1) {
+      n_agree += __shfl_xor(n_agree, off);
+      n_tie += __shfl_xor(n_tie, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(agree, static_cast<unsigned long long>(n_agree));
+      if (n_tie) atomicAdd(agree + 1, static_cast<unsigned long long>(n_tie));
+    }
   }
 }
 
@@ -255,7 +350,7 @@ constexpr int kMaxSliced = 15;
 // K = floor(n_live / 2) compared bit-sliced from the MSB.  pos / neg follow the
 // byte kernels' rules (ties by `tie`, nobody alive -> neither).
 __device__ __forceinline__ void sliced_vote(const uint32_t (&w)[kMaxSliced], int world, int n_live, int tie,
-                                            uint32_t& pos, uint32_t& neg) {
+                                            uint32_t& pos, uint32_t& neg, uint32_t& ties) {
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
 #pragma unroll
   for (int k = 0; k < kMaxSliced; ++k) {
@@ -281,6 +376,7 @@ __device__ __forceinline__ void sliced_vote(const uint32_t (&w)[kMaxSliced], int
       eq &= ~cb[b];
     }
   }
+  ties = 0;
   if (n_live == 0) {
     pos = neg = 0;  // nobody voted: weight decay only
   } else if (n_live & 1) {
@@ -290,6 +386,7 @@ __device__ __forceinline__ void sliced_vote(const uint32_t (&w)[kMaxSliced], int
     const uint32_t lt = ~(gt | eq);
     pos = gt | (tie == 2 ? eq : 0u);
     neg = lt | (tie == 0 ? eq : 0u);
+    ties = eq;  // count == n_live / 2: resolved by the tie rule
   }
 }
 
@@ -312,17 +409,61 @@ lion_vote_apply32_kernel(const int64_t* __restrict__ seg, const int64_t* __restr
       live_mask |= 1u << k;
       ++n_live;
     }
-  uint32_t n_agree = 0;
+  uint32_t n_agree = 0, n_tie = 0;
   // Each lane owns 8 consecutive coordinates (coalesced 16-byte p accesses,
   // as in K0); the 4 lanes of a 32-coordinate group load the same plane dword
   // and vote on all of it, then keep their byte.
   const int sub = threadIdx.x & 3;  // bit_off % 2048 == 0, start % 8192 == 0
+  if (r.vec && start + kChunk <= r.n && agree == nullptr) {  // block-uniform: all loads first
+    Raw8<DT> rp[kIters];
+    uint32_t pw[kIters], nw[kIters];
+    if (mode == 2) {
+#pragma unroll
+      for (int it = 0; it < kIters; ++it) {
+        const int64_t e = start + it * kSpan + threadIdx.x * 8;
+        const int64_t word = (r.bit_off + e) >> 5;
+        rp[it].load(p + e);
+        pw[it] = reinterpret_cast<const uint32_t*>(planes)[word];
+        nw[it] = neg_plane ? reinterpret_cast<const uint32_t*>(neg_plane)[word] : ~pw[it];
+      }
+    } else {
+      uint32_t w[kIters][kMaxSliced];
+#pragma unroll
+      for (int it = 0; it < kIters; ++it) {
+        const int64_t e = start + it * kSpan + threadIdx.x * 8;
+        const int64_t word = (r.bit_off + e) >> 5;
+        rp[it].load(p + e);
+#pragma unroll
+        for (int k = 0; k < kMaxSliced; ++k)
+          w[it][k] = (live_mask >> k) & 1 ? reinterpret_cast<const uint32_t*>(planes + k * plane_stride)[word] : 0u;
+      }
+#pragma unroll
+      for (int it = 0; it < kIters; ++it) {
+        uint32_t tb;
+        sliced_vote(w[it], world, n_live, tie, pw[it], nw[it], tb);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int64_t e = start + it * kSpan + threadIdx.x * 8;
+      const uint32_t pos = (pw[it] >> (8 * sub)) & 0xffu, neg = (nw[it] >> (8 * sub)) & 0xffu;
+      float pv[8];
+      rp[it].unpack(pv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float delta = static_cast<float>(static_cast<int>((pos >> j) & 1) - static_cast<int>((neg >> j) & 1));
+        pv[j] = __fmaf_rn(neg_lr, delta, E::rnd(pv[j] * decay));
+      }
+      E::store8(p + e, pv);
+    }
+    return;
+  }
 #pragma unroll
   for (int it = 0; it < kIters; ++it) {
     const int64_t e = start + it * kSpan + threadIdx.x * 8;
     if (e >= r.n) break;
     const int64_t word = (r.bit_off + e) >> 5;
-    uint32_t pos, neg;
+    uint32_t pos, neg, tb = 0;
     if (mode == 2) {
       pos = reinterpret_cast<const uint32_t*>(planes)[word];
       neg = neg_plane ? reinterpret_cast<const uint32_t*>(neg_plane)[word] : ~pos;
@@ -331,7 +472,7 @@ lion_vote_apply32_kernel(const int64_t* __restrict__ seg, const int64_t* __restr
 #pragma unroll
       for (int k = 0; k < kMaxSliced; ++k)  // every live plane's load first
         w[k] = (live_mask >> k) & 1 ? reinterpret_cast<const uint32_t*>(planes + k * plane_stride)[word] : 0u;
-      sliced_vote(w, world, n_live, tie, pos, neg);
+      sliced_vote(w, world, n_live, tie, pos, neg, tb);
     }
     pos = (pos >> (8 * sub)) & 0xffu;
     neg = (neg >> (8 * sub)) & 0xffu;
@@ -340,6 +481,7 @@ lion_vote_apply32_kernel(const int64_t* __restrict__ seg, const int64_t* __restr
       const int64_t left = r.n - e;
       const uint32_t valid = left >= 8 ? 0xffu : ((1u << left) - 1u);
       n_agree += __popc(((mine & pos) | (~mine & neg)) & valid);
+      n_tie += __popc((tb >> (8 * sub)) & valid);  // (pre-voted planes: the ties were counted by K4)
     }
     float pv[8];
     load8g<DT>(p, e, r.n, r.vec, pv);
@@ -351,8 +493,14 @@ lion_vote_apply32_kernel(const int64_t* __restrict__ seg, const int64_t* __restr
     store8g<DT>(p, e, r.n, r.vec, pv);
   }
   if (agree != nullptr) {
-    for (int off = 32; off > 0; off >>= 1) n_agree += __shfl_xor(n_agree, off);
-    if ((threadIdx.x & 63) == 0) atomicAdd(agree, static_cast<unsigned long long>(n_agree));
+    for (int off = 32; off > 0; off >>= 1) {
+      n_agree += __shfl_xor(n_agree, off);
+      n_tie += __shfl_xor(n_tie, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(agree, static_cast<unsigned long long>(n_agree));
+      if (n_tie) atomicAdd(agree + 1, static_cast<unsigned long long>(n_tie));
+    }
   }
 }
 
@@ -362,56 +510,87 @@ lion_vote_apply32_kernel(const int64_t* __restrict__ seg, const int64_t* __restr
 // 4 bytes (32 coordinates) per thread, grid-stride.
 __global__ void __launch_bounds__(kThreads)
 vote_reduce_kernel(const uint8_t* __restrict__ recv, int64_t nbytes, const uint8_t* __restrict__ alive,
-                   int world, int tie, uint8_t* __restrict__ out, uint8_t* __restrict__ neg_out) {
+                   int world, int tie, uint8_t* __restrict__ out, uint8_t* __restrict__ neg_out,
+                   unsigned long long* __restrict__ ties) {
   const int64_t nwords = nbytes >> 2;  // nbytes % 4 == 0 guaranteed by the planner
   int n_live = 0;
   for (int k = 0; k < world; ++k) n_live += alive[k] != 0;
+  uint32_t n_tie = 0;  // tie-rate telemetry (ties != nullptr)
   if (world <= kMaxSliced) {  // bit-sliced counters, every plane word loaded up front
     uint32_t live_mask = 0;
     for (int k = 0; k < world; ++k) live_mask |= static_cast<uint32_t>(alive[k] != 0) << k;
-    for (int64_t w = blockIdx.x * (int64_t)kThreads + threadIdx.x; w < nwords;
+    // 16 bytes per plane per thread (one dwordx4 load per plane, 4 KiB per
+    // wave instruction): the dword version left the kernel at 40 % of HBM
+    const bool v16 = (nbytes & 15) == 0 && (reinterpret_cast<uintptr_t>(recv) & 15) == 0 &&
+                     (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
+                     (neg_out == nullptr || (reinterpret_cast<uintptr_t>(neg_out) & 15) == 0);
+    const int64_t nq = v16 ? nwords >> 2 : 0;
+    for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < nq; i += (int64_t)gridDim.x * kThreads) {
+      uint4 v[kMaxSliced];
+#pragma unroll
+      for (int k = 0; k < kMaxSliced; ++k)
+        v[k] = (live_mask >> k) & 1 ? reinterpret_cast<const uint4*>(recv + k * nbytes)[i] : make_uint4(0, 0, 0, 0);
+      uint32_t pos[4], ng[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t x[kMaxSliced], tb;
+#pragma unroll
+        for (int k = 0; k < kMaxSliced; ++k) x[k] = c == 0 ? v[k].x : c == 1 ? v[k].y : c == 2 ? v[k].z : v[k].w;
+        sliced_vote(x, world, n_live, tie, pos[c], ng[c], tb);
+        n_tie += __popc(tb);
+      }
+      reinterpret_cast<uint4*>(out)[i] = make_uint4(pos[0], pos[1], pos[2], pos[3]);
+      if (neg_out != nullptr) reinterpret_cast<uint4*>(neg_out)[i] = make_uint4(ng[0], ng[1], ng[2], ng[3]);
+    }
+    for (int64_t w = 4 * nq + blockIdx.x * (int64_t)kThreads + threadIdx.x; w < nwords;
          w += (int64_t)gridDim.x * kThreads) {
       uint32_t v[kMaxSliced];
 #pragma unroll
       for (int k = 0; k < kMaxSliced; ++k)
         v[k] = (live_mask >> k) & 1 ? reinterpret_cast<const uint32_t*>(recv + k * nbytes)[w] : 0u;
-      uint32_t pos, ng;
-      sliced_vote(v, world, n_live, tie, pos, ng);
+      uint32_t pos, ng, tb;
+      sliced_vote(v, world, n_live, tie, pos, ng, tb);
+      n_tie += __popc(tb);
       reinterpret_cast<uint32_t*>(out)[w] = pos;
       if (neg_out != nullptr) reinterpret_cast<uint32_t*>(neg_out)[w] = ng;
     }
-    return;
-  }
-  for (int64_t w = blockIdx.x * (int64_t)kThreads + threadIdx.x; w < nwords;
-       w += (int64_t)gridDim.x * kThreads) {
-    uint32_t cnt[32];
+  } else {  // wider worlds: byte-spread counters
+    for (int64_t w = blockIdx.x * (int64_t)kThreads + threadIdx.x; w < nwords;
+         w += (int64_t)gridDim.x * kThreads) {
+      uint32_t cnt[32];
 #pragma unroll
-    for (int j = 0; j < 32; ++j) cnt[j] = 0;
-    for (int r0 = 0; r0 < world; r0 += 255) {
-      const int r1 = min(world, r0 + 255);
-      uint64_t acc[4] = {0, 0, 0, 0};
-      for (int k = r0; k < r1; ++k) {
-        if (!alive[k]) continue;
-        const uint32_t v = reinterpret_cast<const uint32_t*>(recv + k * nbytes)[w];
+      for (int j = 0; j < 32; ++j) cnt[j] = 0;
+      for (int r0 = 0; r0 < world; r0 += 255) {
+        const int r1 = min(world, r0 + 255);
+        uint64_t acc[4] = {0, 0, 0, 0};
+        for (int k = r0; k < r1; ++k) {
+          if (!alive[k]) continue;
+          const uint32_t v = reinterpret_cast<const uint32_t*>(recv + k * nbytes)[w];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[b] += spread8(v >> (8 * b));
+          for (int b = 0; b < 4; ++b) acc[b] += spread8(v >> (8 * b));
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) cnt[8 * b + j] += static_cast<uint32_t>((acc[b] >> (8 * j)) & 0xffu);
       }
+      uint32_t pos = 0, ng = 0;
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) cnt[8 * b + j] += static_cast<uint32_t>((acc[b] >> (8 * j)) & 0xffu);
+      for (int j = 0; j < 32; ++j) {
+        const int twice = 2 * static_cast<int>(cnt[j]);
+        const bool is_pos = n_live > 0 && (twice > n_live || (twice == n_live && tie == 2));
+        const bool is_neg = n_live > 0 && (twice < n_live || (twice == n_live && tie == 0));
+        n_tie += n_live > 0 && twice == n_live;
+        pos |= static_cast<uint32_t>(is_pos) << j;
+        ng |= static_cast<uint32_t>(is_neg) << j;
+      }
+      reinterpret_cast<uint32_t*>(out)[w] = pos;
+      if (neg_out != nullptr) reinterpret_cast<uint32_t*>(neg_out)[w] = ng;
     }
-    uint32_t pos = 0, ng = 0;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const int twice = 2 * static_cast<int>(cnt[j]);
-      const bool is_pos = n_live > 0 && (twice > n_live || (twice == n_live && tie == 2));
-      const bool is_neg = n_live > 0 && (twice < n_live || (twice == n_live && tie == 0));
-      pos |= static_cast<uint32_t>(is_pos) << j;
-      ng |= static_cast<uint32_t>(is_neg) << j;
-    }
-    reinterpret_cast<uint32_t*>(out)[w] = pos;
-    if (neg_out != nullptr) reinterpret_cast<uint32_t*>(neg_out)[w] = ng;
+  }
+  if (ties != nullptr) {
+    for (int off = 32; off > 0; off >>= 1) n_tie += __shfl_xor(n_tie, off);
+    if ((threadIdx.x & 63) == 0 && n_tie) atomicAdd(ties, static_cast<unsigned long long>(n_tie));
   }
 }
 
@@ -546,13 +725,13 @@ hipError_t launch_clip_coef(const float* partial, int64_t n, float max_norm, flo
 }
 
 hipError_t launch_vote_reduce(const uint8_t* recv, int64_t nbytes, const uint8_t* alive, int world, int tie,
-                              uint8_t* out, uint8_t* neg_out, hipStream_t st) {
+                              uint8_t* out, uint8_t* neg_out, unsigned long long* ties, hipStream_t st) {
   const int64_t nwords = nbytes >> 2;
   if (nwords == 0) return hipSuccess;
   int64_t blocks = (nwords + kThreads - 1) / kThreads;
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(vote_reduce_kernel, dim3(blocks), dim3(kThreads), 0, st, recv, nbytes, alive, world, tie,
-                     out, neg_out);
+                     out, neg_out, ties);
   return hipGetLastError();
 }
 

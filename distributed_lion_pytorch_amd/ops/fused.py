@@ -641,7 +641,31 @@ def embed(ids: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor, p: float) -> 
 
 # ------------------------------------------------------------------ attention
 def _attn_ok(x: torch.Tensor, T: int, D: int) -> bool:
-    return x.dtype == torch.bfloat16 and D in (64, 128) and T % 64 == 0 and _use_hip(x)
+    """The gfx950 flash kernels take any sequence length (tail tiles are
+    masked in-kernel) at head_dim 64 / 128 -- every GPT-2 and Llama-2/3 size."""
+    return x.dtype == torch.bfloat16 and D in (64, 128) and T >= 1 and _use_hip(x)
+
+
+_MATH_WARNED = set()
+
+
+def _sdpa_math(q, k, v, dropout_p: float) -> torch.Tensor:
+    """Fallback for what the flash kernels do not cover (head_dim not in {64,
+    128}, fp32/fp16 inputs, no extension): PyTorch's *math* SDPA backend only
+    -- matmul + softmax ATen ops (hipBLASLt GEMMs) -- never the flash /
+    memory-efficient backends, which on ROCm are Triton-built (aotriton).
+    O(T^2) memory; a one-time warning names the shape."""
+    from torch.nn.attention import SDPBackend, sdpa_kernel
+
+    key = (tuple(q.shape[-2:]), q.dtype, q.device.type)
+    if q.is_cuda and key not in _MATH_WARNED:
+        _MATH_WARNED.add(key)
+        import warnings
+
+        warnings.warn(f"dlion attention: no gfx950 flash kernel for head_dim={q.shape[-1]} / {q.dtype}; "
+                      "using the math SDPA backend (O(T^2) memory)")
+    with sdpa_kernel([SDPBackend.MATH]):
+        return F.scaled_dot_product_attention(q, k, v, dropout_p=dropout_p, is_causal=True)
 
 
 def _new_seed() -> int:
@@ -701,7 +725,7 @@ def causal_attention(qkv: torch.Tensor, dropout_p: float) -> torch.Tensor:
         with torch.autocast("cuda", enabled=False):
             return _FlashAttnPacked.apply(qkv, float(dropout_p), _new_seed()).view(B, T, H * D)
     q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)  # [B, H, T, D] views
-    y = F.scaled_dot_product_attention(q, k, v, dropout_p=dropout_p, is_causal=True)
+    y = _sdpa_math(q, k, v, dropout_p)
     return y.transpose(1, 2).reshape(B, T, H * D)
 
 
@@ -737,7 +761,7 @@ class _QKVAttention(torch.autograd.Function):
         B, T = qkv.shape[:2]
         dout = dy.reshape(out.shape).contiguous()
         dqkv = torch.empty_like(qkv)
-        part = torch.empty(B * (T // 32), w.shape[1], dtype=torch.float32, device=qkv.device)
+        part = torch.empty(B * ((T + 31) // 32), w.shape[1], dtype=torch.float32, device=qkv.device)
         hip.ops().attn_bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], out, dout, lse, ctx.p, ctx.seed,
                            dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], part)
         g = dqkv.view(B * T, -1)
@@ -793,7 +817,7 @@ def causal_attention_gqa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, drop
     if rep > 1:
         kh = kh.repeat_interleave(rep, dim=1)
         vh = vh.repeat_interleave(rep, dim=1)
-    y = F.scaled_dot_product_attention(qh, kh, vh, dropout_p=dropout_p, is_causal=True)
+    y = _sdpa_math(qh, kh, vh, dropout_p)
     return y.transpose(1, 2).reshape(B, T, H * D)
 
 

@@ -69,8 +69,8 @@ class HipExecutor:
                                  planes, stride, alive, mode, tie, neg, hp.decay, -hp.lr, own, agree)
 
     def vote_reduce(self, recv: torch.Tensor, nbytes: int, alive: torch.Tensor, tie: int, out: torch.Tensor,
-                    neg_out: Optional[torch.Tensor]) -> None:
-        self.ops.vote_reduce(recv, nbytes, alive, tie, out, neg_out)
+                    neg_out: Optional[torch.Tensor], ties: Optional[torch.Tensor] = None) -> None:
+        self.ops.vote_reduce(recv, nbytes, alive, tie, out, neg_out, ties)
 
 
 class TorchExecutor:
@@ -122,14 +122,23 @@ class TorchExecutor:
                 delta = ref.vote_delta(bits, alive, mode, tie)
             if agree is not None and own is not None:
                 mine = ref.unpack_bits(own[o:o + nb], s.numel)
-                agree += ((mine.float() * 2 - 1) * delta > 0).sum().to(agree.dtype)
+                agree[0] += ((mine.float() * 2 - 1) * delta > 0).sum().to(agree.dtype)
+                if mode != ref.VOTE_PREVOTED:  # pre-voted planes: K4 counted the ties
+                    live = alive.to(torch.bool)
+                    twice = 2 * bits[live].to(torch.int64).sum(0)
+                    agree[1] += ((twice == int(live.sum())) & (int(live.sum()) > 0)).sum().to(agree.dtype)
             ref.apply_delta_(s.param, delta.to(s.param.device), hp.lr, hp.wd)
 
     def vote_reduce(self, recv: torch.Tensor, nbytes: int, alive: torch.Tensor, tie: int, out: torch.Tensor,
-                    neg_out: Optional[torch.Tensor]) -> None:
+                    neg_out: Optional[torch.Tensor], ties: Optional[torch.Tensor] = None) -> None:
         w = alive.numel()
         bits = ref.unpack_bits(recv[: w * nbytes].view(w, nbytes))
         pos, ngb = ref.vote_reduce_bits(bits, alive, tie)
+        if ties is not None:
+            live = alive.to(torch.bool)
+            n_live = int(live.sum())
+            twice = 2 * bits[live].to(torch.int64).sum(0)
+            ties += ((twice == n_live) & (n_live > 0)).sum().to(ties.dtype)
         out[:nbytes] = ref.pack_bits(pos)
         if neg_out is not None:
             neg_out[:nbytes] = ref.pack_bits(ngb)

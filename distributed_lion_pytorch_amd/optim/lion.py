@@ -107,7 +107,8 @@ class Lion(Optimizer):
         self._dropped: set = set()
         self._dropout_schedule: Dict[int, Sequence[int]] = {}
         self._agree: Optional[torch.Tensor] = None
-        self._agree_total = 0
+        self._agree_coords = 0  # coordinates covered by the agreement counter since the last stats()
+        self._tie_coords = 0
         self.last_world = 1
         self.elastic_timeout = elastic_timeout
         self._elastic = None
@@ -317,8 +318,7 @@ class Lion(Optimizer):
             return self._elastic_step(plan, ex, meta, hps, grads, moms, world, rank, gscale)
         xch, t = self._exchange, self.phase_timer
         alive = self._alive(world, plan.device)
-        if self.telemetry and self._agree is None:
-            self._agree = torch.zeros(1, dtype=torch.int64, device=plan.device)
+        self._telemetry_setup(plan, xch)
         # encode bucket i, then its collective overlaps the encode of i+1
         states = self._encode_launch(plan, ex, meta, hps, grads, moms, rank, gscale, alive)
         with phase_of(t, "exchange"):
@@ -330,6 +330,21 @@ class Lion(Optimizer):
                 ex.apply(meta, b, a.planes, a.stride, alive, a.mode, ref.TIE_CODES[self.tie_break], a.neg,
                          hps[b.group], own=xch.send_view(b) if self.telemetry else None,
                          agree=self._agree if self.telemetry else None)
+
+    def _telemetry_setup(self, plan, xch) -> None:
+        """telemetry: [agreements, ties] counters on the device, and the number
+        of coordinates they cover (this rank votes on all of them, or on its
+        1/W shard under a2a, where K4 counts the ties)."""
+        if not self.telemetry:
+            return
+        if self._agree is None or self._agree.device != plan.device:
+            self._agree = torch.zeros(2, dtype=torch.int64, device=plan.device)
+        if xch is not None and hasattr(xch, "need_neg"):  # a2a
+            xch.ties = self._agree[1:2]
+            self._tie_coords += sum(b.nbytes * 8 // xch.world for b in plan.buckets)
+        else:
+            self._tie_coords += sum(s.numel for s in plan.segments)
+        self._agree_coords += sum(s.numel for s in plan.segments)
 
     def _encode_launch(self, plan, ex, meta, hps, grads, moms, rank, gscale, alive):
         xch, stochastic, t = self._exchange, self.max_grad_norm is not None, self.phase_timer
@@ -358,8 +373,7 @@ class Lion(Optimizer):
 
         el, xch, t = self._elastic, self._exchange, self.phase_timer
         alive = self._alive(world, plan.device)
-        if self.telemetry and self._agree is None:
-            self._agree = torch.zeros(1, dtype=torch.int64, device=plan.device)
+        self._telemetry_setup(plan, xch)
         tie = ref.TIE_CODES[self.tie_break]
         ok = True
         try:
@@ -435,9 +449,14 @@ class Lion(Optimizer):
         if self._elastic is not None:
             out.update(self._elastic.stats())
         if self._agree is not None:
-            out["vote_agree"] = int(self._agree.item())
+            agree, ties = (int(x) for x in self._agree.tolist())  # one device sync (telemetry only)
+            out["vote_agree"] = agree
+            out["vote_ties"] = ties
+            out["vote_agree_rate"] = agree / max(1, self._agree_coords)
+            out["vote_tie_rate"] = ties / max(1, self._tie_coords)
             if reset:
                 self._agree.zero_()
+                self._agree_coords = self._tie_coords = 0
         return out
 
     @property

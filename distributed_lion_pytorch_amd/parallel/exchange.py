@@ -83,6 +83,7 @@ class VoteExchange:
         self.executor = executor
         self.tie, self.mode = tie, mode
         self.wire = WireCounter()
+        self.ties: Optional[torch.Tensor] = None  # int64 tie counter (telemetry), set by the optimizer
         # ``send``: reuse already-encoded planes (the elastic re-vote after a regroup)
         self.send = send if send is not None else torch.zeros(plan.total_bytes, dtype=torch.uint8,
                                                               device=plan.device)
@@ -154,7 +155,7 @@ class AllToAllExchange(VoteExchange):
         shard = b.nbytes // self.world
         pos = self._v(self.shard_pos, b, self.world)
         neg = self._v(self.shard_neg, b, self.world) if self.need_neg else None
-        self.executor.vote_reduce(self._v(self.recv, b), shard, alive, self.tie, pos, neg)
+        self.executor.vote_reduce(self._v(self.recv, b), shard, alive, self.tie, pos, neg, self.ties)
         works = [dist.all_gather_into_tensor(self._v(self.voted, b), pos, group=self.group, async_op=True)]
         if self.need_neg:
             works.append(dist.all_gather_into_tensor(self._v(self.voted_neg, b), neg, group=self.group,

@@ -200,14 +200,27 @@ class AsyncMixin:
             self.log({"replicas_identical": float(same), "world_end": float(dist.get_world_size())})
         return out
 
+    def _phase_timer(self):
+        """HIP-event phase times of the step (fwd_bwd, clip, and Lion's encode /
+        exchange / apply) for metrics.jsonl; ``DLION_PHASE_TIMES=0`` disables."""
+        lion = _lion_of(self.optimizer)
+        if lion is None or os.environ.get("DLION_PHASE_TIMES", "1") == "0":
+            return None
+        if lion.phase_timer is None:
+            from ..utils.timing import PhaseTimer
+
+            lion.phase_timer = PhaseTimer(self.args.device)
+        return lion.phase_timer
+
     def _training_step(self, model, inputs, num_items_in_batch=None):
         from ..ops.linear import begin_fusion_window, end_fusion_window
+        from ..utils.timing import phase_of
 
         fuse = self._engine_fusion(model)
         if fuse:
             begin_fusion_window(getattr(self, "current_gradient_accumulation_steps", None))
         try:
-            with no_sync(model):
+            with no_sync(model), phase_of(self._phase_timer(), "fwd_bwd"):
                 loss = super().training_step(model, inputs, num_items_in_batch)
         except BaseException:
             if fuse:
@@ -219,6 +232,9 @@ class AsyncMixin:
             from ..ops.fused import check_index_errors
 
             check_index_errors()  # out-of-range ids / labels flagged by the kernels (no stall)
+            t = self._phase_timer()
+            if t is not None:
+                t.step()
         return loss
 
     def _prepare_input(self, data):
@@ -270,6 +286,12 @@ class AsyncMixin:
         return n
 
     def _clip_grad_norm(self, model):
+        from ..utils.timing import phase_of
+
+        with phase_of(self._phase_timer(), "clip"):
+            return self._clip_grad_norm_impl(model)
+
+    def _clip_grad_norm_impl(self, model):
         lion = _lion_of(self.optimizer)
         if lion is not None and self._engine_fusion(model):
             mine = {id(p) for g in lion.param_groups for p in g["params"]}

@@ -42,6 +42,9 @@ class JsonlMetricsCallback(TrainerCallback):
 
     def on_log(self, args, state, control, logs=None, optimizer=None, **kw):
         if not is_rank0():
+            timer = getattr(getattr(optimizer, "optimizer", optimizer), "phase_timer", None)
+            if timer is not None:
+                timer.reset()  # only rank 0 reports; the others must not accumulate events
             return
         now = time.perf_counter()
         rec = {"step": state.global_step, "time": time.time()}
@@ -55,6 +58,11 @@ class JsonlMetricsCallback(TrainerCallback):
         opt = getattr(optimizer, "optimizer", optimizer)  # accelerate wraps it
         if opt is not None and hasattr(opt, "stats"):
             rec["lion"] = opt.stats(reset=True)
+        timer = getattr(opt, "phase_timer", None)
+        if timer is not None:
+            # mean ms per optimizer step since the last record: fwd_bwd, clip and
+            # the vote's encode / exchange (exposed comm) / apply, or local_update
+            rec["phase_ms_per_step"] = {k: round(v, 3) for k, v in timer.summary(reset=True).items()}
         os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
         with open(self.path, "a") as f:
             f.write(json.dumps(rec, default=float) + "\n")
