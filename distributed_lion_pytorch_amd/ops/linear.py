@@ -60,18 +60,33 @@ from __future__ import annotations
 import contextlib
 import math
 import os
+import threading
 import weakref
 
 import torch
 
-_FUSE_ACCUM = {"on": False, "multi": True, "nodefer": False}
 _ACC_BUDGET = (8 << 30) if os.environ.get("DLION_SPLITK_ACC", "1") != "0" else 0  # bytes of fp32 accumulators
-_ACC: dict = {}  # key -> [weakrefs of params, fp32 buffer [S, ...], [(param ref, col0, ncols)]]
-_PENDING: list = []  # keys written in the current window, in order
 _WDEFER_ON = os.environ.get("DLION_WGRAD_DEFER", "1") != "0"
-_WDEFER: dict = {}  # key -> [params, cols, [a segments], [b segments], [versions]]
-_WDEFER_BYTES = [0]
 _WDEFER_MAX_SEG = 16  # csrc/gemm_tn.hip kMaxSeg
+
+
+class _FusionState(threading.local):
+    """The fusion window's state, per thread: a window is one thread's
+    optimizer step (two trainers on two threads never share accumulators or
+    kept operands).  Entries are keyed by parameter, so several models
+    trained in one thread's window (e.g. a policy and a trainable second model)
+    keep separate accumulators.  Device memory held here is bounded by
+    ``_ACC_BUDGET`` + ``_wdefer_budget()``, which trainer/memory.py counts."""
+
+    def __init__(self):
+        self.fuse = {"on": False, "multi": True, "nodefer": False}
+        self.acc: dict = {}  # key -> [weakrefs of params, fp32 buffer [S, ...], [(param ref, col0, ncols)]]
+        self.pending: list = []  # keys written in the current window, in order
+        self.wdefer: dict = {}  # key -> [params, cols, [a segments], [b segments], [versions]]
+        self.wdefer_bytes = [0]
+
+
+_ST = _FusionState()
 
 
 @contextlib.contextmanager
@@ -79,55 +94,55 @@ def grad_accumulation_fusion(enabled: bool = True, micro_batches: int | None = N
     """Fusion window = the micro-batches of one optimizer step.  ``micro_batches``
     (if known) gates the split-K accumulators: with one micro-batch they save
     nothing, so the weight gradient is reduced straight into ``param.grad``."""
-    prev = (_FUSE_ACCUM["on"], _FUSE_ACCUM["multi"])
+    prev = (_ST.fuse["on"], _ST.fuse["multi"])
     outer = bool(enabled) and not prev[0]
-    _FUSE_ACCUM["on"] = bool(enabled)
+    _ST.fuse["on"] = bool(enabled)
     if outer:
-        _FUSE_ACCUM["multi"] = micro_batches is None or int(micro_batches) > 1
+        _ST.fuse["multi"] = micro_batches is None or int(micro_batches) > 1
     ok = False
     try:
         yield
         ok = True
     finally:
-        _FUSE_ACCUM["on"], _FUSE_ACCUM["multi"] = prev
+        _ST.fuse["on"], _ST.fuse["multi"] = prev
         if outer:
             if ok:
                 flush_split_k_accumulators()
                 flush_deferred_partials()
-            _PENDING.clear()
+            _ST.pending.clear()
             _clear_deferred()
             _drop_deferred()
-            _FUSE_ACCUM["nodefer"] = False
+            _ST.fuse["nodefer"] = False
 
 
 def begin_fusion_window(micro_batches: int | None = None) -> bool:
     """Non-context form of :func:`grad_accumulation_fusion` for loops that do
     not own the micro-batch iteration (the HF Trainer's ``training_step`` runs
     once per micro-batch).  Returns False if a window is already open."""
-    if _FUSE_ACCUM["on"]:
+    if _ST.fuse["on"]:
         return False
-    _FUSE_ACCUM["on"] = True
-    _FUSE_ACCUM["multi"] = micro_batches is None or int(micro_batches) > 1
+    _ST.fuse["on"] = True
+    _ST.fuse["multi"] = micro_batches is None or int(micro_batches) > 1
     return True
 
 
 def end_fusion_window(flush: bool = True) -> None:
     """Close the window opened by :func:`begin_fusion_window`: every weight
     gradient of the window is in ``param.grad`` afterwards."""
-    if not _FUSE_ACCUM["on"]:
+    if not _ST.fuse["on"]:
         return
-    _FUSE_ACCUM["on"], _FUSE_ACCUM["multi"] = False, True
+    _ST.fuse["on"], _ST.fuse["multi"] = False, True
     if flush:
         flush_split_k_accumulators()
         flush_deferred_partials()
-    _PENDING.clear()
+    _ST.pending.clear()
     _clear_deferred()
     _drop_deferred()
-    _FUSE_ACCUM["nodefer"] = False
+    _ST.fuse["nodefer"] = False
 
 
 def fusion_window_open() -> bool:
-    return bool(_FUSE_ACCUM["on"])
+    return bool(_ST.fuse["on"])
 
 
 def no_wgrad_deferral_this_window() -> None:
@@ -135,8 +150,8 @@ def no_wgrad_deferral_this_window() -> None:
     layer inputs alive until the window's exit would undo the checkpointing's
     memory saving, so this window computes its weight gradients per
     micro-batch (into the fp32 accumulators) instead."""
-    if _FUSE_ACCUM["on"]:
-        _FUSE_ACCUM["nodefer"] = True
+    if _ST.fuse["on"]:
+        _ST.fuse["nodefer"] = True
 
 
 def _flush_entry(ent) -> None:
@@ -161,43 +176,43 @@ def _run_deferred(key) -> None:
     """One TN GEMM over every kept segment of `key` into its accumulator."""
     from . import hip
 
-    params, cols, segs_a, segs_b, vers = _WDEFER.pop(key)
-    _WDEFER_BYTES[0] -= sum(t.numel() * t.element_size() for t in segs_a + segs_b)
+    params, cols, segs_a, segs_b, vers = _ST.wdefer.pop(key)
+    _ST.wdefer_bytes[0] -= sum(t.numel() * t.element_size() for t in segs_a + segs_b)
     for t, v in zip(segs_a + segs_b, vers):
         if t._version != v:
             raise RuntimeError("dlion: an operand kept for a deferred weight gradient was modified in place")
-    ent = _ACC[key]
-    accumulate = key in _PENDING
+    ent = _ST.acc[key]
+    accumulate = key in _ST.pending
     hip.ops().gemm_tn_(segs_a, segs_b, ent[1], accumulate)
     if not accumulate:
-        _PENDING.append(key)
+        _ST.pending.append(key)
 
 
 def _run_all_deferred() -> None:
-    for key in list(_WDEFER):
+    for key in list(_ST.wdefer):
         _run_deferred(key)
 
 
 def _drop_deferred() -> None:
-    _WDEFER.clear()
-    _WDEFER_BYTES[0] = 0
+    _ST.wdefer.clear()
+    _ST.wdefer_bytes[0] = 0
 
 
 def _defer_wgrad(params, cols, a, b, s) -> bool:
     """Keep a^T b's operands for one window-level GEMM (see the module notes).
     False if not applicable (fallback: _acc_gemm now)."""
-    if not (_WDEFER_ON and _FUSE_ACCUM["multi"]) or _FUSE_ACCUM["nodefer"]:
+    if not (_WDEFER_ON and _ST.fuse["multi"]) or _ST.fuse["nodefer"]:
         return False
     key = tuple(id(p) for p in params)
     nb = a.numel() * a.element_size() + b.numel() * b.element_size()
-    ent = _WDEFER.get(key)
+    ent = _ST.wdefer.get(key)
     if ent is not None:
         a0, b0 = ent[2][0], ent[3][0]
         if (a.shape != a0.shape or b.shape != b0.shape or a.stride() != a0.stride() or b.stride() != b0.stride()
                 or any(r() is not p for r, p in zip(ent[0], params))):
             _run_deferred(key)
             ent = None
-    if _WDEFER_BYTES[0] + nb > _wdefer_budget():
+    if _ST.wdefer_bytes[0] + nb > _wdefer_budget():
         if ent is not None:
             _run_deferred(key)
         return False
@@ -205,11 +220,11 @@ def _defer_wgrad(params, cols, a, b, s) -> bool:
         # the accumulator [s, R, C] the window's exit reduces into param.grad
         if not _ensure_acc(params, cols, (s, a.shape[1], b.shape[1]), a.device):
             return False
-        ent = _WDEFER[key] = [[weakref.ref(p) for p in params], cols, [], [], []]
+        ent = _ST.wdefer[key] = [[weakref.ref(p) for p in params], cols, [], [], []]
     ent[2].append(a)
     ent[3].append(b)
     ent[4].extend([a._version, b._version])
-    _WDEFER_BYTES[0] += nb
+    _ST.wdefer_bytes[0] += nb
     if len(ent[2]) == _WDEFER_MAX_SEG:
         _run_deferred(key)
     return True
@@ -219,11 +234,11 @@ def flush_split_k_accumulators() -> None:
     """Reduce every split-K accumulator written in this window into its
     parameters' ``.grad`` (one fused sum + deposit per weight)."""
     _run_all_deferred()
-    for key in _PENDING:
-        ent = _ACC.get(key)
+    for key in _ST.pending:
+        ent = _ST.acc.get(key)
         if ent is not None:
             _flush_entry(ent)
-    _PENDING.clear()
+    _ST.pending.clear()
 
 
 def release_split_k_accumulators() -> None:
@@ -232,32 +247,32 @@ def release_split_k_accumulators() -> None:
     flush_split_k_accumulators()
     flush_deferred_partials()
     _drop_deferred()
-    _ACC.clear()
+    _ST.acc.clear()
 
 
 def _ensure_acc(params, cols, shape, device) -> bool:
     """Make sure the window accumulator of `params` has `shape` (flushing a
     differently shaped one that already holds this window's partials)."""
     key = tuple(id(p) for p in params)
-    ent = _ACC.get(key)
+    ent = _ST.acc.get(key)
     if ent is not None and all(r() is p for r, p in zip(ent[0], params)) and tuple(ent[1].shape) == tuple(shape):
         return True
     if ent is not None:
-        if key in _PENDING:
+        if key in _ST.pending:
             # split factor / token count changed inside the window: the
             # partials so far go into param.grad before the buffer is replaced
             _flush_entry(ent)
-            _PENDING.remove(key)
-        _ACC.pop(key)
-    used = sum(e[1].numel() * 4 for e in _ACC.values() if all(r() is not None for r in e[0]))
-    for k in [k for k, e in _ACC.items() if any(r() is None for r in e[0])]:
-        _ACC.pop(k)  # parameters gone: drop their buffers
-        if k in _PENDING:
-            _PENDING.remove(k)
+            _ST.pending.remove(key)
+        _ST.acc.pop(key)
+    used = sum(e[1].numel() * 4 for e in _ST.acc.values() if all(r() is not None for r in e[0]))
+    for k in [k for k, e in _ST.acc.items() if any(r() is None for r in e[0])]:
+        _ST.acc.pop(k)  # parameters gone: drop their buffers
+        if k in _ST.pending:
+            _ST.pending.remove(k)
     if used + math.prod(shape) * 4 > _ACC_BUDGET:
         return False
     buf = torch.empty(shape, device=device, dtype=torch.float32)
-    _ACC[key] = [[weakref.ref(p) for p in params], buf, [(weakref.ref(p), c0, n) for p, (c0, n) in zip(params, cols)]]
+    _ST.acc[key] = [[weakref.ref(p) for p in params], buf, [(weakref.ref(p), c0, n) for p, (c0, n) in zip(params, cols)]]
     return True
 
 
@@ -267,18 +282,18 @@ def _acc_gemm(params, cols, a, b, s) -> bool:
     `cols` of the flattened R*C).  False if the buffer cannot be used (over
     budget, single-micro-batch window): the caller then deposits into
     ``param.grad`` directly, on top of any flushed partials."""
-    if not _FUSE_ACCUM["multi"]:
+    if not _ST.fuse["multi"]:
         return False
     key = tuple(id(p) for p in params)
-    if key in _WDEFER:
+    if key in _ST.wdefer:
         _run_deferred(key)  # keep the micro-batch order of the accumulation simple
     if not _ensure_acc(params, cols, (s, a.shape[1], b.shape[1]), a.device):
         return False
-    ent = _ACC[key]
-    accumulate = key in _PENDING
+    ent = _ST.acc[key]
+    accumulate = key in _ST.pending
     wgrad_partials(a, b, s, out=ent[1], accumulate=accumulate)
     if not accumulate:
-        _PENDING.append(key)
+        _ST.pending.append(key)
     return True
 
 
@@ -331,7 +346,7 @@ def wgrad_splits(a: torch.Tensor, b: torch.Tensor) -> tuple:
     M, R, C = a.shape[0], a.shape[1], b.shape[1]
     # small outputs: hipBLASLt per micro-batch, but the own kernel when the
     # window defers the GEMM (attn c_proj over 8 micro-batches: 29 vs 43 us/mb)
-    deferred = _WDEFER_ON and _FUSE_ACCUM["on"] and _FUSE_ACCUM["multi"] and not _FUSE_ACCUM["nodefer"]
+    deferred = _WDEFER_ON and _ST.fuse["on"] and _ST.fuse["multi"] and not _ST.fuse["nodefer"]
     if ((deferred or math.ceil(R / 256) * math.ceil(C / 256) >= _TN_MIN_TILES) and _tn_eligible(a, b)
             and hip.available()):
         return tn_split_factor(M, R, C), True
@@ -364,7 +379,7 @@ def wgrad_partials(a: torch.Tensor, b: torch.Tensor, s: int, out=None, accumulat
 
 
 def _fuse_target(w) -> bool:
-    return (_FUSE_ACCUM["on"] and isinstance(w, torch.nn.Parameter) and w.requires_grad and w.is_cuda
+    return (_ST.fuse["on"] and isinstance(w, torch.nn.Parameter) and w.requires_grad and w.is_cuda
             and w.dtype == torch.bfloat16 and w.is_contiguous())
 
 
@@ -388,7 +403,7 @@ def defer_partials(key, part2d: torch.Tensor, fn) -> bool:
     """Keep ``part2d`` for ``fn(concatenated stacks)`` at the window's end.
     False (nothing kept) outside a multi-micro-batch window or over budget:
     the caller then deposits now."""
-    if not (_DEFER_ON and _FUSE_ACCUM["on"] and _FUSE_ACCUM["multi"]):
+    if not (_DEFER_ON and _ST.fuse["on"] and _ST.fuse["multi"]):
         return False
     nb = part2d.numel() * part2d.element_size()
     if nb > _DEFER_MAX_PART or _DEFER_BYTES[0] + nb > _DEFER_CAP:
@@ -541,7 +556,7 @@ def wgrad_into(a: torch.Tensor, b: torch.Tensor, w: torch.nn.Parameter) -> None:
         from . import hip
 
         if hip.available():
-            if _FUSE_ACCUM["on"] and ((own and _defer_wgrad([w], [(0, K * N)], a, b, s))
+            if _ST.fuse["on"] and ((own and _defer_wgrad([w], [(0, K * N)], a, b, s))
                                       or _acc_gemm([w], [(0, K * N)], a, b, s)):
                 return  # reduced into w.grad when the accumulation window closes
             g = w.grad  # _acc_gemm may have flushed earlier partials into it
@@ -957,7 +972,7 @@ def _multi_wgrad_into(dy, x2d, params, sizes) -> None:
             for n in sizes:
                 cols.append((off * K, n * K))
                 off += n
-            if _FUSE_ACCUM["on"] and ((own and _defer_wgrad(list(params), cols, dy, x2d, s))
+            if _ST.fuse["on"] and ((own and _defer_wgrad(list(params), cols, dy, x2d, s))
                                       or _acc_gemm(list(params), cols, dy, x2d, s)):
                 return  # reduced into each params[i].grad when the window closes
             if own and s == 1 and all(p.dtype == torch.bfloat16 for p in params):

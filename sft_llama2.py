@@ -93,6 +93,11 @@ def load_samples(script_args, seed):
 
 
 def create_datasets(tokenizer, script_args, seed):
+    if script_args.streaming:
+        # the reference streams the hub dataset (sft_llama2.py:100-112); offline the rows come from a
+        # local json/jsonl file or the synthetic generator and are packed up front in host memory
+        logger.warning("--streaming has no effect offline: the samples are read from a local file (or generated) "
+                       "and packed in host memory; pass --streaming false to silence this")
     rows = load_samples(script_args, seed)
     n_valid = min(script_args.size_valid_set, max(1, len(rows) // 20))
     train_rows, valid_rows = rows[n_valid:], rows[:n_valid]

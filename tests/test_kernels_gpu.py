@@ -115,8 +115,8 @@ def test_vote_apply_kernel_fake_voters(dtype, world, mode, tie, cuda):
     p2 = _clone(ps)
     hx, tx = HipExecutor(plan), TorchExecutor(plan)
     meta = plan.meta(gs, ms)
-    agree = torch.zeros(1, dtype=torch.int64, device=cuda)
-    agree_t = torch.zeros(1, dtype=torch.int64, device=cuda)
+    agree = torch.zeros(2, dtype=torch.int64, device=cuda)  # [agreements, ties]
+    agree_t = torch.zeros(2, dtype=torch.int64, device=cuda)
     for b in plan.buckets:
         pl = planes[world * b.byte_off: world * (b.byte_off + b.nbytes)]
         own = pl[: b.nbytes]
@@ -127,7 +127,9 @@ def test_vote_apply_kernel_fake_voters(dtype, world, mode, tie, cuda):
     torch.cuda.synchronize()
     for a, b in zip(ps, p2):
         _assert_close(a, b, dtype, exact=mode != ref.VOTE_AVERAGE)
-    assert agree.item() == agree_t.item()
+    assert agree.tolist() == agree_t.tolist()
+    if mode == ref.VOTE_MAJORITY and world in (2, 3):  # an even live count (alive[1] = 0 for W > 2)
+        assert agree[1].item() > 0  # even live count: random planes tie somewhere
 
 
 def _rebind(bucket, new_params, plan):
@@ -152,10 +154,14 @@ def test_vote_reduce_and_prevoted_apply(world, tie, cuda):
     for ex in (_bare_hip(), TorchExecutor.__new__(TorchExecutor)):
         pos = torch.zeros(nbytes, dtype=torch.uint8, device=cuda)
         neg = torch.zeros(nbytes, dtype=torch.uint8, device=cuda)
-        ex.vote_reduce(recv, nbytes, alive, tie, pos, neg)
-        outs.append((pos, neg))
+        ties = torch.zeros(1, dtype=torch.int64, device=cuda)
+        ex.vote_reduce(recv, nbytes, alive, tie, pos, neg, ties)
+        outs.append((pos, neg, ties))
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    # tie telemetry (K4 under a2a): identical counts, non-zero exactly for an even live count
+    assert outs[0][2].item() == outs[1][2].item()
+    assert (outs[0][2].item() > 0) == ((world - 1) % 2 == 0)
 
 
 def _bare_hip():

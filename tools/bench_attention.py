@@ -52,12 +52,16 @@ def main():
         with torch.no_grad():
             sdpa(False)
 
+    only_ours = os.environ.get("DLION_BENCH_OURS_ONLY") == "1"  # PMC passes: our kernels only
     for _ in range(5):
         res["ours_fwd"].append(timeit(ours_fwd))
-        res["sdpa_fwd"].append(timeit(sdpa_fwd))
         res["ours_fb"].append(timeit(ours_fb))
-        res["sdpa_fb"].append(timeit(lambda: sdpa(True)))
+        if not only_ours:
+            res["sdpa_fwd"].append(timeit(sdpa_fwd))
+            res["sdpa_fb"].append(timeit(lambda: sdpa(True)))
     for k, v in res.items():
+        if not v:
+            continue
         ms = statistics.median(v)
         fl = flops_f if k.endswith("fwd") else 3.5 * flops_f
         print(f"{k:10s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TFLOP/s")
