@@ -102,6 +102,8 @@ def parse():
     ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"],
                     help="auto: cuda when a GPU is visible (cpu + gloo: plumbing rehearsal of the multi-rank path)")
     ap.add_argument("--no_phase_times", action="store_true", help="do not record per-phase HIP events")
+    ap.add_argument("--elastic_timeout", type=float, default=None,
+                    help="run the vote as guarded, store-committed collectives (worker-dropout mode) to measure its cost")
     ap.add_argument("--data", default="random", choices=["random", "markov"],
                     help="random token ids (throughput) | a learnable Markov-chain corpus (learning curves)")
     ap.add_argument("--loss_log", default=None,
@@ -193,6 +195,8 @@ def setup_dist(args):
         if args.backend == "nccl":
             for k, v in RCCL_ENV_DEFAULTS.items():
                 os.environ.setdefault(k, v)
+            if args.elastic_timeout is not None:  # the elastic path aborts communicators itself
+                os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
             dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -241,7 +245,7 @@ def build_native(args, dev):
         model.gradient_checkpointing_enable()
     broadcast_parameters(model)
     opt = Lion([p for p in model.parameters() if p.requires_grad], lr=args.lr, weight_decay=args.weight_decay,
-               exchange=args.exchange, bucket_mb=args.bucket_mb)
+               exchange=args.exchange, bucket_mb=args.bucket_mb, elastic_timeout=args.elastic_timeout)
     args.ref_model = ref_model  # not a submodule: stays out of the parameter counts
     return model, opt, cfg
 
@@ -454,6 +458,7 @@ def main():
                 "optimizer": f"distributed Lion (majority vote), lr {args.lr:g}, wd {args.weight_decay:g}",
                 "exchange": exchange,
                 "impl": args.impl,
+                "elastic_timeout": args.elastic_timeout,
             },
             "wire_bytes_per_step_per_rank": wire_meas["wire_bytes_sent"] if world > 1 else 0,
             "wire_bytes_per_step_per_rank_measured": wire_meas,

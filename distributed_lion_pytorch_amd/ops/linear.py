@@ -60,7 +60,6 @@ from __future__ import annotations
 import contextlib
 import math
 import os
-import threading
 import weakref
 
 import torch
@@ -70,13 +69,15 @@ _WDEFER_ON = os.environ.get("DLION_WGRAD_DEFER", "1") != "0"
 _WDEFER_MAX_SEG = 16  # csrc/gemm_tn.hip kMaxSeg
 
 
-class _FusionState(threading.local):
-    """The fusion window's state, per thread: a window is one thread's
-    optimizer step (two trainers on two threads never share accumulators or
-    kept operands).  Entries are keyed by parameter, so several models
-    trained in one thread's window (e.g. a policy and a trainable second model)
-    keep separate accumulators.  Device memory held here is bounded by
-    ``_ACC_BUDGET`` + ``_wdefer_budget()``, which trainer/memory.py counts."""
+class _FusionState:
+    """The fusion window's state -- process-wide on purpose: PyTorch runs the
+    CUDA backward on its own per-device autograd thread, so a window opened by
+    the training loop's thread must be visible there (a thread-local copy
+    deposited every micro-batch immediately).  Entries are keyed by parameter,
+    so several models trained in one window (e.g. a policy and a trainable
+    second model) keep separate accumulators; one training loop per process
+    owns the window.  Device memory held here is bounded by ``_ACC_BUDGET`` +
+    ``_wdefer_budget()``, which trainer/memory.py counts."""
 
     def __init__(self):
         self.fuse = {"on": False, "multi": True, "nodefer": False}
