@@ -56,9 +56,9 @@ def test_window_wgrad_deferral(cuda, monkeypatch, defer):
     with L.grad_accumulation_fusion(True, micro_batches=mbs):
         for x, g in zip(xs, gs):
             L.wgrad_into(x, g, w)
-        assert bool(L._WDEFER) == defer
+        assert bool(L._ST.wdefer) == defer
         assert w.grad is None  # nothing reduced before the window closes
-    assert not L._WDEFER
+    assert not L._ST.wdefer
     ref = sum(x.float().t() @ g.float() for x, g in zip(xs, gs))
     err = (w.grad.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 8e-3, err
@@ -88,7 +88,7 @@ def test_window_wgrad_deferral_edge_cases(cuda, monkeypatch, case):
     with L.grad_accumulation_fusion(True, micro_batches=len(Ms)):
         for x, g in zip(xs, gs):
             L.wgrad_into(x, g, w)
-    assert not L._WDEFER
+    assert not L._ST.wdefer
     ref = sum(x.float().t() @ g.float() for x, g in zip(xs, gs))
     err = (w.grad.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 8e-3, err

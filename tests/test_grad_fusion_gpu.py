@@ -61,8 +61,8 @@ def test_split_k_accumulator_window(cuda, monkeypatch):
             y = L.linear_nk(x, w)
             y.backward(dy)
             assert w.grad is None, "deposit must wait for the end of the window"
-            assert len(L._PENDING) == 1
-    assert not L._PENDING
+            assert len(L._ST.pending) == 1
+    assert not L._ST.pending
     ref = sum(dy.float().t() @ x.float() for x, dy in zip(xs, dys))
     err = (w.grad.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 8e-3, err
@@ -112,8 +112,8 @@ def test_split_k_window_edge_cases(case, cuda, monkeypatch):
             else:
                 L.linear_nk(x, w).backward(dy)
         if case == "single_micro_batch":
-            assert not L._PENDING and w.grad is not None
-    assert not L._PENDING
+            assert not L._ST.pending and w.grad is not None
+    assert not L._ST.pending
     ref = _window_ref(steps)
     if case == "shared_weight":
         ref2 = ref.clone()
@@ -123,4 +123,4 @@ def test_split_k_window_edge_cases(case, cuda, monkeypatch):
     err = (w.grad.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 8e-3, (case, err)
     L.release_split_k_accumulators()
-    assert not L._ACC
+    assert not L._ST.acc
