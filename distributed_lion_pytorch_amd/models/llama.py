@@ -69,13 +69,23 @@ def _rope_theta(cfg) -> float:
 
 
 class Rotary(nn.Module):
-    """cos/sin tables computed once per (T, device, dtype) -- no per-step trig."""
+    """cos/sin tables computed once per (T, device, dtype) -- no per-step trig.
+
+    The inverse frequencies are NOT a module buffer: ``model.to(bfloat16)``
+    would round them to bf16 (0.4 % relative), and at position ~1000 that is
+    an angle error of several radians -- the bf16 training path had
+    effectively scrambled positions for the high-frequency pairs (caught by
+    tests/test_parity_full_gpu.py against HF fp32).  They are computed in fp32
+    exactly as HF's LlamaRotaryEmbedding does, at table-build time."""
 
     def __init__(self, head_dim: int, theta: float):
         super().__init__()
-        inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
-        self.register_buffer("inv_freq", inv.float(), persistent=False)
+        self.head_dim, self.theta = int(head_dim), float(theta)
         self._cache = {}
+
+    @property
+    def inv_freq(self) -> torch.Tensor:
+        return 1.0 / (self.theta ** (torch.arange(0, self.head_dim, 2, dtype=torch.int64).float() / self.head_dim))
 
     def tables(self, T: int, device, dtype):
         key = (T, device, dtype)

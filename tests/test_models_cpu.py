@@ -131,3 +131,19 @@ def test_token_logps_matches_log_softmax_cpu():
     h.grad = w.grad = None
     ref.sum(-1).mul(g).sum().backward()
     assert torch.allclose(gh, h.grad, atol=1e-4) and torch.allclose(gw, w.grad, atol=1e-4)
+
+
+def test_rope_frequencies_stay_fp32_under_bf16_cast():
+    """model.to(bfloat16) must not round the RoPE inverse frequencies (they were
+    a module buffer: at position ~1000 the bf16 rounding is an angle error of
+    radians).  The tables equal HF LlamaRotaryEmbedding's fp32 ones exactly."""
+    from transformers.models.llama.modeling_llama import LlamaRotaryEmbedding
+
+    from distributed_lion_pytorch_amd.models.llama import LlamaForCausalLM, llama_config
+
+    cfg = llama_config("llama-tiny", max_position_embeddings=4096)
+    m = LlamaForCausalLM(cfg).to(torch.bfloat16)
+    cos, sin = m.model.rotary.tables(2048, torch.device("cpu"), torch.float32)
+    hf = LlamaRotaryEmbedding(config=cfg)
+    hc, hs = hf(torch.zeros(1, dtype=torch.float32), torch.arange(2048)[None])
+    assert torch.equal(cos, hc[0]) and torch.equal(sin, hs[0])
