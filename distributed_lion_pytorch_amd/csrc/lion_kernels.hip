@@ -427,20 +427,20 @@ lion_vote_apply32_kernel(const int64_t* __restrict__ seg, const int64_t* __restr
         nw[it] = neg_plane ? reinterpret_cast<const uint32_t*>(neg_plane)[word] : ~pw[it];
       }
     } else {
-      uint32_t w[kIters][kMaxSliced];
+      // majority over W planes: hoisting every plane word of all 4 iterations
+      // (4 x 15 registers behind a runtime live mask) spilled and ran at 21 %
+      // of HBM; only the p loads are hoisted here, the plane words of each
+      // iteration are loaded and voted on per iteration (the byte-light part)
+#pragma unroll
+      for (int it = 0; it < kIters; ++it) rp[it].load(p + start + it * kSpan + threadIdx.x * 8);
 #pragma unroll
       for (int it = 0; it < kIters; ++it) {
-        const int64_t e = start + it * kSpan + threadIdx.x * 8;
-        const int64_t word = (r.bit_off + e) >> 5;
-        rp[it].load(p + e);
+        const int64_t word = (r.bit_off + start + it * kSpan + threadIdx.x * 8) >> 5;
+        uint32_t w[kMaxSliced], tb;
 #pragma unroll
         for (int k = 0; k < kMaxSliced; ++k)
-          w[it][k] = (live_mask >> k) & 1 ? reinterpret_cast<const uint32_t*>(planes + k * plane_stride)[word] : 0u;
-      }
-#pragma unroll
-      for (int it = 0; it < kIters; ++it) {
-        uint32_t tb;
-        sliced_vote(w[it], world, n_live, tie, pw[it], nw[it], tb);
+          w[k] = (live_mask >> k) & 1 ? reinterpret_cast<const uint32_t*>(planes + k * plane_stride)[word] : 0u;
+        sliced_vote(w, world, n_live, tie, pw[it], nw[it], tb);
       }
     }
 #pragma unroll
@@ -508,6 +508,9 @@ lion_vote_apply32_kernel(const int64_t* __restrict__ seg, const int64_t* __restr
 // recv: [W][nbytes] shards gathered by all_to_all; out: voted positive bits;
 // neg_out (optional): voted negative bits (only needed when ties map to 0).
 // 4 bytes (32 coordinates) per thread, grid-stride.
+// SLICED (W <= 15) and the byte-spread path are separate instantiations: the
+// byte path's 32 counters would otherwise set the register budget of both
+template <bool SLICED>
 __global__ void __launch_bounds__(kThreads)
 vote_reduce_kernel(const uint8_t* __restrict__ recv, int64_t nbytes, const uint8_t* __restrict__ alive,
                    int world, int tie, uint8_t* __restrict__ out, uint8_t* __restrict__ neg_out,
@@ -516,33 +519,11 @@ vote_reduce_kernel(const uint8_t* __restrict__ recv, int64_t nbytes, const uint8
   int n_live = 0;
   for (int k = 0; k < world; ++k) n_live += alive[k] != 0;
   uint32_t n_tie = 0;  // tie-rate telemetry (ties != nullptr)
-  if (world <= kMaxSliced) {  // bit-sliced counters, every plane word loaded up front
+  if constexpr (SLICED) {  // bit-sliced counters, every plane word loaded up front
     uint32_t live_mask = 0;
     for (int k = 0; k < world; ++k) live_mask |= static_cast<uint32_t>(alive[k] != 0) << k;
-    // 16 bytes per plane per thread (one dwordx4 load per plane, 4 KiB per
-    // wave instruction): the dword version left the kernel at 40 % of HBM
-    const bool v16 = (nbytes & 15) == 0 && (reinterpret_cast<uintptr_t>(recv) & 15) == 0 &&
-                     (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
-                     (neg_out == nullptr || (reinterpret_cast<uintptr_t>(neg_out) & 15) == 0);
-    const int64_t nq = v16 ? nwords >> 2 : 0;
-    for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < nq; i += (int64_t)gridDim.x * kThreads) {
-      uint4 v[kMaxSliced];
-#pragma unroll
-      for (int k = 0; k < kMaxSliced; ++k)
-        v[k] = (live_mask >> k) & 1 ? reinterpret_cast<const uint4*>(recv + k * nbytes)[i] : make_uint4(0, 0, 0, 0);
-      uint32_t pos[4], ng[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        uint32_t x[kMaxSliced], tb;
-#pragma unroll
-        for (int k = 0; k < kMaxSliced; ++k) x[k] = c == 0 ? v[k].x : c == 1 ? v[k].y : c == 2 ? v[k].z : v[k].w;
-        sliced_vote(x, world, n_live, tie, pos[c], ng[c], tb);
-        n_tie += __popc(tb);
-      }
-      reinterpret_cast<uint4*>(out)[i] = make_uint4(pos[0], pos[1], pos[2], pos[3]);
-      if (neg_out != nullptr) reinterpret_cast<uint4*>(neg_out)[i] = make_uint4(ng[0], ng[1], ng[2], ng[3]);
-    }
-    for (int64_t w = 4 * nq + blockIdx.x * (int64_t)kThreads + threadIdx.x; w < nwords;
+    // (a 16-byte-per-plane variant measured slower: 31 vs 40 % of HBM at Llama-3-8B)
+    for (int64_t w = blockIdx.x * (int64_t)kThreads + threadIdx.x; w < nwords;
          w += (int64_t)gridDim.x * kThreads) {
       uint32_t v[kMaxSliced];
 #pragma unroll
@@ -730,8 +711,12 @@ hipError_t launch_vote_reduce(const uint8_t* recv, int64_t nbytes, const uint8_t
   if (nwords == 0) return hipSuccess;
   int64_t blocks = (nwords + kThreads - 1) / kThreads;
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(vote_reduce_kernel, dim3(blocks), dim3(kThreads), 0, st, recv, nbytes, alive, world, tie,
-                     out, neg_out, ties);
+  if (world <= kMaxSliced)
+    hipLaunchKernelGGL(vote_reduce_kernel<true>, dim3(blocks), dim3(kThreads), 0, st, recv, nbytes, alive, world, tie,
+                       out, neg_out, ties);
+  else
+    hipLaunchKernelGGL(vote_reduce_kernel<false>, dim3(blocks), dim3(kThreads), 0, st, recv, nbytes, alive, world,
+                       tie, out, neg_out, ties);
   return hipGetLastError();
 }
 
