@@ -86,9 +86,9 @@ def _digest(src: Path, flags) -> str:
     return h.hexdigest()[:16]
 
 
-def _compile(src: Path, flags, verbose: bool, force: bool) -> Path:
-    obj = BUILD_DIR / (src.name + ".o")
-    stamp = BUILD_DIR / (src.name + ".sha")
+def _compile(src: Path, flags, verbose: bool, force: bool, bdir: Path = BUILD_DIR) -> Path:
+    obj = bdir / (src.name + ".o")
+    stamp = bdir / (src.name + ".sha")
     flags = flags + EXTRA_FLAGS.get(src.name, [])
     dig = _digest(src, flags)
     if not force and obj.exists() and stamp.exists() and stamp.read_text() == dig:
@@ -106,19 +106,27 @@ def _compile(src: Path, flags, verbose: bool, force: bool) -> Path:
     return obj
 
 
-def build(verbose: bool = False, force: bool = False) -> Path:
-    """Compile every HIP/C++ source in csrc/ for gfx950 and link _dlion_C.so."""
-    BUILD_DIR.mkdir(parents=True, exist_ok=True)
-    flags = _flags()
+def build(verbose: bool = False, force: bool = False, defines=(), out: Path | None = None) -> Path:
+    """Compile every HIP/C++ source in csrc/ for gfx950 and link _dlion_C.so.
+
+    ``defines`` (``NAME=VALUE`` strings) and ``out`` build a variant of the
+    extension (tuning macros, e.g. ``DLION_DKV_WAVES128=1``) into its own
+    object directory and shared object, loadable with ``DLION_LIB=<out>``."""
+    out = Path(out) if out else LIB_PATH
+    bdir = BUILD_DIR
+    flags = _flags() + [f"-D{d}" for d in defines]
+    if defines or out != LIB_PATH:
+        bdir = BUILD_DIR.parent / ("dlion_C-" + hashlib.sha256(" ".join(defines).encode()).hexdigest()[:8])
+    bdir.mkdir(parents=True, exist_ok=True)
     srcs = _sources()
     jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", "8"))))
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, flags, verbose, force), srcs))
+        objs = list(ex.map(lambda s: _compile(s, flags, verbose, force, bdir), srcs))
     _, lib, _ = _torch_paths()
     newest = max(o.stat().st_mtime for o in objs)
-    if not force and LIB_PATH.exists() and LIB_PATH.stat().st_mtime >= newest:
-        return LIB_PATH
-    tmp = LIB_PATH.with_suffix(".so.tmp")
+    if not force and out.exists() and out.stat().st_mtime >= newest:
+        return out
+    tmp = out.with_suffix(".so.tmp")
     cmd = (
         [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}"]
         + [str(o) for o in objs]
@@ -129,10 +137,17 @@ def build(verbose: bool = False, force: bool = False) -> Path:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":
-    out = build(verbose="-v" in sys.argv, force="--force" in sys.argv)
-    print(out)
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-v", action="store_true")
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--define", "-D", action="append", default=[], help="NAME=VALUE macro for a variant build")
+    ap.add_argument("--out", default=None, help="shared object path for a variant build")
+    a = ap.parse_args()
+    print(build(verbose=a.v, force=a.force, defines=tuple(a.define), out=a.out))

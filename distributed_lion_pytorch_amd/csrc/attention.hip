@@ -30,6 +30,20 @@
 #include "common.h"
 #include "attention.h"
 
+// Occupancy floors (waves per SIMD), A/B-measured (profiles/r3/attn_occupancy_ab.txt):
+// dK/dV D=64 at 3 waves fits 168 VGPRs without spills and is ~4 % faster over
+// fwd+bwd; forcing dQ D=64 to 4 waves (128 VGPRs, 12 dwords of spill) or
+// dK/dV D=128 to 2 waves (~30 dwords of spill) does not pay.
+#ifndef DLION_DKV_WAVES64
+#define DLION_DKV_WAVES64 3
+#endif
+#ifndef DLION_DQ_WAVES64
+#define DLION_DQ_WAVES64 1
+#endif
+#ifndef DLION_DKV_WAVES128
+#define DLION_DKV_WAVES128 1
+#endif
+
 namespace dlion {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -373,7 +387,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 
 // --------------------------------------------------------------- backward dQ
 template <int D, bool DROP>
-__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? DLION_DQ_WAVES64 : 1)))
+attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[2];
   __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[2];
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
@@ -498,7 +513,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
 // every head in the GQA group is staged once per block (Q, dO and the 32
 // lse / delta values).  Low key groups (most query tiles) go first.
 template <int D, bool DROP>
-__global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? DLION_DKV_WAVES64 : DLION_DKV_WAVES128)))
+attn_bwd_dkv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) LdsTile<D> qs_[2];
   __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[2];
   __shared__ __attribute__((aligned(16))) float ls_[2][3][32];  // [buf][lse | delta | drop row key][row]
@@ -566,21 +582,6 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
         s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), kf[ks], s);   // S  = Q K^T : rows q, cols key
         dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), vf[ks], dp);  // dP = dO V^T
       }
-      // row statistics of the lane's 16 query rows: rows (reg&3) + 8(reg>>2) + 4hf
-      // come in 4 runs of 4 consecutive rows -> 16-byte LDS reads (broadcast)
-      float lse_r[16], dl_r[16];
-      uint32_t ar_r[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 lv = *reinterpret_cast<const float4*>(&ls_[buf][0][8 * g + 4 * hf]);
-        const float4 dv4 = *reinterpret_cast<const float4*>(&ls_[buf][1][8 * g + 4 * hf]);
-        lse_r[4 * g] = lv.x; lse_r[4 * g + 1] = lv.y; lse_r[4 * g + 2] = lv.z; lse_r[4 * g + 3] = lv.w;
-        dl_r[4 * g] = dv4.x; dl_r[4 * g + 1] = dv4.y; dl_r[4 * g + 2] = dv4.z; dl_r[4 * g + 3] = dv4.w;
-        if constexpr (DROP) {
-          const uint4 av = *reinterpret_cast<const uint4*>(&ls_[buf][2][8 * g + 4 * hf]);
-          ar_r[4 * g] = av.x; ar_r[4 * g + 1] = av.y; ar_r[4 * g + 2] = av.z; ar_r[4 * g + 3] = av.w;
-        }
-      }
       if (qt == ktile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg)
@@ -591,20 +592,35 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
         for (int reg = 0; reg < 16; ++reg)
           if (qb + acc_row(reg, hf) >= a.T) s[reg] = -INFINITY;
       }
+      // row statistics of the lane's 16 query rows: rows (reg&3) + 8(reg>>2) + 4hf
+      // come in 4 runs of 4 consecutive rows -> 16-byte LDS reads (broadcast),
+      // consumed run by run (not all 48 values staged up front: that held the
+      // kernel at 212 VGPRs, two waves per SIMD)
       f32x16 pd;
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -lse_r[reg]));
-        float dpv = dp[reg];
-        float pdv = p;
-        if constexpr (DROP) {  // the lane is the key here: one (cheap) hash per element;
-                               // p and the delta row values already carry 1/(1-p)
-          const bool kp_ = (mix1(ar_r[reg] ^ kmix) << kshift) >= thr_hi;
-          dpv = kp_ ? dpv : 0.f;
-          pdv = kp_ ? p : 0.f;
+      for (int g = 0; g < 4; ++g) {
+        const float4 lv = *reinterpret_cast<const float4*>(&ls_[buf][0][8 * g + 4 * hf]);
+        const float4 dv4 = *reinterpret_cast<const float4*>(&ls_[buf][1][8 * g + 4 * hf]);
+        uint4 av = make_uint4(0, 0, 0, 0);
+        if constexpr (DROP) av = *reinterpret_cast<const uint4*>(&ls_[buf][2][8 * g + 4 * hf]);
+        const float lse_g[4] = {lv.x, lv.y, lv.z, lv.w};
+        const float dl_g[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
+        const uint32_t ar_g[4] = {av.x, av.y, av.z, av.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int reg = 4 * g + i;
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -lse_g[i]));
+          float dpv = dp[reg];
+          float pdv = p;
+          if constexpr (DROP) {  // the lane is the key here: one (cheap) hash per element;
+                                 // p and the delta row values already carry 1/(1-p)
+            const bool kp_ = (mix1(ar_g[i] ^ kmix) << kshift) >= thr_hi;
+            dpv = kp_ ? dpv : 0.f;
+            pdv = kp_ ? p : 0.f;
+          }
+          pd[reg] = pdv;
+          s[reg] = p * (dpv - dl_g[i]);  // dS
         }
-        pd[reg] = pdv;
-        s[reg] = p * (dpv - dl_r[reg]);  // dS
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {

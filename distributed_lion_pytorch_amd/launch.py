@@ -15,7 +15,9 @@ failure -- the opposite of the worker-dropout robustness the reference claims
 * exports RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR /
   MASTER_PORT (127.0.0.1) like torchrun;
 * tolerates up to ``--max_failures`` ranks dying (any exit status, signals
-  included); beyond that it terminates the remaining ranks.  Exit status: 0
+  included) and posts a death notice (``dlion/dead/<rank>``) in the store for
+  each, so the survivors regroup without waiting out a deadline; beyond that
+  it terminates the remaining ranks.  Exit status: 0
   when every other rank exited 0, else the first non-tolerated failure's.
 
 It never touches the GPU (children are fresh interpreters; nothing is forked
@@ -33,6 +35,10 @@ import subprocess
 import sys
 import time
 from typing import List, Optional, Sequence
+
+
+DEATH_KEY = "dlion/dead"  # parallel/elastic.py reads these (kept in sync by test_elastic_cpu)
+DEATH_COUNT_KEY = "dlion/dead_count"
 
 
 def _free_port(host: str) -> int:
@@ -72,6 +78,9 @@ def run(cmd: Sequence[str], nproc: int, max_failures: int = 0, host: str = "127.
             codes[r] = c
             if c != 0:
                 failed.append(r)
+                # death notice for parallel/elastic.py: survivors stop waiting for r at once
+                store.set(f"{DEATH_KEY}/{r}", str(c))
+                store.add(DEATH_COUNT_KEY, 1)
                 if len(failed) > max_failures and rc == 0:
                     rc = c if c > 0 else 128 - c
                     print(f"launch: rank {r} exited with {c} ({len(failed)} failures > {max_failures} tolerated); "

@@ -14,7 +14,8 @@ from pathlib import Path
 
 import torch
 
-LIB_PATH = Path(__file__).resolve().parent.parent / "_dlion_C.so"
+# DLION_LIB points at an alternative build of the same extension (kernel A/B runs)
+LIB_PATH = Path(os.environ.get("DLION_LIB") or Path(__file__).resolve().parent.parent / "_dlion_C.so")
 
 DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 

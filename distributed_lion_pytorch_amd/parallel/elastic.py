@@ -25,8 +25,11 @@ Protocol (all ranks run the same sequence of *guarded* collectives):
    writes ``all``.  ``compare_set`` makes the first written decision final, so
    every survivor acts on the same outcome (apply the step, or regroup).
 3. **Membership.**  After a ``fail`` every live rank checks in under
-   ``<gen>/members``; after ``grace_s`` the first proposal of the ranks seen is
-   the new member list for everybody.  A rank left out (it was only late)
+   ``<gen>/members``; once every member has checked in or is known dead (the
+   launcher posts a death notice when a rank's process exits with an error),
+   or after ``grace_s``, the first proposal of the ranks seen is the new
+   member list for everybody.  Death notices also end the bounded wait of
+   step 1 and the commit wait of step 2 at once.  A rank left out (it was only late)
    raises :class:`WorkerExcluded`.
 4. **Regroup.**  Every process group of the process is aborted
    (``ncclCommAbort`` under RCCL -- it stops the spinning kernels; gloo's abort
@@ -45,6 +48,7 @@ rank (``ElasticGroup.me``).
 """
 from __future__ import annotations
 
+import atexit
 import datetime
 import json
 import logging
@@ -59,6 +63,8 @@ import torch.distributed as dist
 log = logging.getLogger(__name__)
 
 DEFAULT_GRACE_S = 5.0
+DEATH_KEY = "dlion/dead"  # + "/<rank>", in the root rendezvous store (written by ..launch)
+DEATH_COUNT_KEY = "dlion/dead_count"
 
 
 class WorkerExcluded(RuntimeError):
@@ -72,13 +78,22 @@ def _default_store():
 
 
 _GRAVEYARD: list = []  # aborted gloo groups: keep them referenced so no destructor blocks the caller
+_ABORTS: List[threading.Thread] = []
 
 
 def _quiet_abort(pg) -> None:
-    try:
-        pg.abort()
-    except Exception:  # noqa: BLE001 - best effort on a broken group
-        pass
+    for fn in (pg.abort, pg.shutdown):  # shutdown also closes the pairs' sockets
+        try:
+            fn()
+        except Exception:  # noqa: BLE001 - best effort on a broken group
+            pass
+
+
+@atexit.register
+def _drain_graveyard() -> None:
+    """At exit: let the off-thread aborts of the old gloo groups finish."""
+    for t in _ABORTS:
+        t.join(timeout=10.0)
 
 
 def discard_process_groups(backend: str) -> None:
@@ -98,7 +113,9 @@ def discard_process_groups(backend: str) -> None:
     w = c10d._world
     for pg in list(w.pg_names):
         _GRAVEYARD.append(pg)
-        threading.Thread(target=_quiet_abort, args=(pg,), daemon=True).start()
+        t = threading.Thread(target=_quiet_abort, args=(pg,), daemon=True)
+        t.start()
+        _ABORTS.append(t)
     c10d._update_default_pg(None)
     for m in (w.pg_map, w.pg_names, w.pg_group_ranks, w.pg_backend_config, w.pg_to_tag, w.tags_to_pg,
               w.pg_coalesce_state):
@@ -140,6 +157,20 @@ class ElasticGroup:
         self.pg_timeout = datetime.timedelta(seconds=max(600.0, 10.0 * self.timeout))
         self.device = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else None
         self._pg = dist.group.WORLD
+        # death notices: the failure-tolerant launcher (..launch) writes
+        # ``dlion/dead/<rank>`` into the root store when a rank's process exits
+        # with an error, so a dead peer is cut out at once instead of after the
+        # deadline (an RCCL collective on a dead peer spins until aborted)
+        root = self.store
+        while isinstance(root, PrefixStore):
+            root = root.underlying_store
+        self._root = root
+        self._dead: set = set()
+        self._dead_count = 0
+        # gloo completes a collective with an error as soon as a peer's socket
+        # closes (abandoning it instead leaves a work thread that terminate()s
+        # the process at exit); RCCL kernels spin on a dead peer until aborted
+        self._spins = self.backend != "gloo"
 
     @classmethod
     def get(cls, timeout_s: float = 60.0, **kw) -> "ElasticGroup":
@@ -176,6 +207,20 @@ class ElasticGroup:
             return min(self.timeout, DEFAULT_GRACE_S)
         return min(self.timeout, max(1.0, 3.0 * max(self._intervals)))
 
+    def dead_members(self) -> List[int]:
+        """Members the launcher reported dead (one store round trip when
+        nothing new died)."""
+        try:
+            n = self._root.add(DEATH_COUNT_KEY, 0)
+        except Exception:  # noqa: BLE001 - no store, no notices
+            return []
+        if n != self._dead_count:
+            self._dead_count = n
+            for r in self.members:
+                if r not in self._dead and self._root.check([f"{DEATH_KEY}/{r}"]):
+                    self._dead.add(r)
+        return [r for r in self.members if r in self._dead]
+
     def on_regroup(self, fn: Callable[["ElasticGroup"], None]) -> None:
         if fn not in self._listeners:
             self._listeners.append(fn)
@@ -197,9 +242,9 @@ class ElasticGroup:
                     now = time.monotonic()
                     if now > deadline:
                         return False
-                    if now > next_check:  # a peer already declared this collective failed
+                    if now > next_check:  # a peer declared this collective failed, or died
                         next_check = now + 0.02
-                        if self.store.check([dec]):
+                        if self.store.check([dec]) or (self._spins and self.dead_members()):
                             return False
                     time.sleep(self._poll)
                 w.wait()
@@ -234,11 +279,13 @@ class ElasticGroup:
                 return val == b"all"
         else:
             self.store.compare_set(dec, "", "fail")
-        try:
-            self.store.wait([dec], datetime.timedelta(seconds=self.timeout + self.grace))
-            val = self.store.get(dec)
-        except Exception:  # noqa: BLE001 - no decision in time: somebody is gone
-            val = self.store.compare_set(dec, "", "fail")
+        deadline = time.monotonic() + self.timeout + self.grace
+        while not self.store.check([dec]):
+            # a member that died before adding itself never will: decide now
+            if time.monotonic() > deadline or self.dead_members():
+                break
+            time.sleep(0.005)
+        val = self.store.compare_set(dec, "", "fail")
         return val == b"all"
 
     # --------------------------------------------------------------- regroup
@@ -248,12 +295,16 @@ class ElasticGroup:
         t0 = time.monotonic()
         ns = f"{self.gen}/members"
         self.store.set(f"{ns}/alive/{self.me}", "1")
-        keys = [f"{ns}/alive/{r}" for r in self.members]
-        try:
-            self.store.wait(keys, datetime.timedelta(seconds=self.grace))
-        except Exception:  # noqa: BLE001 - somebody did not check in
-            pass
-        seen = [r for r in self.members if self.store.check([f"{ns}/alive/{r}"])]
+        # wait until every member checked in or is known dead, at most ``grace``
+        deadline = time.monotonic() + self.grace
+        seen: List[int] = []
+        while True:
+            seen = [r for r in self.members if self.store.check([f"{ns}/alive/{r}"])]
+            dead = set(self.dead_members())
+            if all(r in dead or r in seen for r in self.members) or time.monotonic() > deadline:
+                break
+            time.sleep(0.01)
+        seen = [r for r in seen if r not in dead]
         survivors = sorted(json.loads(self.store.compare_set(f"{ns}/decision", "", json.dumps(seen))))
         discard_process_groups(self.backend)
         if self.me not in survivors:

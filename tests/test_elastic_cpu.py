@@ -65,13 +65,24 @@ def test_dropout_at_phase(phase, victim, nproc):
 
 def test_two_workers_drop_at_different_steps():
     r = _launch(4, ["dropout_stress.py", "--model", "gpt2-tiny", "--device", "cpu", "--seq_len", "32",
-                    "--micro_batch", "2", "--steps", "6", "--elastic_timeout", "20", "--drop_rank", "-1"],
+                    "--micro_batch", "2", "--steps", "6", "--elastic_timeout", "20", "--drop_rank", "-1",
+                    "--elastic_grace", "60"],
                 max_failures=2, env_extra={"DLION_FAULT": "1:2:after_launch,3:4:backward"})
     assert r.returncode == 0, r.stderr[-4000:]
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][0])
     assert res["world_end"] == 2 and res["survivors"] == [0, 2] and res["replicas_identical"]
     assert [e["dropped"] for e in res["dropout_events"]] == [[1], [3]]
     assert [e["step"] for e in res["dropout_events"]] == [2, 4]
+    # the launcher's death notices end the membership wait at once: nowhere
+    # near the 60 s check-in grace
+    assert res["elastic_stall_s"] < 10.0, res["dropout_events"]
+
+
+def test_death_notice_keys_agree():
+    from distributed_lion_pytorch_amd import launch
+    from distributed_lion_pytorch_amd.parallel import elastic
+
+    assert (launch.DEATH_KEY, launch.DEATH_COUNT_KEY) == (elastic.DEATH_KEY, elastic.DEATH_COUNT_KEY)
 
 
 def test_run_clm_survives_a_dropout(tmp_path):
