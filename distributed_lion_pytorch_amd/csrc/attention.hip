@@ -43,6 +43,11 @@
 #ifndef DLION_DKV_WAVES128
 #define DLION_DKV_WAVES128 1
 #endif
+// LDS ring depth of the backward kernels' streamed tiles: tile i+NB-1 is
+// staged while tile i is consumed (NB = 2: classic double buffering)
+#ifndef DLION_ATTN_STAGES
+#define DLION_ATTN_STAGES 3
+#endif
 
 namespace dlion {
 
@@ -195,6 +200,23 @@ __device__ __forceinline__ void glds4(const float* src, const void* dst) {
 // before it are complete, instead of re-waiting for them with counted vmcnt
 // inside the loop -- which, counting the asm DMAs too, drained the prefetch
 __device__ __forceinline__ void vm_wait0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// vmcnt(n) for a wave-uniform n < 16 (scalar branch over the immediates)
+__device__ __forceinline__ void vm_wait_n(int n) {
+  switch (n) {
+    case 0: __builtin_amdgcn_s_waitcnt(0x0F70); break;
+    case 1: __builtin_amdgcn_s_waitcnt(0x0F71); break;
+    case 2: __builtin_amdgcn_s_waitcnt(0x0F72); break;
+    case 3: __builtin_amdgcn_s_waitcnt(0x0F73); break;
+    case 4: __builtin_amdgcn_s_waitcnt(0x0F74); break;
+    case 5: __builtin_amdgcn_s_waitcnt(0x0F75); break;
+    case 6: __builtin_amdgcn_s_waitcnt(0x0F76); break;
+    case 7: __builtin_amdgcn_s_waitcnt(0x0F77); break;
+    case 8: __builtin_amdgcn_s_waitcnt(0x0F78); break;
+    case 9: __builtin_amdgcn_s_waitcnt(0x0F79); break;
+    case 10: __builtin_amdgcn_s_waitcnt(0x0F7A); break;
+    default: __builtin_amdgcn_s_waitcnt(0x0F7B); break;
+  }
+}
 
 template <int D>
 struct DmaTile {
@@ -389,8 +411,9 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 template <int D, bool DROP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? DLION_DQ_WAVES64 : 1)))
 attn_bwd_dq_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[2];
-  __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[2];
+  constexpr int NB = DLION_ATTN_STAGES;
+  __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[NB];
+  __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[NB];
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
   const int nt = ntiles32(a.T);
   const QBlock blk(a.B * a.H, nt);
@@ -434,17 +457,18 @@ attn_bwd_dq_kernel(AttnArgs a) {
   const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
   const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
   const DmaTile<D> kd(a.k_st), vd(a.v_st);
-  kd.issue(kg, ks_[0], a.T);
-  vd.issue(vg, vs_[0], a.T);
-  vm_wait0();
-  __syncthreads();
+  auto stage = [&](int kt, int buf) {
+    const int row = kt * 32;
+    kd.issue(kg + static_cast<int64_t>(row) * a.k_st, ks_[buf], a.T - row);
+    vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[buf], a.T - row);
+  };
+  for (int j = 0; j < NB - 1 && j <= last; ++j) stage(j, j);
   for (int kt = 0; kt <= last; ++kt) {
-    const int buf = kt & 1;
-    if (kt < last) {  // next tile into the other buffer (last read before the previous barrier)
-      const int nxt = (kt + 1) * 32;
-      kd.issue(kg + static_cast<int64_t>(nxt) * a.k_st, ks_[buf ^ 1], a.T - nxt);
-      vd.issue(vg + static_cast<int64_t>(nxt) * a.v_st, vs_[buf ^ 1], a.T - nxt);
-    }
+    const int buf = kt % NB;
+    // tile kt has landed once only the later tiles' pieces (2 PPW each) are in flight
+    vm_wait_n(min(last - kt, NB - 2) * 2 * DmaTile<D>::PPW);
+    __syncthreads();  // ... for every wave; and every wave is done with the buffer restaged next
+    if (kt + NB - 1 <= last) stage(kt + NB - 1, (kt + NB - 1) % NB);
     if (blk.active && kt <= qtile) {
       const int kb = kt * 32;
       f32x16 s = zero16(), dp = zero16();
@@ -479,8 +503,6 @@ attn_bwd_dq_kernel(AttnArgs a) {
         for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tr_frag<D>(ks_[buf], s2, t, lane), dq[t]);  // dQ += dS K
       }
     }
-    vm_wait0();  // this wave's pieces of the next tile have landed
-    __syncthreads();
   }
   if (!blk.active) return;
   // dq[t]: rows = q (registers), cols = d (lane)
@@ -515,9 +537,10 @@ attn_bwd_dq_kernel(AttnArgs a) {
 template <int D, bool DROP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? DLION_DKV_WAVES64 : DLION_DKV_WAVES128)))
 attn_bwd_dkv_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) LdsTile<D> qs_[2];
-  __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[2];
-  __shared__ __attribute__((aligned(16))) float ls_[2][3][32];  // [buf][lse | delta | drop row key][row]
+  constexpr int NB = DLION_ATTN_STAGES;
+  __shared__ __attribute__((aligned(16))) LdsTile<D> qs_[NB];
+  __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[NB];
+  __shared__ __attribute__((aligned(16))) float ls_[NB][3][32];  // [buf][lse | delta | drop row key][row]
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntiles = ntiles32(a.T), nbhk = a.B * a.Hkv;
   const int bhk = static_cast<int>(blockIdx.x % nbhk);
@@ -567,12 +590,14 @@ attn_bwd_dkv_kernel(AttnArgs a) {
     }
   };
   const uint32_t kmix = (static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u;
-  stage(0, 0);
-  vm_wait0();
-  __syncthreads();
+  for (int j = 0; j < NB - 1 && j < total; ++j) stage(j, j);
+  // LDS-DMA pieces per stage: Q + dO tiles, and wave 0's lse / delta row values
+  const int per_stage = 2 * DmaTile<D>::PPW + (w == 0 ? 1 : 0);
   for (int i = 0; i < total; ++i) {
-    const int buf = i & 1;
-    if (i + 1 < total) stage(i + 1, buf ^ 1);
+    const int buf = i % NB;
+    vm_wait_n(min(total - 1 - i, NB - 2) * per_stage);  // step i landed (later steps may be in flight)
+    __syncthreads();  // for every wave; and every wave is done with the buffer restaged next
+    if (i + NB - 1 < total) stage(i + NB - 1, (i + NB - 1) % NB);
     const int qt = first + i % nq;
     if (active && qt >= ktile) {  // wave-uniform
       const int qb = qt * 32;
@@ -633,8 +658,6 @@ attn_bwd_dkv_kernel(AttnArgs a) {
         }
       }
     }
-    vm_wait0();
-    __syncthreads();
   }
   if (!active) return;
   // dk/dv[t]: rows = key (registers), cols = d (lane)

@@ -26,6 +26,14 @@
 
 namespace dlion {
 
+// Tuning switches (A/B: tools/bench_lion.py with variant builds)
+#ifndef DLION_K2_NT
+#define DLION_K2_NT 0  // non-temporal p stores in the K2 fast path
+#endif
+#ifndef DLION_K4_MAXBLOCKS
+#define DLION_K4_MAXBLOCKS 2048  // K4 grid cap (grid-stride beyond)
+#endif
+
 constexpr int kThreads = 256;
 constexpr int kIters = 4;
 constexpr int kSpan = kThreads * 8;        // 2048 elements per block iteration
@@ -454,7 +462,8 @@ lion_vote_apply32_kernel(const int64_t* __restrict__ seg, const int64_t* __restr
         const float delta = static_cast<float>(static_cast<int>((pos >> j) & 1) - static_cast<int>((neg >> j) & 1));
         pv[j] = __fmaf_rn(neg_lr, delta, E::rnd(pv[j] * decay));
       }
-      E::store8(p + e, pv);
+      if constexpr (DLION_K2_NT) E::store8nt(p + e, pv);
+      else E::store8(p + e, pv);
     }
     return;
   }
@@ -710,7 +719,7 @@ hipError_t launch_vote_reduce(const uint8_t* recv, int64_t nbytes, const uint8_t
   const int64_t nwords = nbytes >> 2;
   if (nwords == 0) return hipSuccess;
   int64_t blocks = (nwords + kThreads - 1) / kThreads;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > DLION_K4_MAXBLOCKS) blocks = DLION_K4_MAXBLOCKS;
   if (world <= kMaxSliced)
     hipLaunchKernelGGL(vote_reduce_kernel<true>, dim3(blocks), dim3(kThreads), 0, st, recv, nbytes, alive, world, tie,
                        out, neg_out, ties);

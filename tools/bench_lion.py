@@ -83,10 +83,17 @@ def main():
             hx.vote_reduce(planes[W * b.byte_off: W * b.byte_off + W * sh], sh, alive, ref.TIE_NEGATIVE,
                            voted[b.byte_off // W: b.byte_off // W + sh], None)
 
+    src = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    dst = torch.empty_like(src)
+
+    def copy():  # practical roofline of a 50/50 read/write stream (what K2's p traffic is)
+        dst.copy_(src)
+
     # compulsory bytes per param: p r+w, g r, m r+w (local); g r, m r+w, 1 bit (encode);
     # p r+w + W bits (apply); W bits read + 1 bit written per shard param (vote_reduce, 1/W of params)
     cases = {"K0 local": (local, 10.0), "K1 encode": (encode, 6.0 + 1 / 8),
-             f"K2 vote+apply W={W}": (apply, 4.0 + W / 8), "K2 prevoted apply": (apply_prevoted, 4.0 + 1 / 8), f"K4 shard vote W={W}": (vote_reduce, (W + 1) / 8 / W)}
+             f"K2 vote+apply W={W}": (apply, 4.0 + W / 8), "K2 prevoted apply": (apply_prevoted, 4.0 + 1 / 8), f"K4 shard vote W={W}": (vote_reduce, (W + 1) / 8 / W),
+             "bf16 copy (reference)": (copy, 4.0)}
     print(f"{model}: {n / 1e6:.1f}M params, {len(ps)} tensors, {len(plan.buckets)} buckets", flush=True)
     res = {k: [] for k in cases}
     for _ in range(3):
