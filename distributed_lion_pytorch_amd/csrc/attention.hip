@@ -44,9 +44,12 @@
 #define DLION_DKV_WAVES128 1
 #endif
 // LDS ring depth of the backward kernels' streamed tiles: tile i+NB-1 is
-// staged while tile i is consumed (NB = 2: classic double buffering)
+// staged while tile i is consumed (NB = 2: classic double buffering).  NB = 3
+// spills 34 dwords in dK/dV under the 3-wave floor (168 VGPRs) and lifts dQ
+// from 133 to 162 VGPRs: GPT-2 bench 977k (NB 3) vs 1007k (NB 2) same box
+// (profiles/r3/attn_stages_ab.txt)
 #ifndef DLION_ATTN_STAGES
-#define DLION_ATTN_STAGES 3
+#define DLION_ATTN_STAGES 2
 #endif
 
 namespace dlion {
