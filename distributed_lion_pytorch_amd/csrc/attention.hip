@@ -40,6 +40,9 @@
 #ifndef DLION_DQ_WAVES64
 #define DLION_DQ_WAVES64 1
 #endif
+#ifndef DLION_DQ_NT64
+#define DLION_DQ_NT64 1
+#endif
 #ifndef DLION_DKV_WAVES128
 #define DLION_DKV_WAVES128 1
 #endif
@@ -411,12 +414,13 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 }
 
 // --------------------------------------------------------------- backward dQ
-template <int D, bool DROP>
+// NT key tiles per barrier (see the forward)
+template <int D, bool DROP, int NT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? DLION_DQ_WAVES64 : 1)))
 attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int NB = DLION_ATTN_STAGES;
-  __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[NB];
-  __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[NB];
+  __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[NB][NT];
+  __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[NB][NT];
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
   const int nt = ntiles32(a.T);
   const QBlock blk(a.B * a.H, nt);
@@ -460,51 +464,69 @@ attn_bwd_dq_kernel(AttnArgs a) {
   const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
   const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
   const DmaTile<D> kd(a.k_st), vd(a.v_st);
-  auto stage = [&](int kt, int buf) {
-    const int row = kt * 32;
-    kd.issue(kg + static_cast<int64_t>(row) * a.k_st, ks_[buf], a.T - row);
-    vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[buf], a.T - row);
+  // super-tile st = key tiles st*NT .. st*NT+NT-1, one LDS slot each; tiles
+  // past `last` re-read tile `last` (valid memory) and are masked below
+  auto stage = [&](int st, int buf) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int row = min(st * NT + j, last) * 32;
+      kd.issue(kg + static_cast<int64_t>(row) * a.k_st, ks_[buf][j], a.T - row);
+      vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[buf][j], a.T - row);
+    }
   };
-  for (int j = 0; j < NB - 1 && j <= last; ++j) stage(j, j);
-  for (int kt = 0; kt <= last; ++kt) {
-    const int buf = kt % NB;
-    // tile kt has landed once only the later tiles' pieces (2 PPW each) are in flight
-    vm_wait_n(min(last - kt, NB - 2) * 2 * DmaTile<D>::PPW);
+  const int ns = last / NT + 1;
+  for (int j = 0; j < NB - 1 && j < ns; ++j) stage(j, j);
+  for (int st = 0; st < ns; ++st) {
+    const int buf = st % NB;
+    // super-tile st has landed once only the later ones' pieces (NT * 2 PPW each) are in flight
+    vm_wait_n(min(ns - 1 - st, NB - 2) * NT * 2 * DmaTile<D>::PPW);
     __syncthreads();  // ... for every wave; and every wave is done with the buffer restaged next
-    if (kt + NB - 1 <= last) stage(kt + NB - 1, (kt + NB - 1) % NB);
-    if (blk.active && kt <= qtile) {
-      const int kb = kt * 32;
-      f32x16 s = zero16(), dp = zero16();
+    if (st + NB - 1 < ns) stage(st + NB - 1, (st + NB - 1) % NB);
+    const int kt0 = st * NT;
+    if (blk.active && kt0 <= qtile) {
+      // NT independent S / dP chains: one tile's exp / hash VALU work can sit
+      // beside the other's MFMAs
+      f32x16 s[NT], dp[NT];
 #pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) {
-        s = mfma32(row_frag<D>(ks_[buf], r, ks, hf), qf[ks], s);    // S^T  = K Q^T
-        dp = mfma32(row_frag<D>(vs_[buf], r, ks, hf), dof[ks], dp);  // dP^T = V dO^T
-      }
-      if (kt == qtile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
+      for (int j = 0; j < NT; ++j) {
+        s[j] = zero16();
+        dp[j] = zero16();
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg)
-          if (kb + acc_row(reg, hf) > q) s[reg] = -INFINITY;
-      }
-#pragma unroll
-      for (int reg = 0; reg < 16; reg += 2) {
-        const int key = kb + acc_row(reg, hf);  // even: regs (reg, reg+1) = keys (key, key+1)
-        uint32_t hsh = 0;
-        if constexpr (DROP) hsh = mix1(arow ^ ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u));
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int kk = key + e;
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg + e], a.scale_log2, -lse2));
-          float dpv = dp[reg + e];
-          if constexpr (DROP) dpv = ((e == 0 ? hsh << 16 : hsh) >= thr_hi) ? dpv : 0.f;  // p, dlt carry 1/(1-p)
-          s[reg + e] = p * (dpv - dlt);  // dS^T
+        for (int ks = 0; ks < D / 16; ++ks) {
+          s[j] = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), qf[ks], s[j]);    // S^T  = K Q^T
+          dp[j] = mfma32(row_frag<D>(vs_[buf][j], r, ks, hf), dof[ks], dp[j]);  // dP^T = V dO^T
         }
       }
+      if (kt0 + NT - 1 >= qtile) {  // the diagonal (or tiles past it) in this group: exp2(-inf) = 0
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 dsf = acc_frag(s, s2);
+        for (int j = 0; j < NT; ++j)
 #pragma unroll
-        for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tr_frag<D>(ks_[buf], s2, t, lane), dq[t]);  // dQ += dS K
+          for (int reg = 0; reg < 16; ++reg)
+            if ((kt0 + j) * 32 + acc_row(reg, hf) > q) s[j][reg] = -INFINITY;
       }
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int reg = 0; reg < 16; reg += 2) {
+          const int key = (kt0 + j) * 32 + acc_row(reg, hf);  // even: regs (reg, reg+1) = keys (key, key+1)
+          uint32_t hsh = 0;
+          if constexpr (DROP) hsh = mix1(arow ^ ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u));
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][reg + e], a.scale_log2, -lse2));
+            float dpv = dp[j][reg + e];
+            if constexpr (DROP) dpv = ((e == 0 ? hsh << 16 : hsh) >= thr_hi) ? dpv : 0.f;  // p, dlt carry 1/(1-p)
+            s[j][reg + e] = p * (dpv - dlt);  // dS^T
+          }
+        }
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 dsf = acc_frag(s[j], s2);
+#pragma unroll
+          for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tr_frag<D>(ks_[buf][j], s2, t, lane), dq[t]);  // dQ += dS K
+        }
     }
   }
   if (!blk.active) return;
@@ -722,18 +744,18 @@ hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
   const dim3 bq(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T)));
   const dim3 bkv(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.Hkv, a.T)));
   // dQ first: it also computes delta = rowsum(dO * O), which dKV reads
-#define BWD(DD)                                                                                           \
+#define BWD(DD, NT)                                                                                       \
   if (drop) {                                                                                             \
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, true>), bq, dim3(256), 0, st, a);                         \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, true, NT>), bq, dim3(256), 0, st, a);                     \
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), bkv, dim3(256), 0, st, a);                       \
   } else {                                                                                                \
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, false>), bq, dim3(256), 0, st, a);                        \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, false, NT>), bq, dim3(256), 0, st, a);                    \
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), bkv, dim3(256), 0, st, a);                      \
   }
   if (D == 64) {
-    BWD(64)
+    BWD(64, DLION_DQ_NT64)
   } else if (D == 128) {
-    BWD(128)
+    BWD(128, 1)
   } else {
     return hipErrorInvalidValue;
   }
