@@ -43,6 +43,10 @@
 #ifndef DLION_DQ_NT64
 #define DLION_DQ_NT64 1
 #endif
+// software-pipelined dQ main loop (NT must be 1)
+#ifndef DLION_DQ_PIPE
+#define DLION_DQ_PIPE 0
+#endif
 #ifndef DLION_DKV_WAVES128
 #define DLION_DKV_WAVES128 1
 #endif
@@ -414,11 +418,16 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 }
 
 // --------------------------------------------------------------- backward dQ
-// NT key tiles per barrier (see the forward)
-template <int D, bool DROP, int NT>
+// NT key tiles per barrier (see the forward).  PIPE: software-pipelined single
+// tiles -- S^T / dP^T of tile kt+1 are issued to the MFMA pipe before tile kt's
+// exp / dropout / dS VALU work and its dQ MFMAs, so the two overlap inside one
+// basic block; a 4-slot ring keeps tile kt (K for dQ), kt+1 (K, V for S / dP)
+// resident and kt+2, kt+3 in flight.
+template <int D, bool DROP, int NT, bool PIPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? DLION_DQ_WAVES64 : 1)))
 attn_bwd_dq_kernel(AttnArgs a) {
-  constexpr int NB = DLION_ATTN_STAGES;
+  static_assert(!PIPE || NT == 1, "the pipelined dQ loop streams single key tiles");
+  constexpr int NB = PIPE ? 4 : DLION_ATTN_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[NB][NT];
   __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[NB][NT];
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
@@ -464,6 +473,69 @@ attn_bwd_dq_kernel(AttnArgs a) {
   const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
   const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
   const DmaTile<D> kd(a.k_st), vd(a.v_st);
+  if constexpr (PIPE) {
+    auto stage1 = [&](int kt) {
+      const int row = kt * 32;
+      kd.issue(kg + static_cast<int64_t>(row) * a.k_st, ks_[kt & 3][0], a.T - row);
+      vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[kt & 3][0], a.T - row);
+    };
+    auto sdp = [&](int kt, f32x16& s, f32x16& dp) {  // S^T = K Q^T, dP^T = V dO^T of key tile kt
+      s = zero16();
+      dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        s = mfma32(row_frag<D>(ks_[kt & 3][0], r, ks, hf), qf[ks], s);
+        dp = mfma32(row_frag<D>(vs_[kt & 3][0], r, ks, hf), dof[ks], dp);
+      }
+    };
+    auto finish = [&](int kt, f32x16& s, const f32x16& dp) {  // dS^T of tile kt, then dQ += dS K
+      const int kb = kt * 32;
+      if (kt == qtile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+          if (kb + acc_row(reg, hf) > q) s[reg] = -INFINITY;
+      }
+#pragma unroll
+      for (int reg = 0; reg < 16; reg += 2) {
+        const int key = kb + acc_row(reg, hf);
+        uint32_t hsh = 0;
+        if constexpr (DROP) hsh = mix1(arow ^ ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u));
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg + e], a.scale_log2, -lse2));
+          float dpv = dp[reg + e];
+          if constexpr (DROP) dpv = ((e == 0 ? hsh << 16 : hsh) >= thr_hi) ? dpv : 0.f;
+          s[reg + e] = p * (dpv - dlt);
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 dsf = acc_frag(s, s2);
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tr_frag<D>(ks_[kt & 3][0], s2, t, lane), dq[t]);
+      }
+    };
+    for (int j = 0; j < 3 && j <= last; ++j) stage1(j);
+    vm_wait_n(min(last, 2) * 2 * DmaTile<D>::PPW);  // tile 0 landed (tiles 1, 2 may be in flight)
+    __syncthreads();
+    f32x16 sA, dpA, sB, dpB;
+    if (blk.active) sdp(0, sA, dpA);
+    // step kt: (sc, dc) hold tile kt's S^T / dP^T; tile kt+1's go to (sn, dn)
+    auto step = [&](int kt, f32x16& sc, f32x16& dc, f32x16& sn, f32x16& dn) {
+      // tile kt+1 landed (kt+2 may be in flight); every wave is done with tile kt-1's slot
+      vm_wait_n((last - kt - 1 >= 1 ? 1 : 0) * 2 * DmaTile<D>::PPW);
+      __syncthreads();
+      if (kt + 3 <= last) stage1(kt + 3);
+      if (blk.active && kt <= qtile) {  // wave-uniform
+        if (kt + 1 <= qtile) sdp(kt + 1, sn, dn);
+        finish(kt, sc, dc);
+      }
+    };
+    for (int kt = 0; kt <= last; kt += 2) {  // unrolled by two: the register sets swap roles, no copies
+      step(kt, sA, dpA, sB, dpB);
+      if (kt + 1 <= last) step(kt + 1, sB, dpB, sA, dpA);
+    }
+  } else {
   // super-tile st = key tiles st*NT .. st*NT+NT-1, one LDS slot each; tiles
   // past `last` re-read tile `last` (valid memory) and are masked below
   auto stage = [&](int st, int buf) {
@@ -528,6 +600,7 @@ attn_bwd_dq_kernel(AttnArgs a) {
           for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tr_frag<D>(ks_[buf][j], s2, t, lane), dq[t]);  // dQ += dS K
         }
     }
+  }
   }
   if (!blk.active) return;
   // dq[t]: rows = q (registers), cols = d (lane)
@@ -744,18 +817,18 @@ hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
   const dim3 bq(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T)));
   const dim3 bkv(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.Hkv, a.T)));
   // dQ first: it also computes delta = rowsum(dO * O), which dKV reads
-#define BWD(DD, NT)                                                                                       \
+#define BWD(DD, NT, PIPE)                                                                                     \
   if (drop) {                                                                                             \
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, true, NT>), bq, dim3(256), 0, st, a);                     \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, true, NT, PIPE>), bq, dim3(256), 0, st, a);                     \
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), bkv, dim3(256), 0, st, a);                       \
   } else {                                                                                                \
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, false, NT>), bq, dim3(256), 0, st, a);                    \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, false, NT, PIPE>), bq, dim3(256), 0, st, a);                    \
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), bkv, dim3(256), 0, st, a);                      \
   }
   if (D == 64) {
-    BWD(64, DLION_DQ_NT64)
+    BWD(64, DLION_DQ_NT64, DLION_DQ_PIPE != 0)
   } else if (D == 128) {
-    BWD(128, 1)
+    BWD(128, 1, false)
   } else {
     return hipErrorInvalidValue;
   }
