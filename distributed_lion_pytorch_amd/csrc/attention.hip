@@ -43,7 +43,10 @@
 #ifndef DLION_DQ_NT64
 #define DLION_DQ_NT64 1
 #endif
-// software-pipelined dQ main loop (NT must be 1)
+// software-pipelined forward (D = 64) and dQ main loops
+#ifndef DLION_FWD_PIPE
+#define DLION_FWD_PIPE 0
+#endif
 #ifndef DLION_DQ_PIPE
 #define DLION_DQ_PIPE 0
 #endif
@@ -283,10 +286,15 @@ struct QBlock {
 // independent QK^T chains and two PV chains per iteration, so hipcc can put one
 // tile's MFMAs beside the other's softmax VALU work; with NT = 1 each step of
 // the QK -> max -> exp -> PV chain waits for the previous one.
-template <int D, bool DROP, int NT>
+// PIPE (NT = 1): software-pipelined -- tile kt+1's QK^T MFMAs are issued
+// before tile kt's softmax VALU work and PV MFMAs (4-slot K/V ring: kt for PV,
+// kt+1 for QK^T, kt+2 / kt+3 in flight).
+template <int D, bool DROP, int NT, bool PIPE = false>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[2][NT];
-  __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[2][NT];
+  static_assert(!PIPE || NT == 1, "the pipelined forward streams single key tiles");
+  constexpr int NB = PIPE ? 4 : 2;
+  __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[NB][NT];
+  __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[NB][NT];
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
   const QBlock blk(a.B * a.H, ntiles32(a.T));
   const int bh = blk.bh, qtile = blk.qtile, last = blk.last;
@@ -312,6 +320,81 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const uint32_t arow = drop_row(a.seed, bh, q);
   const uint32_t thr_hi = a.thresh16 << 16;
   const DmaTile<D> kd(a.k_st), vd(a.v_st);
+  if constexpr (PIPE) {
+    auto stage1 = [&](int kt) {
+      const int row = kt * 32;
+      kd.issue(kg + static_cast<int64_t>(row) * a.k_st, ks_[kt & 3][0], a.T - row);
+      vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[kt & 3][0], a.T - row);
+    };
+    auto qk = [&](int kt, f32x16& sc) {
+      sc = zero16();
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) sc = mfma32(row_frag<D>(ks_[kt & 3][0], r, ks, hf), qf[ks], sc);
+    };
+    auto softmax_pv = [&](int kt, f32x16& sc) {
+      if (kt == qtile) {  // causal mask on the diagonal tile only (scalar branch)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+          if (kt * 32 + acc_row(reg, hf) > q) sc[reg] = -INFINITY;
+      }
+      float tmax = sc[0];
+#pragma unroll
+      for (int reg = 1; reg < 16; ++reg) tmax = fmaxf(tmax, sc[reg]);
+      tmax = xmax32(tmax) * a.scale_log2;
+      float alpha = 1.f;
+      if (!__all(tmax - m <= kDeferLog2)) {  // deferred rescale, as below
+        const float mn = fmaxf(m, tmax);
+        alpha = __builtin_amdgcn_exp2f(m - mn);
+        m = mn;
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) oacc[t][i] *= alpha;
+      }
+      float rs = 0.f;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[reg], a.scale_log2, -m));
+        rs += p;
+        sc[reg] = p;
+      }
+      l = l * alpha + xsum32(rs);
+      if constexpr (DROP) {
+#pragma unroll
+        for (int reg = 0; reg < 16; reg += 2) {
+          const uint32_t key = kt * 32 + acc_row(reg, hf);
+          const uint32_t hsh = mix1(arow ^ ((key >> 1) * 0xC2B2AE35u));
+          if ((hsh << 16) < thr_hi) sc[reg] = 0.f;
+          if (hsh < thr_hi) sc[reg + 1] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pf = acc_frag(sc, s2);
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) oacc[t] = mfma32(tr_frag<D>(vs_[kt & 3][0], s2, t, lane), pf, oacc[t]);
+      }
+    };
+    for (int j = 0; j < 3 && j <= last; ++j) stage1(j);
+    vm_wait_n(min(last, 2) * 2 * DmaTile<D>::PPW);  // tile 0 landed (tiles 1, 2 may be in flight)
+    __syncthreads();
+    f32x16 sA, sB;
+    if (blk.active) qk(0, sA);
+    auto step = [&](int kt, f32x16& sc, f32x16& sn) {
+      // tile kt+1 landed (kt+2 may be in flight); every wave is done with tile kt-1's slot
+      vm_wait_n((last - kt - 1 >= 1 ? 1 : 0) * 2 * DmaTile<D>::PPW);
+      __syncthreads();
+      if (kt + 3 <= last) stage1(kt + 3);
+      if (blk.active && kt <= qtile) {  // wave-uniform
+        if (kt + 1 <= qtile) qk(kt + 1, sn);
+        softmax_pv(kt, sc);
+      }
+    };
+    for (int kt = 0; kt <= last; kt += 2) {  // unrolled by two: the score registers swap roles
+      step(kt, sA, sB);
+      if (kt + 1 <= last) step(kt + 1, sB, sA);
+    }
+  } else {
   // tiles past `last` re-read tile `last` (valid memory); the causal mask
   // zeroes them, since they lie beyond every query of the block
   auto stage = [&](int first, int buf) {
@@ -397,6 +480,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     }
     vm_wait0();  // this wave's pieces of the next tiles have landed
     __syncthreads();
+  }
   }
   if (!blk.active || q >= a.T) return;
   const float inv_l = (DROP ? a.inv_keep : 1.f) / l;
@@ -799,13 +883,17 @@ hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
   const dim3 grid(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T))), block(256);
   // NT = 2 key tiles per barrier at D=64 (GPT-2 shape fwd 0.067 -> 0.065 ms);
   // at D=128 the extra 64 VGPRs cost a wave of occupancy and it was neutral
-#define FWD(DD, NT)                                                                        \
-  if (drop) hipLaunchKernelGGL((attn_fwd_kernel<DD, true, NT>), grid, block, 0, st, a); \
-  else hipLaunchKernelGGL((attn_fwd_kernel<DD, false, NT>), grid, block, 0, st, a);
+#define FWD(DD, NT, PIPE)                                                                        \
+  if (drop) hipLaunchKernelGGL((attn_fwd_kernel<DD, true, NT, PIPE>), grid, block, 0, st, a); \
+  else hipLaunchKernelGGL((attn_fwd_kernel<DD, false, NT, PIPE>), grid, block, 0, st, a);
   if (D == 64) {
-    FWD(64, 2)
+#if DLION_FWD_PIPE
+    FWD(64, 1, true)
+#else
+    FWD(64, 2, false)
+#endif
   } else if (D == 128) {
-    FWD(128, 1)
+    FWD(128, 1, false)
   } else {
     return hipErrorInvalidValue;
   }
