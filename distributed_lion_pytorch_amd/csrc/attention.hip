@@ -50,6 +50,12 @@
 #ifndef DLION_DQ_PIPE
 #define DLION_DQ_PIPE 0
 #endif
+#ifndef DLION_DKV_PIPE
+#define DLION_DKV_PIPE 0
+#endif
+#ifndef DLION_DKV_PIPE_WAVES64
+#define DLION_DKV_PIPE_WAVES64 1
+#endif
 #ifndef DLION_DKV_WAVES128
 #define DLION_DKV_WAVES128 1
 #endif
@@ -716,10 +722,14 @@ attn_bwd_dq_kernel(AttnArgs a) {
 // 4 waves = 4 consecutive key tiles of one (b, kv-head); every query tile of
 // every head in the GQA group is staged once per block (Q, dO and the 32
 // lse / delta values).  Low key groups (most query tiles) go first.
-template <int D, bool DROP>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? DLION_DKV_WAVES64 : DLION_DKV_WAVES128)))
+// PIPE: software-pipelined -- step i+1's S / dP MFMAs are issued before step
+// i's softmax-gradient VALU work and its dV / dK MFMAs (4-slot ring: i for the
+// transposed reads and row statistics, i+1 for S / dP, i+2 / i+3 in flight).
+template <int D, bool DROP, bool PIPE = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    D == 64 ? (PIPE ? DLION_DKV_PIPE_WAVES64 : DLION_DKV_WAVES64) : DLION_DKV_WAVES128)))
 attn_bwd_dkv_kernel(AttnArgs a) {
-  constexpr int NB = DLION_ATTN_STAGES;
+  constexpr int NB = PIPE ? 4 : DLION_ATTN_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> qs_[NB];
   __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[NB];
   __shared__ __attribute__((aligned(16))) float ls_[NB][3][32];  // [buf][lse | delta | drop row key][row]
@@ -775,68 +785,154 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   for (int j = 0; j < NB - 1 && j < total; ++j) stage(j, j);
   // LDS-DMA pieces per stage: Q + dO tiles, and wave 0's lse / delta row values
   const int per_stage = 2 * DmaTile<D>::PPW + (w == 0 ? 1 : 0);
-  for (int i = 0; i < total; ++i) {
+  // S = Q K^T (rows q, cols key) and dP = dO V^T of step i from its slot
+  auto sdp = [&](int i, f32x16& s, f32x16& dp) {
     const int buf = i % NB;
-    vm_wait_n(min(total - 1 - i, NB - 2) * per_stage);  // step i landed (later steps may be in flight)
-    __syncthreads();  // for every wave; and every wave is done with the buffer restaged next
-    if (i + NB - 1 < total) stage(i + NB - 1, (i + NB - 1) % NB);
-    const int qt = first + i % nq;
-    if (active && qt >= ktile) {  // wave-uniform
-      const int qb = qt * 32;
-      f32x16 s = zero16(), dp = zero16();
+    s = zero16();
+    dp = zero16();
 #pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) {
-        s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), kf[ks], s);   // S  = Q K^T : rows q, cols key
-        dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), vf[ks], dp);  // dP = dO V^T
-      }
-      if (qt == ktile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
+    for (int ks = 0; ks < D / 16; ++ks) {
+      s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), kf[ks], s);
+      dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), vf[ks], dp);
+    }
+  };
+  // masks, P / dS from the step's row statistics, dV += Pd^T dO, dK += dS^T Q
+  auto finish = [&](int i, f32x16& s, const f32x16& dp) {
+    const int buf = i % NB;
+    const int qt = first + i % nq, qb = qt * 32;
+    if (qt == ktile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg)
-          if (key > qb + acc_row(reg, hf)) s[reg] = -INFINITY;
-      }
-      if (qb + 32 > a.T) {  // tail query tile: rows past T contribute nothing (p = 0, dS = 0)
+      for (int reg = 0; reg < 16; ++reg)
+        if (key > qb + acc_row(reg, hf)) s[reg] = -INFINITY;
+    }
+    if (qb + 32 > a.T) {  // tail query tile: rows past T contribute nothing (p = 0, dS = 0)
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg)
-          if (qb + acc_row(reg, hf) >= a.T) s[reg] = -INFINITY;
-      }
-      // row statistics of the lane's 16 query rows: rows (reg&3) + 8(reg>>2) + 4hf
-      // come in 4 runs of 4 consecutive rows -> 16-byte LDS reads (broadcast),
-      // consumed run by run (not all 48 values staged up front: that held the
-      // kernel at 212 VGPRs, two waves per SIMD)
-      f32x16 pd;
+      for (int reg = 0; reg < 16; ++reg)
+        if (qb + acc_row(reg, hf) >= a.T) s[reg] = -INFINITY;
+    }
+    // row statistics of the lane's 16 query rows: rows (reg&3) + 8(reg>>2) + 4hf
+    // come in 4 runs of 4 consecutive rows -> 16-byte LDS reads (broadcast),
+    // consumed run by run (not all 48 values staged up front: that held the
+    // kernel at 212 VGPRs, two waves per SIMD)
+    f32x16 pd;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 lv = *reinterpret_cast<const float4*>(&ls_[buf][0][8 * g + 4 * hf]);
-        const float4 dv4 = *reinterpret_cast<const float4*>(&ls_[buf][1][8 * g + 4 * hf]);
-        uint4 av = make_uint4(0, 0, 0, 0);
-        if constexpr (DROP) av = *reinterpret_cast<const uint4*>(&ls_[buf][2][8 * g + 4 * hf]);
-        const float lse_g[4] = {lv.x, lv.y, lv.z, lv.w};
-        const float dl_g[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
-        const uint32_t ar_g[4] = {av.x, av.y, av.z, av.w};
+    for (int g = 0; g < 4; ++g) {
+      const float4 lv = *reinterpret_cast<const float4*>(&ls_[buf][0][8 * g + 4 * hf]);
+      const float4 dv4 = *reinterpret_cast<const float4*>(&ls_[buf][1][8 * g + 4 * hf]);
+      uint4 av = make_uint4(0, 0, 0, 0);
+      if constexpr (DROP) av = *reinterpret_cast<const uint4*>(&ls_[buf][2][8 * g + 4 * hf]);
+      const float lse_g[4] = {lv.x, lv.y, lv.z, lv.w};
+      const float dl_g[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
+      const uint32_t ar_g[4] = {av.x, av.y, av.z, av.w};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int reg = 4 * g + i;
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -lse_g[i]));
-          float dpv = dp[reg];
-          float pdv = p;
-          if constexpr (DROP) {  // the lane is the key here: one (cheap) hash per element;
-                                 // p and the delta row values already carry 1/(1-p)
-            const bool kp_ = (mix1(ar_g[i] ^ kmix) << kshift) >= thr_hi;
-            dpv = kp_ ? dpv : 0.f;
-            pdv = kp_ ? p : 0.f;
-          }
-          pd[reg] = pdv;
-          s[reg] = p * (dpv - dl_g[i]);  // dS
+      for (int e = 0; e < 4; ++e) {
+        const int reg = 4 * g + e;
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -lse_g[e]));
+        float dpv = dp[reg];
+        float pdv = p;
+        if constexpr (DROP) {  // the lane is the key here: one (cheap) hash per element;
+                               // p and the delta row values already carry 1/(1-p)
+          const bool kp_ = (mix1(ar_g[e] ^ kmix) << kshift) >= thr_hi;
+          dpv = kp_ ? dpv : 0.f;
+          pdv = kp_ ? p : 0.f;
         }
+        pd[reg] = pdv;
+        s[reg] = p * (dpv - dl_g[e]);  // dS
       }
+    }
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pf = acc_frag(pd, s2);
-        const bf16x8 dsf = acc_frag(s, s2);
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pf = acc_frag(pd, s2);
+      const bf16x8 dsf = acc_frag(s, s2);
 #pragma unroll
-        for (int t = 0; t < D / 32; ++t) {
-          dv[t] = mfma32(pf, tr_frag<D>(ds_[buf], s2, t, lane), dv[t]);   // dV += Pd^T dO
-          dk[t] = mfma32(dsf, tr_frag<D>(qs_[buf], s2, t, lane), dk[t]);  // dK += dS^T Q
+      for (int t = 0; t < D / 32; ++t) {
+        dv[t] = mfma32(pf, tr_frag<D>(ds_[buf], s2, t, lane), dv[t]);   // dV += Pd^T dO
+        dk[t] = mfma32(dsf, tr_frag<D>(qs_[buf], s2, t, lane), dk[t]);  // dK += dS^T Q
+      }
+    }
+  };
+  auto live = [&](int i) { return active && first + i % nq >= ktile; };  // wave-uniform
+  if constexpr (PIPE) {
+    f32x16 sA, dpA, sB, dpB;
+    vm_wait_n(min(total - 1, NB - 2) * per_stage);  // step 0 landed (steps 1, 2 may be in flight)
+    __syncthreads();
+    if (live(0)) sdp(0, sA, dpA);
+    auto step = [&](int i, f32x16& sc, f32x16& dc, f32x16& sn, f32x16& dn) {
+      // step i+1 landed (i+2 may be in flight); every wave is done with step i-1's slot
+      vm_wait_n((total - 1 - i >= 2 ? 1 : 0) * per_stage);
+      __syncthreads();
+      if (i + NB - 1 < total) stage(i + NB - 1, (i + NB - 1) % NB);
+      if (i + 1 < total && live(i + 1)) sdp(i + 1, sn, dn);
+      if (live(i)) finish(i, sc, dc);
+    };
+    for (int i = 0; i < total; i += 2) {  // unrolled by two: the register sets swap roles, no copies
+      step(i, sA, dpA, sB, dpB);
+      if (i + 1 < total) step(i + 1, sB, dpB, sA, dpA);
+    }
+  } else {  // (the straight loop, kept verbatim: routing it through the lambdas above spills 16 dwords)
+    for (int i = 0; i < total; ++i) {
+      const int buf = i % NB;
+      vm_wait_n(min(total - 1 - i, NB - 2) * per_stage);  // step i landed (later steps may be in flight)
+      __syncthreads();  // for every wave; and every wave is done with the buffer restaged next
+      if (i + NB - 1 < total) stage(i + NB - 1, (i + NB - 1) % NB);
+      const int qt = first + i % nq;
+      if (active && qt >= ktile) {  // wave-uniform
+        const int qb = qt * 32;
+        f32x16 s = zero16(), dp = zero16();
+  #pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) {
+          s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), kf[ks], s);   // S  = Q K^T : rows q, cols key
+          dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), vf[ks], dp);  // dP = dO V^T
+        }
+        if (qt == ktile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
+  #pragma unroll
+          for (int reg = 0; reg < 16; ++reg)
+            if (key > qb + acc_row(reg, hf)) s[reg] = -INFINITY;
+        }
+        if (qb + 32 > a.T) {  // tail query tile: rows past T contribute nothing (p = 0, dS = 0)
+  #pragma unroll
+          for (int reg = 0; reg < 16; ++reg)
+            if (qb + acc_row(reg, hf) >= a.T) s[reg] = -INFINITY;
+        }
+        // row statistics of the lane's 16 query rows: rows (reg&3) + 8(reg>>2) + 4hf
+        // come in 4 runs of 4 consecutive rows -> 16-byte LDS reads (broadcast),
+        // consumed run by run (not all 48 values staged up front: that held the
+        // kernel at 212 VGPRs, two waves per SIMD)
+        f32x16 pd;
+  #pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 lv = *reinterpret_cast<const float4*>(&ls_[buf][0][8 * g + 4 * hf]);
+          const float4 dv4 = *reinterpret_cast<const float4*>(&ls_[buf][1][8 * g + 4 * hf]);
+          uint4 av = make_uint4(0, 0, 0, 0);
+          if constexpr (DROP) av = *reinterpret_cast<const uint4*>(&ls_[buf][2][8 * g + 4 * hf]);
+          const float lse_g[4] = {lv.x, lv.y, lv.z, lv.w};
+          const float dl_g[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
+          const uint32_t ar_g[4] = {av.x, av.y, av.z, av.w};
+  #pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int reg = 4 * g + i;
+            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -lse_g[i]));
+            float dpv = dp[reg];
+            float pdv = p;
+            if constexpr (DROP) {  // the lane is the key here: one (cheap) hash per element;
+                                   // p and the delta row values already carry 1/(1-p)
+              const bool kp_ = (mix1(ar_g[i] ^ kmix) << kshift) >= thr_hi;
+              dpv = kp_ ? dpv : 0.f;
+              pdv = kp_ ? p : 0.f;
+            }
+            pd[reg] = pdv;
+            s[reg] = p * (dpv - dl_g[i]);  // dS
+          }
+        }
+  #pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 pf = acc_frag(pd, s2);
+          const bf16x8 dsf = acc_frag(s, s2);
+  #pragma unroll
+          for (int t = 0; t < D / 32; ++t) {
+            dv[t] = mfma32(pf, tr_frag<D>(ds_[buf], s2, t, lane), dv[t]);   // dV += Pd^T dO
+            dk[t] = mfma32(dsf, tr_frag<D>(qs_[buf], s2, t, lane), dk[t]);  // dK += dS^T Q
+          }
         }
       }
     }
@@ -905,18 +1001,18 @@ hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
   const dim3 bq(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T)));
   const dim3 bkv(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.Hkv, a.T)));
   // dQ first: it also computes delta = rowsum(dO * O), which dKV reads
-#define BWD(DD, NT, PIPE)                                                                                     \
+#define BWD(DD, NT, PIPE, KPIPE)                                                                                  \
   if (drop) {                                                                                             \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, true, NT, PIPE>), bq, dim3(256), 0, st, a);                     \
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), bkv, dim3(256), 0, st, a);                       \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true, KPIPE>), bkv, dim3(256), 0, st, a);                       \
   } else {                                                                                                \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, false, NT, PIPE>), bq, dim3(256), 0, st, a);                    \
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), bkv, dim3(256), 0, st, a);                      \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false, KPIPE>), bkv, dim3(256), 0, st, a);                      \
   }
   if (D == 64) {
-    BWD(64, DLION_DQ_NT64, DLION_DQ_PIPE != 0)
+    BWD(64, DLION_DQ_NT64, DLION_DQ_PIPE != 0, DLION_DKV_PIPE != 0)
   } else if (D == 128) {
-    BWD(128, 1, false)
+    BWD(128, 1, false, false)
   } else {
     return hipErrorInvalidValue;
   }
