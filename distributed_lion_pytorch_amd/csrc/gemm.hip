@@ -80,6 +80,32 @@ __device__ __forceinline__ void glds16(const uint16_t* src, uint8_t* dst) {
                                    (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
+// Epilogue store / aux-load flavour (A/B switches, default off): DLION_GEMM_NT_AUX
+// writes / reads the MLP aux tensor (gelu'(z): written here, read once by the
+// backward) with non-temporal hints, DLION_GEMM_NT_C does the same for C, so
+// the 126 MB outputs of the K = 768 MLP GEMMs do not evict operand panels
+#ifndef DLION_GEMM_NT_AUX
+#define DLION_GEMM_NT_AUX 0
+#endif
+#ifndef DLION_GEMM_NT_C
+#define DLION_GEMM_NT_C 0
+#endif
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT, typename V>
+__device__ __forceinline__ void st16(uint16_t* p, const V& v) {
+  const u32x4 x = __builtin_bit_cast(u32x4, v);
+  if constexpr (NT) __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
+  else *reinterpret_cast<u32x4*>(p) = x;
+}
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const uint16_t* p) {
+  u32x4 x;
+  if constexpr (NT) x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  else x = *reinterpret_cast<const u32x4*>(p);
+  return make_uint4(x[0], x[1], x[2], x[3]);
+}
+constexpr bool kNtAux = DLION_GEMM_NT_AUX != 0, kNtC = DLION_GEMM_NT_C != 0;
+
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -346,7 +372,7 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
       const int row = i * 8 + (lane >> 3);
       const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((ch ^ (row & 7)) << 4));
       const int gm = row_base + row;
-      if (gm < g.M && gn < g.N) *reinterpret_cast<uint4*>(g.C + (int64_t)gm * g.ldc + gn) = v;
+      if (gm < g.M && gn < g.N) st16<kNtC>(g.C + (int64_t)gm * g.ldc + gn, v);
     }
     if constexpr (STAMP) {
       DLION_STAMP(st_[4])
@@ -379,7 +405,7 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
         Elem<kBF16>::load8(reinterpret_cast<const uint16_t*>(&v), z);
         bf16x8 hb;
         if constexpr (EPI <= 3) {
-          *reinterpret_cast<uint4*>(g.aux + (int64_t)gm * g.ldaux + gn) = v;
+          st16<kNtAux>(g.aux + (int64_t)gm * g.ldaux + gn, v);
 #pragma unroll
           for (int j = 0; j < 8; ++j) hb[j] = static_cast<__bf16>(gelu_f(z[j] + b8[j], EPI == 3));
         } else {
@@ -391,9 +417,9 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
             hb[j] = static_cast<__bf16>(gv);
             db[j] = static_cast<__bf16>(dgv);
           }
-          *reinterpret_cast<bf16x8*>(g.aux + (int64_t)gm * g.ldaux + gn) = db;
+          st16<kNtAux>(g.aux + (int64_t)gm * g.ldaux + gn, db);
         }
-        *reinterpret_cast<bf16x8*>(g.C + (int64_t)gm * g.ldc + gn) = hb;
+        st16<kNtC>(g.C + (int64_t)gm * g.ldc + gn, hb);
       }
     }
   } else {
@@ -411,7 +437,7 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int gm = min(row_base + i * 8 + (lane >> 3), g.M - 1);
-      zr[i] = gn < g.N ? *reinterpret_cast<const uint4*>(g.aux + (int64_t)gm * g.ldaux + gn) : make_uint4(0, 0, 0, 0);
+      zr[i] = gn < g.N ? ld16<kNtAux>(g.aux + (int64_t)gm * g.ldaux + gn) : make_uint4(0, 0, 0, 0);
     }
     park([&](float v, int, int) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(v)); });
     float b8[8], cs[8];
@@ -443,7 +469,7 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
           ob[j] = static_cast<__bf16>(o[j]);  // v_cvt_pk_bf16_f32 (RNE)
           cs[j] += static_cast<float>(ob[j]);  // the bias gradient sums the stored bf16 values
         }
-        *reinterpret_cast<bf16x8*>(g.C + (int64_t)gm * g.ldc + gn) = ob;
+        st16<kNtC>(g.C + (int64_t)gm * g.ldc + gn, ob);
       }
     }
     // fold the 8 lanes that share this lane's 8 columns (lane bits 3..5)
