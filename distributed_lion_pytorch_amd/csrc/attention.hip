@@ -43,6 +43,10 @@
 #ifndef DLION_DQ_NT64
 #define DLION_DQ_NT64 1
 #endif
+// DLION_ATTN_NT: O / dQ / dK / dV leave with non-temporal hints (A/B switch)
+#ifndef DLION_ATTN_NT
+#define DLION_ATTN_NT 0
+#endif
 // software-pipelined forward (D = 64) and dQ main loops
 #ifndef DLION_FWD_PIPE
 #define DLION_FWD_PIPE 0
@@ -123,6 +127,10 @@ __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ bf16x8 ld8(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ void st_bf16(__bf16* p, float v) {
+  if constexpr (DLION_ATTN_NT != 0) __builtin_nontemporal_store(static_cast<__bf16>(v), p);
+  else *p = static_cast<__bf16>(v);
+}
 // accumulator registers 8s..8s+7 as a bf16 operand fragment (k-step s).  The
 // k order this gives -- rows {0..3, 8..11} + 4hf (+16s) -- is the "permuted k"
 // every partner operand below is read in.
@@ -498,7 +506,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
       bf16x4 wv;
 #pragma unroll
       for (int i = 0; i < 4; ++i) wv[i] = static_cast<__bf16>(oacc[t][4 * g + i] * inv_l);
-      *reinterpret_cast<bf16x4*>(op + 32 * t + 8 * g + 4 * hf) = wv;
+      if constexpr (DLION_ATTN_NT != 0) __builtin_nontemporal_store(wv, reinterpret_cast<bf16x4*>(op + 32 * t + 8 * g + 4 * hf));
+      else *reinterpret_cast<bf16x4*>(op + 32 * t + 8 * g + 4 * hf) = wv;
     }
   // under dropout the stored row constant is lse + log2(1-p): the backward's
   // exp2(s*scale - lse') is then P/(1-p) directly, and with delta' = delta*(1-p)
@@ -700,7 +709,7 @@ attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int qq = qtile * 32 + acc_row(reg, hf);
-      if (qq < a.T) base[static_cast<int64_t>(qq) * a.dq_st + 32 * t + r] = static_cast<__bf16>(dq[t][reg] * a.scale);
+      if (qq < a.T) st_bf16(base + static_cast<int64_t>(qq) * a.dq_st + 32 * t + r, dq[t][reg] * a.scale);
     }
   if (a.colsum != nullptr) {
     // the c_attn bias gradient's partials: column sums of the stored (bf16) dq
@@ -947,8 +956,8 @@ attn_bwd_dkv_kernel(AttnArgs a) {
     for (int reg = 0; reg < 16; ++reg) {
       if (kb + acc_row(reg, hf) >= a.T) continue;
       const int64_t off = static_cast<int64_t>(kb + acc_row(reg, hf)) * a.dk_st + 32 * t + r;
-      dkb[off] = static_cast<__bf16>(dk[t][reg] * a.scale);
-      dvb[off] = static_cast<__bf16>(dv[t][reg]);
+      st_bf16(dkb + off, dk[t][reg] * a.scale);
+      st_bf16(dvb + off, dv[t][reg]);
     }
   if (a.colsum != nullptr) {  // bias-gradient partials of the k and v columns (H == Hkv)
     float* cs = a.colsum + static_cast<int64_t>(b * ntiles + ktile) * (3 * a.H * D) + hk * D;

@@ -80,15 +80,18 @@ __device__ __forceinline__ void glds16(const uint16_t* src, uint8_t* dst) {
                                    (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
-// Epilogue store / aux-load flavour (A/B switches, default off): DLION_GEMM_NT_AUX
-// writes / reads the MLP aux tensor (gelu'(z): written here, read once by the
-// backward) with non-temporal hints, DLION_GEMM_NT_C does the same for C, so
-// the 126 MB outputs of the K = 768 MLP GEMMs do not evict operand panels
+// Epilogue store / aux-load flavour: DLION_GEMM_NT_AUX writes / reads the MLP
+// aux tensor (gelu'(z): written here, read once by the backward) with
+// non-temporal hints, DLION_GEMM_NT_C does the same for C.  Same-box GPT-2
+// A/B: 1.019M (both off) -> 1.024M (aux) -> 1.035M tok/s (both)
+// (profiles/r3/nt_stores_ab.txt); in isolation the MLP GEMMs gain only 1-5 us,
+// the rest is what the other kernels of the step no longer lose to the
+// 126 MB outputs streaming through L2 / MALL
 #ifndef DLION_GEMM_NT_AUX
-#define DLION_GEMM_NT_AUX 0
+#define DLION_GEMM_NT_AUX 1
 #endif
 #ifndef DLION_GEMM_NT_C
-#define DLION_GEMM_NT_C 0
+#define DLION_GEMM_NT_C 1
 #endif
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 template <bool NT, typename V>
