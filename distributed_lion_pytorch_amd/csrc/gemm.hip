@@ -44,6 +44,11 @@
 // epilogue stores cost more than the hidden prologue saved.
 #include "common.h"
 
+// cache-policy bits of the operand LDS-DMA loads (A/B switch; 2 = nt on gfx950)
+#ifndef DLION_NT_LOAD_AUX
+#define DLION_NT_LOAD_AUX 0
+#endif
+
 namespace dlion {
 
 namespace {
@@ -77,7 +82,7 @@ __device__ __forceinline__ void vm_wait0() { asm volatile("s_waitcnt vmcnt(0)" :
 
 __device__ __forceinline__ void glds16(const uint16_t* src, uint8_t* dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+                                   (__attribute__((address_space(3))) void*)dst, 16, 0, DLION_NT_LOAD_AUX);
 }
 
 // Epilogue store / aux-load flavour: DLION_GEMM_NT_AUX writes / reads the MLP
