@@ -714,27 +714,35 @@ def _nt_candidates(a: torch.Tensor, b_nk: torch.Tensor, prefix: str, bias=None) 
     return c
 
 
-def _pick(key, cands: dict) -> str:
+def _pick(key, cands: dict, rounds: int = 3, reps: int = 3) -> str:
+    """Measured-fastest candidate for ``key``, cached: ``rounds`` interleaved
+    rounds of ``reps`` calls each, the best round per candidate (a single
+    3-call sample let clock ramps / interference flip the choice between runs)."""
     name = _GEMM_PICK.get(key)
     if name is not None and name in cands:
         return name
-    best, best_t = None, None
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    live = {}
     for n, fn in cands.items():
         try:
             fn()  # warm-up (also tunes lt_gemm's algorithm for the shape)
-            ev0.record()
-            for _ in range(3):
-                fn()
-            ev1.record()
-            ev1.synchronize()
-            t = ev0.elapsed_time(ev1)
+            live[n] = float("inf")
         except RuntimeError:
             continue
-        if best_t is None or t < best_t:
-            best, best_t = n, t
-    if best is None:  # nothing ran: the first candidate (ATen) raises its own error when called
-        best = next(iter(cands))
+    for _ in range(rounds):
+        for n in list(live):
+            try:
+                ev0.record()
+                for _ in range(reps):
+                    cands[n]()
+                ev1.record()
+                ev1.synchronize()
+            except RuntimeError:
+                del live[n]
+                continue
+            live[n] = min(live[n], ev0.elapsed_time(ev1))
+    # nothing ran: the first candidate (ATen) raises its own error when called
+    best = min(live, key=live.get) if live else next(iter(cands))
     _GEMM_PICK[key] = best
     return best
 
