@@ -5,7 +5,8 @@ There is no network in this environment (no hub tokenizers or datasets), so:
 * :class:`ByteTokenizer` is a dependency-free HF-style tokenizer (UTF-8 bytes +
   BOS/EOS/PAD) used when no local tokenizer directory is given;
 * ``synthetic_*`` build deterministic datasets of the reference's shapes:
-  CLM token blocks (run_clm.py:509-544 group_texts), stack-exchange-like
+  CLM token blocks (run_clm.py:509-544 group_texts; ``clm_blocks`` groups real
+  text the same way), stack-exchange-like
   "Question/Answer" SFT text (sft_llama2.py:93-96) and prompt/chosen/rejected
   DPO triples (dpo_llama2.py:84-125).
 """
@@ -95,23 +96,103 @@ class SyntheticCLMDataset(Dataset):
         return {"input_ids": ids, "labels": ids.clone()}
 
 
-class BlockDataset(Dataset):
-    """Concatenate tokenized texts and chunk into block_size (run_clm group_texts)."""
+# The reference's CLM preprocessing (run_clm.py:463-544): ``datasets.map`` of
+# the tokenizer, then of group_texts, both ``batched=True`` -- i.e. per batch
+# of 1000 texts the token lists are concatenated (no separator token) and cut
+# into block_size chunks, the remainder of EACH batch dropped -- with
+# ``num_proc=preprocessing_num_workers`` and ``load_from_cache_file=not
+# overwrite_cache``.  Same stream here, without the hub datasets machinery:
+# batches tokenized in a spawn-started worker pool (no fork of a process that
+# may hold a GPU context) and the resulting blocks cached as one .npy keyed by
+# the texts, the tokenizer and block_size.
+MAP_BATCH = 1000
 
-    def __init__(self, token_lists: Iterable[Sequence[int]], block_size: int, eos: Optional[int] = None):
-        flat: List[int] = []
-        for ids in token_lists:
-            flat.extend(ids)
-            if eos is not None:
-                flat.append(eos)
-        n = len(flat) // block_size
-        self.data = torch.tensor(flat[: n * block_size], dtype=torch.long).view(n, block_size)
+
+class TokenBlocks(Dataset):
+    """[n, block_size] token blocks as {'input_ids', 'labels'} rows."""
+
+    def __init__(self, blocks: torch.Tensor):
+        self.data = blocks
 
     def __len__(self):
         return self.data.shape[0]
 
     def __getitem__(self, i):
-        return {"input_ids": self.data[i], "labels": self.data[i].clone()}
+        ids = self.data[i].long()
+        return {"input_ids": ids, "labels": ids.clone()}
+
+
+def _group_batch(token_lists: Sequence[Sequence[int]], block_size: int) -> List[List[int]]:
+    flat: List[int] = []
+    for ids in token_lists:
+        flat.extend(ids)
+    n = len(flat) // block_size
+    return [flat[i * block_size:(i + 1) * block_size] for i in range(n)]
+
+
+_POOL_TOKENIZER = None
+
+
+def _pool_init(tokenizer):
+    global _POOL_TOKENIZER
+    _POOL_TOKENIZER = tokenizer
+
+
+def _pool_batch(args):
+    texts, block_size = args
+    return _group_batch(_POOL_TOKENIZER(list(texts))["input_ids"], block_size)
+
+
+def _blocks_cache_key(texts: Sequence[str], tokenizer, block_size: int) -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    ident = (type(tokenizer).__name__, str(getattr(tokenizer, "name_or_path", "")), len(tokenizer), block_size, MAP_BATCH)
+    h.update(repr(ident).encode())
+    for t in texts:
+        h.update(t.encode("utf-8", "surrogatepass"))
+        h.update(b"\x00")
+    return h.hexdigest()[:24]
+
+
+def default_cache_dir() -> str:
+    base = os.environ.get("HF_DATASETS_CACHE") or os.path.join(
+        os.environ.get("HF_HOME", os.path.join(os.path.expanduser("~"), ".cache", "huggingface")), "datasets")
+    return os.path.join(base, "dlion_clm")
+
+
+def clm_blocks(texts: Sequence[str], tokenizer, block_size: int, num_workers: Optional[int] = None,
+               cache_dir: Optional[str] = None, overwrite_cache: bool = False) -> TokenBlocks:
+    """Tokenize + group ``texts`` exactly as the reference's two batched maps do
+    (see above).  ``num_workers`` > 1 tokenizes batches in parallel processes;
+    ``cache_dir`` (None: no cache) holds the blocks for reuse unless
+    ``overwrite_cache``."""
+    import numpy as np
+
+    texts = list(texts)
+    path = None
+    if cache_dir is not None:
+        path = os.path.join(cache_dir, f"clm-{_blocks_cache_key(texts, tokenizer, block_size)}.npy")
+        if not overwrite_cache and os.path.isfile(path):
+            return TokenBlocks(torch.from_numpy(np.load(path)))
+    batches = [texts[i:i + MAP_BATCH] for i in range(0, len(texts), MAP_BATCH)]
+    if num_workers is not None and num_workers > 1 and len(batches) > 1:
+        import multiprocessing as mp
+
+        with mp.get_context("spawn").Pool(min(num_workers, len(batches)), initializer=_pool_init,
+                                          initargs=(tokenizer,)) as pool:
+            grouped = pool.map(_pool_batch, [(b, block_size) for b in batches])
+    else:
+        grouped = [_group_batch(tokenizer(b)["input_ids"], block_size) for b in batches]
+    rows = [r for g in grouped for r in g]
+    dtype = np.int32 if len(tokenizer) < 2 ** 31 else np.int64
+    arr = np.asarray(rows, dtype=dtype).reshape(len(rows), block_size)
+    if path is not None:
+        os.makedirs(cache_dir, exist_ok=True)
+        tmp = f"{path}.{os.getpid()}.tmp.npy"
+        np.save(tmp, arr)
+        os.replace(tmp, path)  # atomic: ranks that read concurrently see a whole file or none
+    return TokenBlocks(torch.from_numpy(arr))
 
 
 # ---------------------------------------------------------------- SFT data

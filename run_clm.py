@@ -36,7 +36,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from distributed_lion_pytorch_amd.models.registry import build_model, load_config  # noqa: E402
 from distributed_lion_pytorch_amd.trainer.async_trainer import (  # noqa: E402
     AsyncTrainer, AsyncTrainingArguments, build_lion, warn_unsynced)
-from distributed_lion_pytorch_amd.utils.data import BlockDataset, SyntheticCLMDataset, load_tokenizer  # noqa: E402
+from distributed_lion_pytorch_amd.utils.data import SyntheticCLMDataset, clm_blocks, default_cache_dir, load_tokenizer  # noqa: E402
 from distributed_lion_pytorch_amd.utils.metrics import JsonlMetricsCallback  # noqa: E402
 
 logger = logging.getLogger(__name__)
@@ -90,8 +90,19 @@ def split_train_validation(texts, pct: int):
     return texts[n_val:], texts[:n_val]
 
 
-def _blocks(texts, tokenizer, block_size):
-    return BlockDataset([tokenizer(t)["input_ids"] for t in texts], block_size, eos=tokenizer.eos_token_id)
+def _blocks(texts, tokenizer, block_size, data_args=None, train_args=None):
+    """Tokenize + group_texts as the reference's two batched ``datasets.map``
+    calls (run_clm.py:463-544: 1000-text batches, no separator, per-batch
+    remainder dropped), honouring ``preprocessing_num_workers`` and
+    ``overwrite_cache``; ranks other than the main one wait and read the cache."""
+    workers = getattr(data_args, "preprocessing_num_workers", None)
+    overwrite = bool(getattr(data_args, "overwrite_cache", False))
+    cache = default_cache_dir()
+    first = getattr(train_args, "main_process_first", None)
+    if first is None:
+        return clm_blocks(texts, tokenizer, block_size, workers, cache, overwrite)
+    with first(desc="dataset map tokenization"):
+        return clm_blocks(texts, tokenizer, block_size, workers, cache, overwrite)
 
 
 def _cap(ds, n: Optional[int]):
@@ -117,8 +128,8 @@ def build_datasets(data_args, train_args, tokenizer, vocab_size, block_size):
                 tr, va = list(raw["train"][col]), list(raw["validation"][col])
             else:
                 tr, va = split_train_validation(list(raw["train"][col]), pct)
-            return (_cap(_blocks(tr, tokenizer, block_size), data_args.max_train_samples),
-                    _cap(_blocks(va, tokenizer, block_size), data_args.max_eval_samples))
+            return (_cap(_blocks(tr, tokenizer, block_size, data_args, train_args), data_args.max_train_samples),
+                    _cap(_blocks(va, tokenizer, block_size, data_args, train_args), data_args.max_eval_samples))
         except Exception as e:  # offline: no hub datasets
             logger.warning("dataset %s unavailable offline (%s); falling back to synthetic data",
                            data_args.dataset_name, e)
@@ -128,8 +139,8 @@ def build_datasets(data_args, train_args, tokenizer, vocab_size, block_size):
             va = _read_text(data_args.validation_file, data_args.keep_linebreaks)
         else:
             tr, va = split_train_validation(tr, pct)
-        return (_cap(_blocks(tr, tokenizer, block_size), data_args.max_train_samples),
-                _cap(_blocks(va, tokenizer, block_size), data_args.max_eval_samples))
+        return (_cap(_blocks(tr, tokenizer, block_size, data_args, train_args), data_args.max_train_samples),
+                _cap(_blocks(va, tokenizer, block_size, data_args, train_args), data_args.max_eval_samples))
     n_train = data_args.max_train_samples or data_args.synthetic_samples
     n_eval = data_args.max_eval_samples or max(8, n_train // 20)
     # disjoint by construction: the eval set is drawn from a different seed

@@ -1,7 +1,9 @@
 """run_clm.py data-pipeline fidelity to /root/reference/run_clm.py:
 disjoint train/validation splits (``train[:p%]`` / ``train[p%:]``, or the
 dataset's own validation split), ``max_train/eval_samples`` on real data,
-``--streaming`` refused, embedding resize for a larger tokenizer, model card."""
+``--streaming`` refused, embedding resize for a larger tokenizer, model card,
+group_texts over 1000-text batches (no separator token),
+``preprocessing_num_workers`` and ``overwrite_cache``."""
 import os
 import re
 import sys
@@ -13,7 +15,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 import run_clm  # noqa: E402
+from distributed_lion_pytorch_amd.utils import data as data_mod  # noqa: E402
 from distributed_lion_pytorch_amd.utils.data import ByteTokenizer  # noqa: E402
+
+
+@pytest.fixture(autouse=True)
+def _private_cache(tmp_path, monkeypatch):
+    monkeypatch.setenv("HF_DATASETS_CACHE", str(tmp_path / "hf_datasets"))
 
 BASE = ["--report_to", "none", "--use_cpu", "--config_name", "gpt2-tiny", "--per_device_train_batch_size", "2",
         "--learning_rate", "1e-3", "--warmup_steps", "1", "--lion", "--async_grad"]
@@ -93,3 +101,56 @@ def test_embeddings_resized_for_larger_tokenizer(tmp_path):
     assert model.config.vocab_size == 259
     assert model.get_output_embeddings().weight is model.get_input_embeddings().weight  # still tied
     assert os.path.isfile(os.path.join(out, "README.md"))  # model card
+
+
+def _reference_group_texts(texts, tok, block_size):
+    """/root/reference/run_clm.py:463-544 restated: tokenizer map then group_texts
+    map, both batched (1000 texts), remainder of each batch dropped."""
+    from itertools import chain
+
+    out = []
+    for i in range(0, len(texts), 1000):
+        ids = tok(texts[i:i + 1000])["input_ids"]
+        flat = list(chain(*ids))
+        n = len(flat) // block_size * block_size
+        out += [flat[j:j + block_size] for j in range(0, n, block_size)]
+    return out
+
+
+def test_group_texts_matches_reference_batches():
+    tok = ByteTokenizer()
+    texts = [f"line {i} " + "z" * (i % 37) for i in range(2500)]
+    ds = data_mod.clm_blocks(texts, tok, 64)
+    ref = _reference_group_texts(texts, tok, 64)
+    assert len(ds) == len(ref) and all(ds[i]["input_ids"].tolist() == ref[i] for i in range(len(ref)))
+    assert tok.eos_token_id not in ds.data  # no separator token between texts (reference parity)
+
+
+def test_preprocessing_workers_match_serial():
+    tok = ByteTokenizer()
+    texts = [f"w {i} " + "q" * (i % 11) for i in range(2300)]
+    a = data_mod.clm_blocks(texts, tok, 32)
+    b = data_mod.clm_blocks(texts, tok, 32, num_workers=2)
+    assert torch.equal(a.data, b.data)
+
+
+class _CountingTok(ByteTokenizer):
+    calls = 0
+
+    def __call__(self, text, **kw):
+        type(self).calls += 1
+        return super().__call__(text, **kw)
+
+
+def test_cache_hit_and_overwrite_cache(tmp_path):
+    tok = _CountingTok()
+    texts = [f"c {i} " + "y" * 20 for i in range(1500)]
+    cache = str(tmp_path / "cache")
+    first = data_mod.clm_blocks(texts, tok, 32, cache_dir=cache)
+    n = _CountingTok.calls
+    again = data_mod.clm_blocks(texts, tok, 32, cache_dir=cache)
+    assert _CountingTok.calls == n and torch.equal(first.data, again.data)  # served from the cache
+    data_mod.clm_blocks(texts, tok, 32, cache_dir=cache, overwrite_cache=True)
+    assert _CountingTok.calls > n  # recomputed
+    other = data_mod.clm_blocks(texts[:-1], tok, 32, cache_dir=cache)  # different texts: different key
+    assert len(os.listdir(cache)) == 2 and len(other) <= len(first)
