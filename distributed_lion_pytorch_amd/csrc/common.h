@@ -150,6 +150,42 @@ __device__ __forceinline__ void store8g(typename Elem<DT>::S* base, int64_t e, i
   }
 }
 
+// ------------------------------------------------------- wave reductions
+// Full-wave fp32 sum / max, the result in every lane, without LDS: two
+// quad_perm DPP ops and two row_ror DPP ops leave each 16-lane row's result in
+// its lanes; the four row results are read with v_readlane and combined
+// (wave-uniform).  __shfl_xor lowers to six dependent ds_bpermute round trips.
+// (Recombining rows with the permlane16/32 swap builtins on identical operands
+// came out of hipcc as r[0] op r[0] in one kernel -- wrong -- so no swaps.)
+template <bool MAX>
+__device__ __forceinline__ float dpp_step(float v, int sel) {
+  const int x = __builtin_bit_cast(int, v);
+  int y;
+  switch (sel) {  // the DPP control must be an immediate
+    case 0: y = __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false); break;   // quad_perm [1,0,3,2]
+    case 1: y = __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false); break;   // quad_perm [2,3,0,1]
+    case 2: y = __builtin_amdgcn_update_dpp(0, x, 0x124, 0xF, 0xF, false); break;  // row_ror:4
+    default: y = __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false); break; // row_ror:8
+  }
+  const float o = __builtin_bit_cast(float, y);
+  return MAX ? fmaxf(v, o) : v + o;
+}
+template <bool MAX>
+__device__ __forceinline__ float wave_reduce_dpp(float v) {
+  v = dpp_step<MAX>(v, 0);
+  v = dpp_step<MAX>(v, 1);
+  v = dpp_step<MAX>(v, 2);
+  v = dpp_step<MAX>(v, 3);
+  const int x = __builtin_bit_cast(int, v);
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(x, 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(x, 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(x, 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(x, 48));
+  return MAX ? fmaxf(fmaxf(r0, r1), fmaxf(r2, r3)) : (r0 + r1) + (r2 + r3);
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) { return wave_reduce_dpp<false>(v); }
+__device__ __forceinline__ float wave_max_dpp(float v) { return wave_reduce_dpp<true>(v); }
+
 // ------------------------------------------------------------------- GELU
 // tanh via one v_exp_f32 + one v_rcp_f32 (libm tanhf is a ~30-instruction
 // polynomial path and made the memory-bound bias+GELU kernels VALU-bound);

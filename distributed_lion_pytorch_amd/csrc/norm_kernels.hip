@@ -24,11 +24,9 @@
 namespace dlion {
 
 
-__device__ __forceinline__ float wsum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
+// full-wave sum without LDS (common.h wave_sum_dpp): __shfl_xor lowered to six
+// dependent ds_bpermute round trips per reduction, two reductions per row
+__device__ __forceinline__ float wsum(float v) { return wave_sum_dpp(v); }
 
 __device__ __forceinline__ void unpack4(const uint2 v, float (&o)[4]) {
   o[0] = bf16_to_f32(v.x & 0xffffu);
@@ -102,16 +100,36 @@ add_norm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__
   const int64_t row = static_cast<int64_t>(blockIdx.x) * RowGroup<WPR>::kRows + threadIdx.x / G;
   if (row >= rows) return;  // uniform per row group (the whole block when WPR > 1)
   const int64_t base = row * C;
+  // every load of the row is issued before any use (with the null checks
+  // inside the k loop, hipcc waited vmcnt(0) per chunk: six serial round
+  // trips per row); gamma / beta too, ahead of the reductions
+  uint2 rx[NS], ry[NS], rb[NS], rg[NS], re[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) rx[k] = *reinterpret_cast<const uint2*>(x + base + k * 4 * G + tg * 4);
+  const bool has_y = y != nullptr, has_b = has_y && bias != nullptr;
+  if (has_y) {
+#pragma unroll
+    for (int k = 0; k < NS; ++k) ry[k] = *reinterpret_cast<const uint2*>(y + base + k * 4 * G + tg * 4);
+  }
+  if (has_b) {
+#pragma unroll
+    for (int k = 0; k < NS; ++k) rb[k] = *reinterpret_cast<const uint2*>(bias + k * 4 * G + tg * 4);
+  }
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    rg[k] = *reinterpret_cast<const uint2*>(gamma + k * 4 * G + tg * 4);
+    if constexpr (!RMS) re[k] = *reinterpret_cast<const uint2*>(beta + k * 4 * G + tg * 4);
+  }
   float v[NS][4];
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < NS; ++k) {
     const int c = k * 4 * G + tg * 4;
-    ld4(x + base + c, v[k]);
-    if (y != nullptr) {
+    unpack4(rx[k], v[k]);
+    if (has_y) {
       float yv[4], bv[4] = {0.f, 0.f, 0.f, 0.f};
-      ld4(y + base + c, yv);
-      if (bias != nullptr) ld4(bias + c, bv);
+      unpack4(ry[k], yv);
+      if (has_b) unpack4(rb[k], bv);
       const uint32_t kp = thresh16 ? keep4(seed, static_cast<uint64_t>(base + c), thresh16) : 0xfu;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -138,8 +156,8 @@ add_norm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__
   for (int k = 0; k < NS; ++k) {
     const int c = k * 4 * G + tg * 4;
     float g[4], b[4] = {0.f, 0.f, 0.f, 0.f}, o[4];
-    ld4(gamma + c, g);
-    if constexpr (!RMS) ld4(beta + c, b);
+    unpack4(rg[k], g);
+    if constexpr (!RMS) unpack4(re[k], b);
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = (v[k][j] - mean) * rstd * g[j] + b[j];
     st4(h + base + c, o);

@@ -22,16 +22,9 @@ namespace dlion {
 constexpr int kXentThreads = 1024;
 constexpr int kXentWaves = kXentThreads / 64;
 
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
-}
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
+// DPP / readlane wave reductions (common.h), no ds_bpermute chains
+__device__ __forceinline__ float wave_max(float v) { return wave_max_dpp(v); }
+__device__ __forceinline__ float wave_sum(float v) { return wave_sum_dpp(v); }
 
 template <int DT, int VPT>
 __global__ void __launch_bounds__(kXentThreads)
