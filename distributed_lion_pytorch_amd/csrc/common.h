@@ -194,30 +194,38 @@ __device__ __forceinline__ float fast_tanh(float a) {
   const float e = __builtin_amdgcn_exp2f(a * 2.8853900817779268f);  // exp(2a)
   return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
 }
-// GELU: exact = erf form (nn.GELU()), else the tanh approximation (gelu_new).
-// Shared by the bias+GELU kernels and the GEMM epilogue (bitwise-identical).
-__device__ __forceinline__ float gelu_f(float u, bool exact) {
-  if (exact) return 0.5f * u * (1.f + erff(u * 0.7071067811865476f));
-  const float t = fast_tanh(0.7978845608028654f * (u + 0.044715f * u * u * u));
-  return 0.5f * u * (1.f + t);
-}
-
-// d gelu(u) / du, matching gelu_f (shared by the bias+GELU backward kernel and
-// the GEMM's DGELU epilogue)
 constexpr float kSqrt2OverPi = 0.7978845608028654f;
 constexpr float kKappa = 0.044715f;
 constexpr float kInvSqrt2 = 0.7071067811865476f;
 constexpr float kInvSqrt2Pi = 0.3989422804014327f;
+constexpr float kLog2e = 1.4426950408889634f;
+// tanh-approximate GELU in its sigmoid form: 0.5 u (1 + tanh y) = u s with
+// s = 1 / (1 + exp(-2y)), y = sqrt(2/pi) (u + kappa u^3); the exponent's
+// constants fold into one FMA on u^2.  Saturates correctly (exp2 -> inf: s = 0).
+__device__ __forceinline__ float gelu_sig(float u, float u2) {
+  const float a = u * __builtin_fmaf(u2, -2.f * kSqrt2OverPi * kKappa * kLog2e, -2.f * kSqrt2OverPi * kLog2e);
+  return __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(a) + 1.f);
+}
+// GELU: exact = erf form (nn.GELU()), else the tanh approximation (gelu_new).
+// Shared by the bias+GELU kernels and the GEMM epilogues (bitwise-identical).
+__device__ __forceinline__ float gelu_f(float u, bool exact) {
+  if (exact) return 0.5f * u * (1.f + erff(u * 0.7071067811865476f));
+  return u * gelu_sig(u, u * u);
+}
 
+// d gelu(u) / du, matching gelu_f (shared by the bias+GELU backward kernel and
+// the GEMM's DGELU epilogue): s + 2k u s (1 - s) (1 + 3 kappa u^2)
 __device__ __forceinline__ float gelu_grad(float u, bool exact) {
   if (exact) return 0.5f * (1.f + erff(u * kInvSqrt2)) + u * kInvSqrt2Pi * __expf(-0.5f * u * u);
   const float u2 = u * u;
-  const float t = fast_tanh(kSqrt2OverPi * (u + kKappa * u2 * u));
-  return 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * kSqrt2OverPi * (1.f + 3.f * kKappa * u2);
+  const float s = gelu_sig(u, u2);
+  const float q = u * __builtin_fmaf(u2, 6.f * kSqrt2OverPi * kKappa, 2.f * kSqrt2OverPi);
+  return __builtin_fmaf(q, __builtin_fmaf(-s, s, s), s);
 }
 
-// gelu(u) and gelu'(u) from one tanh / erf (the GEMM's GELU epilogue that
-// stores the derivative for the backward instead of the pre-activation)
+// gelu(u) and gelu'(u) from one exp / rcp (or erf): the GEMM's GELU epilogue
+// that stores the derivative for the backward instead of the pre-activation
+// (8 VALU + 2 transcendental per element; the tanh form took ~17 + 2)
 __device__ __forceinline__ void gelu_and_grad(float u, bool exact, float& g, float& dg) {
   if (exact) {
     const float e = erff(u * kInvSqrt2);
@@ -226,9 +234,10 @@ __device__ __forceinline__ void gelu_and_grad(float u, bool exact, float& g, flo
     return;
   }
   const float u2 = u * u;
-  const float t = fast_tanh(kSqrt2OverPi * (u + kKappa * u2 * u));
-  g = 0.5f * u * (1.f + t);
-  dg = 0.5f * (1.f + t) + 0.5f * u * (1.f - t * t) * kSqrt2OverPi * (1.f + 3.f * kKappa * u2);
+  const float s = gelu_sig(u, u2);
+  g = u * s;
+  const float q = u * __builtin_fmaf(u2, 6.f * kSqrt2OverPi * kKappa, 2.f * kSqrt2OverPi);
+  dg = __builtin_fmaf(q, __builtin_fmaf(-s, s, s), s);
 }
 
 // ------------------------------------------------------------ vote counting
