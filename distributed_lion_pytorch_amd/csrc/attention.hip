@@ -51,6 +51,10 @@
 #ifndef DLION_FWD_PIPE
 #define DLION_FWD_PIPE 0
 #endif
+// dQ with NT > 1: process the NT tiles of a barrier interval one after the other
+#ifndef DLION_DQ_SEQ
+#define DLION_DQ_SEQ 0
+#endif
 #ifndef DLION_DQ_PIPE
 #define DLION_DQ_PIPE 0
 #endif
@@ -654,7 +658,46 @@ attn_bwd_dq_kernel(AttnArgs a) {
     __syncthreads();  // ... for every wave; and every wave is done with the buffer restaged next
     if (st + NB - 1 < ns) stage(st + NB - 1, (st + NB - 1) % NB);
     const int kt0 = st * NT;
-    if (blk.active && kt0 <= qtile) {
+    if (DLION_DQ_SEQ && NT > 1) {
+      // NT tiles per barrier processed one after the other in one register
+      // set: only the barrier count drops (no second S / dP chain)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int kt = kt0 + j;
+        if (!(blk.active && kt <= qtile)) continue;  // wave-uniform (past-the-diagonal tiles: skipped)
+        const int kb = kt * 32;
+        f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) {
+          s = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), qf[ks], s);
+          dp = mfma32(row_frag<D>(vs_[buf][j], r, ks, hf), dof[ks], dp);
+        }
+        if (kt == qtile) {
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg)
+            if (kb + acc_row(reg, hf) > q) s[reg] = -INFINITY;
+        }
+#pragma unroll
+        for (int reg = 0; reg < 16; reg += 2) {
+          const int key = kb + acc_row(reg, hf);
+          uint32_t hsh = 0;
+          if constexpr (DROP) hsh = mix1(arow ^ ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u));
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg + e], a.scale_log2, -lse2));
+            float dpv = dp[reg + e];
+            if constexpr (DROP) dpv = ((e == 0 ? hsh << 16 : hsh) >= thr_hi) ? dpv : 0.f;
+            s[reg + e] = p * (dpv - dlt);
+          }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 dsf = acc_frag(s, s2);
+#pragma unroll
+          for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tr_frag<D>(ks_[buf][j], s2, t, lane), dq[t]);
+        }
+      }
+    } else if (blk.active && kt0 <= qtile) {
       // NT independent S / dP chains: one tile's exp / hash VALU work can sit
       // beside the other's MFMAs
       f32x16 s[NT], dp[NT];
