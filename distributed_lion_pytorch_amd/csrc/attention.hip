@@ -48,6 +48,10 @@
 #define DLION_ATTN_NT 0
 #endif
 // software-pipelined forward (D = 64) and dQ main loops
+// key tiles per barrier in the D = 64 forward
+#ifndef DLION_FWD_NT64
+#define DLION_FWD_NT64 2
+#endif
 #ifndef DLION_FWD_PIPE
 #define DLION_FWD_PIPE 0
 #endif
@@ -1038,7 +1042,7 @@ hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
 #if DLION_FWD_PIPE
     FWD(64, 1, true)
 #else
-    FWD(64, 2, false)
+    FWD(64, DLION_FWD_NT64, false)
 #endif
   } else if (D == 128) {
     FWD(128, 1, false)
