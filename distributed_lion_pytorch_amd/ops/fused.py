@@ -1058,6 +1058,7 @@ def _lm_dgrad(g: torch.Tensor, weight: torch.Tensor, wp: torch.Tensor) -> torch.
 
 
 _LM_TN = os.environ.get("DLION_LM_TN", "1") != "0"  # A/B switch for _lm_wgrad_partials
+_LM_FWD_OWN = os.environ.get("DLION_LM_FWD_OWN", "0") == "1"  # A/B switch: LM-head logits on the own NT GEMM
 
 
 def _lm_wgrad_partials(g: torch.Tensor, h2d: torch.Tensor, v: int):
@@ -1088,7 +1089,10 @@ class _LMHeadCE(torch.autograd.Function):
         v = weight.shape[0]
         need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         wp = _pad_rows(weight)
-        logits = gemm_fwd(h2d, wp)  # [N, Vp] in the compute dtype
+        if _LM_FWD_OWN and h2d.is_cuda and hip.available() and h2d.dtype == torch.bfloat16 and h2d.shape[1] % 128 == 0:
+            logits = hip.ops().gemm_nt(h2d.contiguous(), wp, None)  # own NT GEMM, non-temporal C stores
+        else:
+            logits = gemm_fwd(h2d, wp)  # [N, Vp] in the compute dtype
         if normalizer is None:
             n_valid = (labels1d != -100).sum().clamp_min(1).to(torch.float32)
         else:

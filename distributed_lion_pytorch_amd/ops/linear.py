@@ -684,6 +684,7 @@ def transposed_weight(w: torch.Tensor) -> torch.Tensor:
 _AUTOTUNE = os.environ.get("DLION_GEMM_AUTOTUNE", "1") != "0"
 _TUNE_MIN_FLOP = float(2 ** 34)
 _GEMM_PICK: dict = {}  # key -> candidate name
+_GEMM_FORCE = os.environ.get("DLION_GEMM_FORCE", "")
 
 
 def _own_nt_ok(a: torch.Tensor, b_nk: torch.Tensor) -> bool:
@@ -721,6 +722,10 @@ def _pick(key, cands: dict, rounds: int = 3, reps: int = 3) -> str:
     name = _GEMM_PICK.get(key)
     if name is not None and name in cands:
         return name
+    forced = [n for n in cands if _GEMM_FORCE and n.endswith(_GEMM_FORCE)]
+    if forced:  # A/B switch: DLION_GEMM_FORCE=own | lt | aten pins that candidate wherever it exists
+        _GEMM_PICK[key] = forced[0]
+        return forced[0]
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     live = {}
     for n, fn in cands.items():
