@@ -47,6 +47,17 @@ __device__ __forceinline__ void ld4(const uint16_t* p, float (&o)[4]) {
 #define DLION_NORM_NT 0
 #endif
 typedef unsigned int norm_u32x2 __attribute__((ext_vector_type(2)));
+// DLION_NORM_NTLOAD: the row streams read once (x, y forward; dh, xo, dxo
+// backward) with non-temporal hints (A/B switch)
+#ifndef DLION_NORM_NTLOAD
+#define DLION_NORM_NTLOAD 0
+#endif
+__device__ __forceinline__ uint2 ldrow(const uint16_t* p) {
+  norm_u32x2 v;
+  if constexpr (DLION_NORM_NTLOAD != 0) v = __builtin_nontemporal_load(reinterpret_cast<const norm_u32x2*>(p));
+  else v = *reinterpret_cast<const norm_u32x2*>(p);
+  return make_uint2(v[0], v[1]);
+}
 __device__ __forceinline__ void st4(uint16_t* p, const float (&o)[4]) {
   norm_u32x2 v;
   v[0] = static_cast<uint32_t>(f32_to_bf16(o[0])) | (static_cast<uint32_t>(f32_to_bf16(o[1])) << 16);
@@ -105,11 +116,11 @@ add_norm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__
   // trips per row); gamma / beta too, ahead of the reductions
   uint2 rx[NS], ry[NS], rb[NS], rg[NS], re[NS];
 #pragma unroll
-  for (int k = 0; k < NS; ++k) rx[k] = *reinterpret_cast<const uint2*>(x + base + k * 4 * G + tg * 4);
+  for (int k = 0; k < NS; ++k) rx[k] = ldrow(x + base + k * 4 * G + tg * 4);
   const bool has_y = y != nullptr, has_b = has_y && bias != nullptr;
   if (has_y) {
 #pragma unroll
-    for (int k = 0; k < NS; ++k) ry[k] = *reinterpret_cast<const uint2*>(y + base + k * 4 * G + tg * 4);
+    for (int k = 0; k < NS; ++k) ry[k] = ldrow(y + base + k * 4 * G + tg * 4);
   }
   if (has_b) {
 #pragma unroll
@@ -202,9 +213,9 @@ add_norm_bwd_kernel(const uint16_t* __restrict__ dh, const uint16_t* __restrict_
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
       const int c = k * 4 * G + tg * 4;
-      nxo[k] = *reinterpret_cast<const uint2*>(xo + b + c);
-      ndh[k] = *reinterpret_cast<const uint2*>(dh + b + c);
-      if (dxo_in != nullptr) ndx[k] = *reinterpret_cast<const uint2*>(dxo_in + b + c);
+      nxo[k] = ldrow(xo + b + c);
+      ndh[k] = ldrow(dh + b + c);
+      if (dxo_in != nullptr) ndx[k] = ldrow(dxo_in + b + c);
     }
     nmean = RMS ? 0.f : mean_in[r];
     nrstd = rstd_in[r];
