@@ -1059,6 +1059,7 @@ def _lm_dgrad(g: torch.Tensor, weight: torch.Tensor, wp: torch.Tensor) -> torch.
 
 _LM_TN = os.environ.get("DLION_LM_TN", "1") != "0"  # A/B switch for _lm_wgrad_partials
 _LM_FWD_OWN = os.environ.get("DLION_LM_FWD_OWN", "0") == "1"  # A/B switch: LM-head logits on the own NT GEMM
+_LM_DEFER = os.environ.get("DLION_LM_DEFER", "1") != "0"  # LM-head weight gradient in the window-level TN GEMM
 
 
 def _lm_wgrad_partials(g: torch.Tensor, h2d: torch.Tensor, v: int):
@@ -1107,6 +1108,15 @@ class _LMHeadCE(torch.autograd.Function):
             dh = _lm_dgrad(logits, weight, wp)  # [N, C]
             dw = None
             ctx.dw_parts = False
+            ctx.defer = ctx.needs_input_grad[1] and _lm_defer_ok(weight, logits, h2d)
+            if ctx.defer:
+                # the weight gradient joins the fusion window: the backward scales h by
+                # the loss gradient and hands (softmax - onehot, s * h) to the window's
+                # single TN GEMM over all micro-batches (ops/linear.py deferral)
+                ctx.save_for_backward(dh, logits, n_valid, h2d)
+                ctx.has_dw = True
+                ctx.weight = weight
+                return loss
             if ctx.needs_input_grad[1]:
                 dw = _lm_wgrad_partials(logits, h2d, v)
                 ctx.dw_parts = dw is not None
@@ -1122,6 +1132,8 @@ class _LMHeadCE(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if getattr(ctx, "defer", False):
+            return _LMHeadCE._backward_deferred(ctx, g)
         dh, dw, n_valid = ctx.saved_tensors
         if not (dh.is_cuda and dh.dtype == torch.bfloat16 and _use_hip(dh)):
             scale = (g / n_valid).to(dh.dtype)
@@ -1161,6 +1173,40 @@ class _LMHeadCE(torch.autograd.Function):
                 else:
                     gw = out
         return gh, gw, None, None
+
+
+def _lm_defer_ok(weight, logits, h2d) -> bool:
+    """The LM head's weight gradient can join the window-level TN GEMM: a
+    multi-micro-batch fusion window, a fusable bf16 weight, TN-eligible operands."""
+    from . import linear
+
+    return (_LM_DEFER and _LM_TN and logits.is_cuda and linear._WDEFER_ON and linear._ST.fuse["on"]
+            and linear._ST.fuse["multi"] and not linear._ST.fuse["nodefer"] and linear._fuse_target(weight)
+            and logits.shape[1] % 8 == 0 and linear._tn_eligible(logits, h2d) and hip.available())
+
+
+def _lm_backward_deferred(ctx, g):
+    from . import linear
+
+    dh, logits, n_valid, h2d = ctx.saved_tensors
+    s = (g.float() / n_valid).reshape(1)
+    ops = hip.ops()
+    gh = None
+    if ctx.needs_input_grad[0]:
+        gh = torch.empty_like(dh)
+        ops.scale_acc_(dh, s, gh, False)
+    w = ctx.weight
+    v, c = w.shape
+    hs = torch.empty_like(h2d)  # s * h: the per-micro-batch loss scale rides on the small operand
+    ops.scale_acc_(h2d.contiguous(), s, hs, False)
+    split = linear.tn_split_factor(logits.shape[0], logits.shape[1], c)
+    if not linear._defer_wgrad([w], [(0, v * c)], logits, hs, split):
+        part = ops.gemm_tn([logits], [hs], split)  # over budget / window closed: now
+        linear.deposit_grad(w, part.view(split, -1)[:, : v * c], defer=False)
+    return gh, None, None, None
+
+
+_LMHeadCE._backward_deferred = staticmethod(_lm_backward_deferred)
 
 
 def _softmax_xent_torch_(logits: torch.Tensor, labels: torch.Tensor, v: int) -> torch.Tensor:
