@@ -98,6 +98,9 @@ __device__ __forceinline__ void glds16(const uint16_t* src, uint8_t* dst) {
 #ifndef DLION_GEMM_NT_C
 #define DLION_GEMM_NT_C 1
 #endif
+#ifndef DLION_GEMM_NT_C_PLAIN
+#define DLION_GEMM_NT_C_PLAIN 0
+#endif
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 template <bool NT, typename V>
 __device__ __forceinline__ void st16(uint16_t* p, const V& v) {
@@ -380,7 +383,9 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
       const int row = i * 8 + (lane >> 3);
       const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((ch ^ (row & 7)) << 4));
       const int gm = row_base + row;
-      if (gm < g.M && gn < g.N) st16<kNtC>(g.C + (int64_t)gm * g.ldc + gn, v);
+      // plain / bias outputs (input gradients, projections: read at once by the
+      // next kernel) keep normal stores; only the MLP epilogues' streams go non-temporal
+      if (gm < g.M && gn < g.N) st16<kNtC && DLION_GEMM_NT_C_PLAIN>(g.C + (int64_t)gm * g.ldc + gn, v);
     }
     if constexpr (STAMP) {
       DLION_STAMP(st_[4])
