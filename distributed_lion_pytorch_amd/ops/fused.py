@@ -1174,6 +1174,28 @@ class _LMHeadCE(torch.autograd.Function):
                     gw = out
         return gh, gw, None, None
 
+    @staticmethod
+    def _backward_deferred(ctx, g):
+        """Backward of a head whose weight gradient joined the fusion window."""
+        from . import linear
+
+        dh, logits, n_valid, h2d = ctx.saved_tensors
+        s = (g.float() / n_valid).reshape(1)
+        ops = hip.ops()
+        gh = None
+        if ctx.needs_input_grad[0]:
+            gh = torch.empty_like(dh)
+            ops.scale_acc_(dh, s, gh, False)
+        w = ctx.weight
+        v, c = w.shape
+        hs = torch.empty_like(h2d)  # s * h: the per-micro-batch loss scale rides on the small operand
+        ops.scale_acc_(h2d.contiguous(), s, hs, False)
+        split = linear.tn_split_factor(logits.shape[0], logits.shape[1], c)
+        if not linear._defer_wgrad([w], [(0, v * c)], logits, hs, split):
+            part = ops.gemm_tn([logits], [hs], split)  # over budget / window closed: now
+            linear.deposit_grad(w, part.view(split, -1)[:, : v * c], defer=False)
+        return gh, None, None, None
+
 
 def _lm_defer_ok(weight, logits, h2d) -> bool:
     """The LM head's weight gradient can join the window-level TN GEMM: a
@@ -1185,28 +1207,6 @@ def _lm_defer_ok(weight, logits, h2d) -> bool:
             and logits.shape[1] % 8 == 0 and linear._tn_eligible(logits, h2d) and hip.available())
 
 
-def _lm_backward_deferred(ctx, g):
-    from . import linear
-
-    dh, logits, n_valid, h2d = ctx.saved_tensors
-    s = (g.float() / n_valid).reshape(1)
-    ops = hip.ops()
-    gh = None
-    if ctx.needs_input_grad[0]:
-        gh = torch.empty_like(dh)
-        ops.scale_acc_(dh, s, gh, False)
-    w = ctx.weight
-    v, c = w.shape
-    hs = torch.empty_like(h2d)  # s * h: the per-micro-batch loss scale rides on the small operand
-    ops.scale_acc_(h2d.contiguous(), s, hs, False)
-    split = linear.tn_split_factor(logits.shape[0], logits.shape[1], c)
-    if not linear._defer_wgrad([w], [(0, v * c)], logits, hs, split):
-        part = ops.gemm_tn([logits], [hs], split)  # over budget / window closed: now
-        linear.deposit_grad(w, part.view(split, -1)[:, : v * c], defer=False)
-    return gh, None, None, None
-
-
-_LMHeadCE._backward_deferred = staticmethod(_lm_backward_deferred)
 
 
 def _softmax_xent_torch_(logits: torch.Tensor, labels: torch.Tensor, v: int) -> torch.Tensor:
