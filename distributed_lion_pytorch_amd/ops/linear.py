@@ -80,7 +80,7 @@ class _FusionState:
     ``_wdefer_budget()``, which trainer/memory.py counts."""
 
     def __init__(self):
-        self.fuse = {"on": False, "multi": True, "nodefer": False}
+        self.fuse = {"on": False, "multi": True, "nodefer": False, "n_mb": 8}  # n_mb: micro-batches per window (8 if unknown)
         self.acc: dict = {}  # key -> [weakrefs of params, fp32 buffer [S, ...], [(param ref, col0, ncols)]]
         self.pending: list = []  # keys written in the current window, in order
         self.wdefer: dict = {}  # key -> [params, cols, [a segments], [b segments], [versions]]
@@ -100,6 +100,7 @@ def grad_accumulation_fusion(enabled: bool = True, micro_batches: int | None = N
     _ST.fuse["on"] = bool(enabled)
     if outer:
         _ST.fuse["multi"] = micro_batches is None or int(micro_batches) > 1
+        _ST.fuse["n_mb"] = int(micro_batches) if micro_batches else 8
     ok = False
     try:
         yield
@@ -124,6 +125,7 @@ def begin_fusion_window(micro_batches: int | None = None) -> bool:
         return False
     _ST.fuse["on"] = True
     _ST.fuse["multi"] = micro_batches is None or int(micro_batches) > 1
+    _ST.fuse["n_mb"] = int(micro_batches) if micro_batches else 8
     return True
 
 
@@ -317,6 +319,7 @@ def _tn_eligible(a: torch.Tensor, b: torch.Tensor) -> bool:
 
 
 _TN_WAVE = int(os.environ.get("DLION_TN_WAVE", "256"))  # grid-size target of tn_split_factor
+_TN_WINDOW_SPLIT = os.environ.get("DLION_TN_WINDOW_SPLIT", "1") != "0"  # deferred splits sized for the window
 _TN_MIN_TILES = 16  # below: hipBLASLt (attn c_proj 768x768, 9 tiles: 43 us vs 55 us in the step)
 
 
@@ -324,7 +327,7 @@ _TN_CU_RATE = 4.9e12  # FLOP/s of one CU in the TN kernel (1.25 PF/s over 256 CU
 _TN_BW = 5.0e12  # B/s for the fp32 partials (written once, read once by the reduction)
 
 
-def tn_split_factor(M: int, R: int, C: int) -> int:
+def tn_split_factor(M: int, R: int, C: int, max_split: int = 16) -> int:
     """Splits of the token axis for the own TN kernel: minimises waves of
     (256x256 tiles x splits) blocks x per-block time + the fp32 partial
     traffic (splits x R x C x 8 bytes).  GPT-2 c_fc: 7 (252 blocks, one wave),
@@ -332,7 +335,7 @@ def tn_split_factor(M: int, R: int, C: int) -> int:
     Llama-sized weights: 1."""
     tiles = math.ceil(R / 256) * math.ceil(C / 256)
     best, best_cost = 1, None
-    for s in range(1, max(1, min(16, M // 128)) + 1):
+    for s in range(1, max(1, min(max_split, M // 128)) + 1):
         waves = math.ceil(tiles * s / _TN_WAVE)
         cost = waves * (2.0 * 65536 * M / s) / _TN_CU_RATE + 8.0 * s * R * C / _TN_BW
         if best_cost is None or cost < best_cost:
@@ -350,6 +353,13 @@ def wgrad_splits(a: torch.Tensor, b: torch.Tensor) -> tuple:
     deferred = _WDEFER_ON and _ST.fuse["on"] and _ST.fuse["multi"] and not _ST.fuse["nodefer"]
     if ((deferred or math.ceil(R / 256) * math.ceil(C / 256) >= _TN_MIN_TILES) and _tn_eligible(a, b)
             and hip.available()):
+        if deferred and _TN_WINDOW_SPLIT:
+            # the window's GEMM reduces over every micro-batch's tokens: size the
+            # split for that K (GPT-2 attn c_proj, 9 tiles: 28 splits = 252 blocks
+            # instead of the per-micro-batch choice of 16 = 144 blocks, 0.77 PF/s)
+            # (capped by one micro-batch's rows: a window flushed early -- budget, 16
+            # segments -- may run with a single segment)
+            return tn_split_factor(M * _ST.fuse["n_mb"], R, C, max_split=min(32, M // 128)), True
         return tn_split_factor(M, R, C), True
     return split_k_factor(M, R, C), False
 

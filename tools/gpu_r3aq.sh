@@ -1,0 +1,10 @@
+# Deferred TN splits sized for the window's K (default) vs per micro-batch; fusion / model / parity tests
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/r3aq
+timeout -k 10 500 python -u -m pytest tests/test_grad_fusion_gpu.py tests/test_models_gpu.py tests/test_parity_full_gpu.py tests/test_gemm_tn_gpu.py -q -x --timeout 240 --timeout-method thread > gpurun_out/r3aq/tests.log 2>&1 || { tail -40 gpurun_out/r3aq/tests.log; exit 1; }
+tail -1 gpurun_out/r3aq/tests.log
+for v in 1 0 1 0 1 0; do
+  DLION_TN_WINDOW_SPLIT=$v timeout -k 10 200 python bench.py --steps 12 --warmup 3 > gpurun_out/r3aq/bench_$v.json 2> gpurun_out/r3aq/bench_$v.err || { tail -20 gpurun_out/r3aq/bench_$v.err; exit 1; }
+  echo "window_split=$v $(python -c "import json;d=json.load(open('gpurun_out/r3aq/bench_$v.json'));print(d['value'],d['ms_per_step'])")"
+done | tee gpurun_out/r3aq/bench_ab.txt
