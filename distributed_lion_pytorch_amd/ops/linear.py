@@ -761,10 +761,10 @@ def _pick(key, cands: dict, rounds: int = 3, reps: int = 3) -> str:
     best = min(live, key=live.get) if live else next(iter(cands))
     others = [n for n in live if not n.endswith("own")]
     if best.endswith("own") and others:
-        # in the training step the own kernel loses a few % against its isolated
-        # timing (GPT-2's N = 768 input gradients: picked at a 2-4 % isolated win,
-        # the step ran 0.3 % slower than with hipBLASLt -- profiles/r3/gemm_choice_ab.txt):
-        # it has to win by a margin
+        # in the training step the own kernel does worse than its isolated timing
+        # says (GPT-2's N = 768 input gradients: picked on that timing, the step
+        # ran 0.3-0.5 % slower than with hipBLASLt -- profiles/r3/gemm_choice_ab.txt),
+        # so it has to win by a margin
         alt = min(others, key=live.get)
         if live[best] > live[alt] * (1.0 - _OWN_MARGIN):
             best = alt
