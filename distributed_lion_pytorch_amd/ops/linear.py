@@ -763,7 +763,7 @@ def _pick(key, cands: dict, rounds: int = 3, reps: int = 3) -> str:
     if best.endswith("own") and others:
         # in the training step the own kernel does worse than its isolated timing
         # says (GPT-2's N = 768 input gradients: picked on that timing, the step
-        # ran 0.3-0.5 % slower than with hipBLASLt -- profiles/r3/gemm_choice_ab.txt),
+        # ran 0.3-0.5 % slower than with hipBLASLt -- profiles/r3/misc_ab.txt),
         # so it has to win by a margin
         alt = min(others, key=live.get)
         if live[best] > live[alt] * (1.0 - _OWN_MARGIN):
