@@ -124,3 +124,33 @@ def test_split_k_window_edge_cases(case, cuda, monkeypatch):
     assert err < 8e-3, (case, err)
     L.release_split_k_accumulators()
     assert not L._ST.acc
+
+
+def test_lm_head_weight_gradient_joins_the_window(cuda, monkeypatch):
+    """Inside a multi-micro-batch window the LM head's weight gradient is not
+    computed per micro-batch: (softmax - onehot, s * h) go to the window's TN
+    GEMM and reach w.grad when the window closes -- equal to the per-micro-batch
+    path (different loss scales per micro-batch included)."""
+    from distributed_lion_pytorch_amd.ops import fused
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    torch.manual_seed(5)
+    N, C, V = 256, 256, 1000
+    hs = [torch.randn(N, C, device=cuda).to(torch.bfloat16).requires_grad_(True) for _ in range(3)]
+    w = torch.nn.Parameter((torch.randn(V, C, device=cuda) * 0.05).to(torch.bfloat16))
+    labels = [torch.randint(0, V, (N,), device=cuda) for _ in range(3)]
+    labels[1][::3] = -100  # a different normalizer per micro-batch
+    grads = {}
+    for defer in (True, False):
+        monkeypatch.setattr(fused, "_LM_DEFER", defer)
+        w.grad = None
+        with L.grad_accumulation_fusion(True, micro_batches=3):
+            for i in range(3):
+                (fused.lm_head_cross_entropy(hs[i], w, labels[i]) * (i + 1)).backward()
+                if defer:
+                    assert w.grad is None, "the deferred gradient must wait for the end of the window"
+        grads[defer] = w.grad.float().clone()
+    ref = grads[False]
+    err = (grads[True] - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-2, err
