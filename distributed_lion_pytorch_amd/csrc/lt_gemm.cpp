@@ -17,7 +17,14 @@
 // heuristic returns up to kCand candidates, each is timed on the caller's
 // stream (skipped under stream capture) and the fastest is cached, so a call
 // costs ~11 us of host time against ~19 us for ATen's per-call heuristic
-// query (tools/bench_host_overhead.py).  The library is torch's own bundled
+// query (tools/bench_host_overhead.py).  The candidates are every algorithm
+// of the library that supports the problem (hipblaslt_ext::getAllAlgos +
+// matmulIsAlgoSupported: ~230 for GPT-2's bf16 shapes), not only the
+// heuristic's top kCand: one short screening sample each, then the best kCand
+// go through the same interleaved rounds as the heuristic set (which always
+// stays in the final round).  GPT-2 LM-head forward 1378 -> 1258 us, three
+// of the four other shapes 2-5 % faster; same-box bench 1.037M -> 1.042M
+// tok/s (profiles/r3/lt_all_ab.txt).  DLION_LT_ALL=0: heuristic set only.  The library is torch's own bundled
 // libhipblaslt (linked by SONAME, so the copy libtorch_hip already loaded is
 // reused -- no second hipBLASLt in the process).
 #include <ATen/ATen.h>
@@ -25,11 +32,16 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 
+#include <algorithm>
 #include <array>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <set>
+#include <vector>
 
 namespace dlion {
 namespace {
@@ -56,8 +68,8 @@ struct Plan {
   size_t ws = 0;
   bool ok = false;
   bool tuned = false;
-  int n_cand = 0;
-  hipblasLtMatmulHeuristicResult_t cand[kCand];
+  int n_heur = 0;  // cand[0, n_heur): hipBLASLt's heuristic picks, the rest: exhaustive search
+  std::vector<hipblasLtMatmulHeuristicResult_t> cand;
 };
 
 std::mutex g_mu;
@@ -99,6 +111,11 @@ hipblasStatus_t run(DevState& st, Plan& p, const hipblasLtMatmulAlgo_t& algo, co
                          st.workspace.data_ptr(), kWorkspace, s);
 }
 
+bool exhaustive() {
+  const char* v = std::getenv("DLION_LT_ALL");
+  return v == nullptr || v[0] != '0';
+}
+
 Plan& get_plan(DevState& st, const Key& key, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldc,
                int epi, const void* bias) {
   auto it = g_plans.find(key);
@@ -125,15 +142,41 @@ Plan& get_plan(DevState& st, const Key& key, int64_t m, int64_t n, int64_t k, in
   lt_check(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)),
            "preference workspace");
   int got = 0;
+  hipblasLtMatmulHeuristicResult_t heur[kCand];
   const hipblasStatus_t hs =
-      hipblasLtMatmulAlgoGetHeuristic(st.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, kCand, p.cand, &got);
+      hipblasLtMatmulAlgoGetHeuristic(st.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, kCand, heur, &got);
   hipblasLtMatmulPreferenceDestroy(pref);
-  p.n_cand = 0;
+  std::set<int> seen;
   if (hs == HIPBLAS_STATUS_SUCCESS) {
     for (int i = 0; i < got; ++i)
-      if (p.cand[i].state == HIPBLAS_STATUS_SUCCESS && p.cand[i].workspaceSize <= kWorkspace) p.cand[p.n_cand++] = p.cand[i];
+      if (heur[i].state == HIPBLAS_STATUS_SUCCESS && heur[i].workspaceSize <= kWorkspace) {
+        p.cand.push_back(heur[i]);
+        seen.insert(hipblaslt_ext::getIndexFromAlgo(heur[i].algo));
+      }
   }
-  p.ok = p.n_cand > 0;
+  p.n_heur = static_cast<int>(p.cand.size());
+  if (exhaustive()) {
+    std::vector<hipblasLtMatmulHeuristicResult_t> all;
+    if (hipblaslt_ext::getAllAlgos(st.handle, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, HIPBLAS_OP_T, HIPBLAS_OP_N,
+                                   HIP_R_16BF, HIP_R_16BF, HIP_R_16BF, HIP_R_16BF, HIPBLAS_COMPUTE_32F,
+                                   all) == HIPBLAS_STATUS_SUCCESS) {
+      const float alpha = 1.f, beta = 0.f;
+      for (auto& r : all) {
+        const int idx = hipblaslt_ext::getIndexFromAlgo(r.algo);
+        if (seen.count(idx)) continue;
+        size_t ws = 0;
+        if (hipblaslt_ext::matmulIsAlgoSupported(st.handle, p.desc, &alpha, p.la, p.lb, &beta, p.lc, p.lc, r.algo,
+                                                 ws) != HIPBLAS_STATUS_SUCCESS ||
+            ws > kWorkspace)
+          continue;
+        r.workspaceSize = ws;
+        r.state = HIPBLAS_STATUS_SUCCESS;
+        p.cand.push_back(r);
+        seen.insert(idx);
+      }
+    }
+  }
+  p.ok = !p.cand.empty();
   if (p.ok) {
     p.algo = p.cand[0].algo;
     p.ws = p.cand[0].workspaceSize;
@@ -146,10 +189,22 @@ bool tuning_enabled() {
   return v == nullptr || v[0] != '0';
 }
 
-// time every candidate (2 launches each after a warm-up) and keep the fastest
+float time_algo(DevState& st, Plan& p, const hipblasLtMatmulAlgo_t& algo, const void* a, const void* b, void* c,
+                hipStream_t s, hipEvent_t e0, hipEvent_t e1, int reps) {
+  hipEventRecord(e0, s);
+  bool ok = true;
+  for (int r = 0; r < reps && ok; ++r) ok = run(st, p, algo, a, b, c, s) == HIPBLAS_STATUS_SUCCESS;
+  hipEventRecord(e1, s);
+  hipEventSynchronize(e1);
+  float ms = 0.f;
+  if (!ok || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return -1.f;
+  return ms;
+}
+
+// time the candidates and keep the fastest
 void tune(DevState& st, Plan& p, const void* a, const void* b, void* c, hipStream_t s) {
   p.tuned = true;
-  if (p.n_cand < 2 || !tuning_enabled()) return;
+  if (p.cand.size() < 2 || !tuning_enabled()) return;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
   hipEvent_t e0, e1;
@@ -158,42 +213,59 @@ void tune(DevState& st, Plan& p, const void* a, const void* b, void* c, hipStrea
     hipEventDestroy(e0);
     return;
   }
+  // final set: the heuristic picks, plus (exhaustive search) the kCand best of
+  // one warm-up + one 2-run screening sample of every other supported algorithm
+  std::vector<int> fin;
+  for (int i = 0; i < p.n_heur; ++i) fin.push_back(i);
+  const int n_all = static_cast<int>(p.cand.size());
+  if (n_all > p.n_heur) {
+    std::vector<std::pair<float, int>> scr;
+    for (int i = p.n_heur; i < n_all; ++i) {
+      if (run(st, p, p.cand[i].algo, a, b, c, s) != HIPBLAS_STATUS_SUCCESS) continue;
+      const float ms = time_algo(st, p, p.cand[i].algo, a, b, c, s, e0, e1, 2);
+      if (ms > 0.f) scr.emplace_back(ms, i);
+    }
+    std::sort(scr.begin(), scr.end());
+    for (size_t j = 0; j < scr.size() && j < static_cast<size_t>(kCand); ++j) fin.push_back(scr[j].second);
+  }
   // kRounds interleaved rounds of kReps runs per candidate, best round per
   // candidate: one 2-run sample per candidate (the first version) let clock
   // ramps and neighbour interference pick a 10-15 % slower algorithm on some
   // runs, which showed up as run-to-run spread of the whole step
   constexpr int kRounds = 3, kReps = 3;
-  float best_ms[kCand];
-  for (int i = 0; i < kCand; ++i) best_ms[i] = 1e30f;
-  for (int i = 0; i < p.n_cand; ++i)  // warm-up (and drop candidates that fail)
-    if (run(st, p, p.cand[i].algo, a, b, c, s) != HIPBLAS_STATUS_SUCCESS) best_ms[i] = -1.f;
+  std::vector<float> best_ms(fin.size(), 1e30f);
+  for (size_t j = 0; j < fin.size(); ++j)  // warm-up (and drop candidates that fail)
+    if (run(st, p, p.cand[fin[j]].algo, a, b, c, s) != HIPBLAS_STATUS_SUCCESS) best_ms[j] = -1.f;
   for (int rd = 0; rd < kRounds; ++rd) {
-    for (int i = 0; i < p.n_cand; ++i) {
-      if (best_ms[i] < 0.f) continue;
-      hipEventRecord(e0, s);
-      bool ok = true;
-      for (int r = 0; r < kReps && ok; ++r) ok = run(st, p, p.cand[i].algo, a, b, c, s) == HIPBLAS_STATUS_SUCCESS;
-      hipEventRecord(e1, s);
-      hipEventSynchronize(e1);
-      float ms = 0.f;
-      if (!ok || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
-        best_ms[i] = -1.f;
+    for (size_t j = 0; j < fin.size(); ++j) {
+      if (best_ms[j] < 0.f) continue;
+      const float ms = time_algo(st, p, p.cand[fin[j]].algo, a, b, c, s, e0, e1, kReps);
+      if (ms < 0.f) {
+        best_ms[j] = -1.f;
         continue;
       }
-      if (ms < best_ms[i]) best_ms[i] = ms;
+      if (ms < best_ms[j]) best_ms[j] = ms;
     }
   }
-  float best = 1e30f;
-  int besti = 0;
-  for (int i = 0; i < p.n_cand; ++i)
-    if (best_ms[i] >= 0.f && best_ms[i] < best) {
-      best = best_ms[i];
-      besti = i;
+  float best = 1e30f, heur_best = 1e30f;
+  size_t bestj = 0;
+  for (size_t j = 0; j < fin.size(); ++j) {
+    if (best_ms[j] < 0.f) continue;
+    if (best_ms[j] < best) {
+      best = best_ms[j];
+      bestj = j;
     }
+    if (fin[j] < p.n_heur) heur_best = std::min(heur_best, best_ms[j]);
+  }
   hipEventDestroy(e0);
   hipEventDestroy(e1);
-  p.algo = p.cand[besti].algo;
-  p.ws = p.cand[besti].workspaceSize;
+  const char* vb = std::getenv("DLION_LT_VERBOSE");
+  if (vb != nullptr && vb[0] == '1')
+    std::fprintf(stderr, "[lt_gemm] %d heuristic + %d other algorithms: best heuristic %.1f us, chosen %.1f us (%s)\n",
+                 p.n_heur, n_all - p.n_heur, heur_best * 1e3f / kReps, best * 1e3f / kReps,
+                 fin[bestj] < p.n_heur ? "heuristic" : "search");
+  p.algo = p.cand[fin[bestj]].algo;
+  p.ws = p.cand[fin[bestj]].workspaceSize;
 }
 
 }  // namespace

@@ -65,6 +65,10 @@ def main():
                     us = timeit(lambda: hip.ops().gemm_tn(xs, ys, s), iters=5)
                     win.append(f"s={s}:{us / a.window:7.1f}us/mb {a.window * flop / us / 1e9:4.2f}PF")
                 print(f"{'  window':12s} " + "  ".join(win), flush=True)
+                xc, yc = torch.cat(xs), torch.cat(ys)  # hipBLASLt (ATen heuristic) on the concatenated window
+                us = timeit(lambda: torch.mm(xc.t(), yc), iters=5)
+                print(f"{'  blas win':12s} {us / a.window:7.1f}us/mb {a.window * flop / us / 1e9:4.2f}PF", flush=True)
+                del xc, yc
                 del xs, ys
 
 
