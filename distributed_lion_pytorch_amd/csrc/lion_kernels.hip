@@ -30,6 +30,14 @@ namespace dlion {
 #ifndef DLION_K2_NT
 #define DLION_K2_NT 0  // non-temporal p stores in the K2 fast path
 #endif
+#ifndef DLION_K2_PAIR
+#define DLION_K2_PAIR 1  // pre-voted apply: two chunks per block (one metadata chain per 16k params);
+                         // GPT-2 122 -> 113 us, Llama-3-8B unchanged (profiles/r3/lion_pair_ab.txt)
+#endif
+#ifndef DLION_K4_UNROLL
+#define DLION_K4_UNROLL 2  // K4 sliced path: words per thread per grid-stride iteration (1 or 2);
+                           // GPT-2 shard 8.1 -> 7.4 us, Llama-3-8B unchanged
+#endif
 #ifndef DLION_K4_MAXBLOCKS
 #define DLION_K4_MAXBLOCKS 2048  // K4 grid cap (grid-stride beyond)
 #endif
@@ -513,6 +521,89 @@ lion_vote_apply32_kernel(const int64_t* __restrict__ seg, const int64_t* __restr
   }
 }
 
+// K2 pre-voted apply (mode 2, no telemetry), two chunks per block.  Every
+// block of the one-chunk kernel starts with two dependent metadata loads
+// (chunk row -> segment row) before its first data load, and a pre-voted
+// chunk moves only 4.125 B per parameter, so that chain is a large share of
+// a block's life (GPT-2: 67 % of HBM against the copy reference's 86 %,
+// profiles/r3/lion_ab_nt_k4cap.txt).  Here both chunks' metadata loads are in
+// flight together and, when both chunks are full, all 8 p vectors and plane
+// words of the pair are loaded before the first use.
+template <int DT>
+__device__ __forceinline__ void prevoted_chunk(const SegRow& r, int64_t start, const uint8_t* __restrict__ planes,
+                                               const uint8_t* __restrict__ neg_plane, float decay, float neg_lr) {
+  using E = Elem<DT>;
+  using S = typename E::S;
+  S* p = const_cast<S*>(static_cast<const S*>(r.p));
+  const int sub = threadIdx.x & 3;
+#pragma unroll
+  for (int it = 0; it < kIters; ++it) {
+    const int64_t e = start + it * kSpan + threadIdx.x * 8;
+    if (e >= r.n) break;
+    const int64_t word = (r.bit_off + e) >> 5;
+    uint32_t pos = reinterpret_cast<const uint32_t*>(planes)[word];
+    uint32_t neg = neg_plane ? reinterpret_cast<const uint32_t*>(neg_plane)[word] : ~pos;
+    pos = (pos >> (8 * sub)) & 0xffu;
+    neg = (neg >> (8 * sub)) & 0xffu;
+    float pv[8];
+    load8g<DT>(p, e, r.n, r.vec, pv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float delta = static_cast<float>(static_cast<int>((pos >> j) & 1) - static_cast<int>((neg >> j) & 1));
+      pv[j] = __fmaf_rn(neg_lr, delta, E::rnd(pv[j] * decay));
+    }
+    store8g<DT>(p, e, r.n, r.vec, pv);
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(kThreads)
+lion_apply_prevoted2_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ chunks, int64_t n_chunks,
+                            const uint8_t* __restrict__ planes, const uint8_t* __restrict__ neg_plane, float decay,
+                            float neg_lr) {
+  using E = Elem<DT>;
+  using S = typename E::S;
+  const int64_t c0 = 2 * static_cast<int64_t>(blockIdx.x);
+  const bool has1 = c0 + 1 < n_chunks;
+  const int64_t s0 = chunks[2 * c0], st0 = chunks[2 * c0 + 1];
+  const int64_t s1 = has1 ? chunks[2 * c0 + 2] : s0, st1 = has1 ? chunks[2 * c0 + 3] : st0;
+  const SegRow r0 = load_seg(seg, s0);
+  const SegRow r1 = load_seg(seg, s1);
+  const bool full0 = r0.vec && st0 + kChunk <= r0.n, full1 = has1 && r1.vec && st1 + kChunk <= r1.n;
+  if (full0 && full1) {  // block-uniform
+    S* p0 = const_cast<S*>(static_cast<const S*>(r0.p));
+    S* p1 = const_cast<S*>(static_cast<const S*>(r1.p));
+    const int sub = threadIdx.x & 3;
+    Raw8<DT> rp[2 * kIters];
+    uint32_t pw[2 * kIters], nw[2 * kIters];
+#pragma unroll
+    for (int q = 0; q < 2 * kIters; ++q) {
+      const SegRow& r = q < kIters ? r0 : r1;
+      const int64_t e = (q < kIters ? st0 : st1) + (q % kIters) * kSpan + threadIdx.x * 8;
+      const int64_t word = (r.bit_off + e) >> 5;
+      rp[q].load((q < kIters ? p0 : p1) + e);
+      pw[q] = reinterpret_cast<const uint32_t*>(planes)[word];
+      nw[q] = neg_plane ? reinterpret_cast<const uint32_t*>(neg_plane)[word] : ~pw[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 2 * kIters; ++q) {
+      const int64_t e = (q < kIters ? st0 : st1) + (q % kIters) * kSpan + threadIdx.x * 8;
+      const uint32_t pos = (pw[q] >> (8 * sub)) & 0xffu, neg = (nw[q] >> (8 * sub)) & 0xffu;
+      float pv[8];
+      rp[q].unpack(pv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float delta = static_cast<float>(static_cast<int>((pos >> j) & 1) - static_cast<int>((neg >> j) & 1));
+        pv[j] = __fmaf_rn(neg_lr, delta, E::rnd(pv[j] * decay));
+      }
+      E::store8((q < kIters ? p0 : p1) + e, pv);
+    }
+    return;
+  }
+  prevoted_chunk<DT>(r0, st0, planes, neg_plane, decay, neg_lr);
+  if (has1) prevoted_chunk<DT>(r1, st1, planes, neg_plane, decay, neg_lr);
+}
+
 // ----------------------------------------------------------------------- K4
 // recv: [W][nbytes] shards gathered by all_to_all; out: voted positive bits;
 // neg_out (optional): voted negative bits (only needed when ties map to 0).
@@ -532,8 +623,32 @@ vote_reduce_kernel(const uint8_t* __restrict__ recv, int64_t nbytes, const uint8
     uint32_t live_mask = 0;
     for (int k = 0; k < world; ++k) live_mask |= static_cast<uint32_t>(alive[k] != 0) << k;
     // (a 16-byte-per-plane variant measured slower: 31 vs 40 % of HBM at Llama-3-8B)
-    for (int64_t w = blockIdx.x * (int64_t)kThreads + threadIdx.x; w < nwords;
-         w += (int64_t)gridDim.x * kThreads) {
+    const int64_t stride = (int64_t)gridDim.x * kThreads;
+    int64_t w = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+    if constexpr (DLION_K4_UNROLL == 2) {
+      // two words per iteration, every plane load of both issued first
+      // (one word per lane keeps only W dwords in flight per wave)
+      for (; w + stride < nwords; w += 2 * stride) {
+        uint32_t v[kMaxSliced], u[kMaxSliced];
+#pragma unroll
+        for (int k = 0; k < kMaxSliced; ++k) {
+          const bool on = (live_mask >> k) & 1;
+          v[k] = on ? reinterpret_cast<const uint32_t*>(recv + k * nbytes)[w] : 0u;
+          u[k] = on ? reinterpret_cast<const uint32_t*>(recv + k * nbytes)[w + stride] : 0u;
+        }
+        uint32_t pos, ng, tb, pos2, ng2, tb2;
+        sliced_vote(v, world, n_live, tie, pos, ng, tb);
+        sliced_vote(u, world, n_live, tie, pos2, ng2, tb2);
+        n_tie += __popc(tb) + __popc(tb2);
+        reinterpret_cast<uint32_t*>(out)[w] = pos;
+        reinterpret_cast<uint32_t*>(out)[w + stride] = pos2;
+        if (neg_out != nullptr) {
+          reinterpret_cast<uint32_t*>(neg_out)[w] = ng;
+          reinterpret_cast<uint32_t*>(neg_out)[w + stride] = ng2;
+        }
+      }
+    }
+    for (; w < nwords; w += stride) {
       uint32_t v[kMaxSliced];
 #pragma unroll
       for (int k = 0; k < kMaxSliced; ++k)
@@ -689,6 +804,11 @@ hipError_t launch_lion_vote_apply(int dt, const int64_t* seg, const int64_t* chu
                                   int mode, int tie, const uint8_t* neg, float decay, float neg_lr,
                                   const uint8_t* own, unsigned long long* agree, hipStream_t st) {
   if (n_chunks == 0) return hipSuccess;
+  if (DLION_K2_PAIR && mode == 2 && agree == nullptr) {
+    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_apply_prevoted2_kernel<DT>), dim3((n_chunks + 1) / 2), dim3(kThreads),
+                                          0, st, seg, chunks, n_chunks, planes, neg, decay, neg_lr));
+    return hipGetLastError();
+  }
   if (mode == 2 || (mode == 0 && world <= kMaxSliced)) {
     DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_vote_apply32_kernel<DT>), dim3(n_chunks), dim3(kThreads), 0, st,
                                           seg, chunks, planes, plane_stride, alive, world, mode, tie, neg, decay,
@@ -718,7 +838,8 @@ hipError_t launch_vote_reduce(const uint8_t* recv, int64_t nbytes, const uint8_t
                               uint8_t* out, uint8_t* neg_out, unsigned long long* ties, hipStream_t st) {
   const int64_t nwords = nbytes >> 2;
   if (nwords == 0) return hipSuccess;
-  int64_t blocks = (nwords + kThreads - 1) / kThreads;
+  const int64_t per_block = static_cast<int64_t>(kThreads) * (world <= kMaxSliced ? DLION_K4_UNROLL : 1);
+  int64_t blocks = (nwords + per_block - 1) / per_block;
   if (blocks > DLION_K4_MAXBLOCKS) blocks = DLION_K4_MAXBLOCKS;
   if (world <= kMaxSliced)
     hipLaunchKernelGGL(vote_reduce_kernel<true>, dim3(blocks), dim3(kThreads), 0, st, recv, nbytes, alive, world, tie,

@@ -132,6 +132,33 @@ def test_vote_apply_kernel_fake_voters(dtype, world, mode, tie, cuda):
         assert agree[1].item() > 0  # even live count: random planes tie somewhere
 
 
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("tie", [ref.TIE_NEGATIVE, ref.TIE_ZERO])
+def test_prevoted_apply_matches_oracle(dtype, tie, cuda):
+    """K2 mode 2 (a2a path: one voted plane, optional neg plane) without
+    telemetry -- the path of the two-chunks-per-block kernel: odd chunk counts,
+    partial and misaligned tensors, full chunk pairs."""
+    ps, gs, ms = _tensors(dtype, cuda, seed=3)
+    plan = FlatPlan([(p, 0) for p in ps], world=4, bucket_bytes=1 << 16, device=cuda)
+    hp = HParams(lr=3e-3, wd=0.05, beta1=0.9, beta2=0.99)
+    gen = torch.Generator(device="cpu").manual_seed(7 + tie)
+    pos = torch.randint(0, 256, (plan.total_bytes,), generator=gen, dtype=torch.uint8).to(cuda)
+    neg = (torch.randint(0, 256, (plan.total_bytes,), generator=gen, dtype=torch.uint8).to(cuda) & ~pos
+           if tie == ref.TIE_ZERO else None)
+    alive = torch.ones(4, dtype=torch.uint8, device=cuda)
+    p2 = _clone(ps)
+    hx, tx = HipExecutor(plan), TorchExecutor(plan)
+    meta = plan.meta(gs, ms)
+    for b in plan.buckets:
+        sl = slice(b.byte_off, b.byte_off + b.nbytes)
+        ng = neg[sl] if neg is not None else None
+        hx.apply(meta, b, pos[sl], b.nbytes, alive, ref.VOTE_PREVOTED, tie, ng, hp)
+        tx.apply(None, _rebind(b, p2, plan), pos[sl], b.nbytes, alive, ref.VOTE_PREVOTED, tie, ng, hp)
+    torch.cuda.synchronize()
+    for a, b in zip(ps, p2):
+        _assert_close(a, b, dtype)
+
+
 def _rebind(bucket, new_params, plan):
     import copy
 
