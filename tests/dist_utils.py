@@ -1,4 +1,5 @@
 """Multi-process helpers: spawn W gloo ranks on 127.0.0.1 and collect results."""
+import io
 import os
 import socket
 import traceback
@@ -24,7 +25,12 @@ def _entry(rank, world, port, fn, args, q):
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         out = fn(rank, world, *args)
-        q.put((rank, "ok", out))
+        # by value: a tensor put on the queue travels as a shared-memory fd that the
+        # parent fetches from THIS process, which may already have exited
+        # (ConnectionResetError in rebuild_storage_fd on a loaded box)
+        buf = io.BytesIO()
+        torch.save(out, buf)
+        q.put((rank, "ok", buf.getvalue()))
     except Exception:  # pragma: no cover - reported to the parent
         q.put((rank, "err", traceback.format_exc()))
     finally:
@@ -46,7 +52,7 @@ def run_world(fn, world, *args, timeout=240):
             rank, status, out = q.get(timeout=timeout)
             if status != "ok":
                 raise RuntimeError(f"rank {rank} failed:\n{out}")
-            results[rank] = out
+            results[rank] = torch.load(io.BytesIO(out), weights_only=True)
     finally:
         for p in procs:
             p.join(timeout=30)
