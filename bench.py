@@ -28,6 +28,7 @@ step (the worker-dropout stress itself is dropout_stress.py).
 from __future__ import annotations
 
 import argparse
+import copy
 import json
 import os
 import sys
@@ -265,7 +266,10 @@ def build_reference(args, dev):
 
     torch.manual_seed(0)
     with torch.device(dev):
-        init = build_model(cfg, native=True).to(dtype=torch.bfloat16).state_dict()
+        # from a copy: building the native model sets the config's attention
+        # implementation to "eager", which would send HF's model to eager
+        # attention instead of its default SDPA (what the reference's run_clm gets)
+        init = build_model(copy.deepcopy(cfg), native=True).to(dtype=torch.bfloat16).state_dict()
     model = transformers.GPT2LMHeadModel(cfg).to(device=dev, dtype=torch.bfloat16)
     missing = model.load_state_dict(init, strict=False)
     assert not [k for k in missing.missing_keys if "attn.bias" not in k and "masked_bias" not in k], missing
