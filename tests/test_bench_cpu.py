@@ -74,3 +74,18 @@ def test_learning_curves_native_vs_reference_track(tmp_path):
     assert len(a) == len(b) == 20
     assert a[-1] < a[0] - 0.5  # it learns
     assert max(abs(x - y) for x, y in zip(a, b)) < 0.05
+
+
+def test_reference_model_keeps_hf_default_attention():
+    """The reference run's HF model uses HF's default SDPA attention, as the
+    reference's run_clm does: building the native init weights (same seed) must
+    not flip the shared config to the eager path (that cost the reference run
+    30 % on the GPU: 331k -> 229k tok/s, profiles/r3/reference_sdpa.txt)."""
+    import argparse
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    args = argparse.Namespace(model="gpt2-tiny", dropout=None, lr=1e-4, weight_decay=0.1)
+    model, _, cfg = bench.build_reference(args, torch.device("cpu"))
+    assert model.config._attn_implementation == "sdpa"
