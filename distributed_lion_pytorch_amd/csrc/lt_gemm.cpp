@@ -20,7 +20,8 @@
 // query (tools/bench_host_overhead.py).  The candidates are every algorithm
 // of the library that supports the problem (hipblaslt_ext::getAllAlgos +
 // matmulIsAlgoSupported: ~230 for GPT-2's bf16 shapes), not only the
-// heuristic's top kCand: one short screening sample each, then the best kCand
+// heuristic's top kCand: one or two timed runs each (dropped if over 2x the
+// best heuristic pick), a 2-run sample for the rest, then the best kCand
 // go through the same interleaved rounds as the heuristic set (which always
 // stays in the final round).  GPT-2 LM-head forward 1378 -> 1258 us, three
 // of the four other shapes 2-5 % faster; same-box bench 1.037M -> 1.042M
@@ -213,15 +214,27 @@ void tune(DevState& st, Plan& p, const void* a, const void* b, void* c, hipStrea
     hipEventDestroy(e0);
     return;
   }
-  // final set: the heuristic picks, plus (exhaustive search) the kCand best of
-  // one warm-up + one 2-run screening sample of every other supported algorithm
+  // final set: the heuristic picks, plus (exhaustive search) the kCand best
+  // screened others
   std::vector<int> fin;
   for (int i = 0; i < p.n_heur; ++i) fin.push_back(i);
   const int n_all = static_cast<int>(p.cand.size());
   if (n_all > p.n_heur) {
+    // one timed run first (a second one if it was slow: it may have paid for
+    // loading the kernel's code object): most of the library's algorithms are
+    // tiny-tile ones 10-500x slower at these sizes (up to 40 ms per call at
+    // GPT-2's LM head), which get no more runs than that
+    float ref_ms = 1e30f;
+    for (int i = 0; i < p.n_heur; ++i) {
+      run(st, p, p.cand[i].algo, a, b, c, s);
+      const float ms = time_algo(st, p, p.cand[i].algo, a, b, c, s, e0, e1, 1);
+      if (ms > 0.f) ref_ms = std::min(ref_ms, ms);
+    }
     std::vector<std::pair<float, int>> scr;
     for (int i = p.n_heur; i < n_all; ++i) {
-      if (run(st, p, p.cand[i].algo, a, b, c, s) != HIPBLAS_STATUS_SUCCESS) continue;
+      float once = time_algo(st, p, p.cand[i].algo, a, b, c, s, e0, e1, 1);
+      if (once > 2.f * ref_ms) once = time_algo(st, p, p.cand[i].algo, a, b, c, s, e0, e1, 1);
+      if (once <= 0.f || once > 2.f * ref_ms) continue;
       const float ms = time_algo(st, p, p.cand[i].algo, a, b, c, s, e0, e1, 2);
       if (ms > 0.f) scr.emplace_back(ms, i);
     }
