@@ -34,6 +34,10 @@ namespace dlion {
 #define DLION_K2_PAIR 1  // pre-voted apply: two chunks per block (one metadata chain per 16k params);
                          // GPT-2 122 -> 113 us, Llama-3-8B unchanged (profiles/r3/lion_pair_ab.txt)
 #endif
+#ifndef DLION_K2_PAIR_MAJ
+#define DLION_K2_PAIR_MAJ 1  // the same for the majority vote over W <= 15 planes (all-gather exchange):
+                             // W=8 GPT-2 170 -> 155 us, Llama-3-8B 9.3 -> 8.5 ms (profiles/r3/lion_pair_maj_ab.txt)
+#endif
 #ifndef DLION_K4_UNROLL
 #define DLION_K4_UNROLL 2  // K4 sliced path: words per thread per grid-stride iteration (1 or 2);
                            // GPT-2 shard 8.1 -> 7.4 us, Llama-3-8B unchanged
@@ -521,46 +525,70 @@ lion_vote_apply32_kernel(const int64_t* __restrict__ seg, const int64_t* __restr
   }
 }
 
-// K2 pre-voted apply (mode 2, no telemetry), two chunks per block.  Every
-// block of the one-chunk kernel starts with two dependent metadata loads
-// (chunk row -> segment row) before its first data load, and a pre-voted
-// chunk moves only 4.125 B per parameter, so that chain is a large share of
-// a block's life (GPT-2: 67 % of HBM against the copy reference's 86 %,
-// profiles/r3/lion_ab_nt_k4cap.txt).  Here both chunks' metadata loads are in
-// flight together and, when both chunks are full, all 8 p vectors and plane
-// words of the pair are loaded before the first use.
+// K2 without telemetry, two chunks per block: pre-voted (mode 2, the a2a
+// path) and majority over W <= 15 planes (mode 0, the all-gather path).
+// Every block of the one-chunk kernel starts with two dependent metadata
+// loads (chunk row -> segment row) before its first data load, and a
+// pre-voted chunk moves only 4.125 B per parameter, so that chain is a large
+// share of a block's life (GPT-2: 67 % of HBM against the copy reference's
+// 86 %, profiles/r3/lion_ab_nt_k4cap.txt).  Here both chunks' metadata loads
+// are in flight together and, when both chunks are full, all 8 p vectors of
+// the pair (and the pre-voted plane words) are loaded before the first use.
+struct VoteCtx {
+  const uint8_t* planes;
+  int64_t plane_stride;
+  const uint8_t* neg_plane;
+  uint32_t live_mask;
+  int world, n_live, tie;
+};
+
+template <bool MAJ>
+__device__ __forceinline__ void vote_word(const VoteCtx& v, int64_t word, uint32_t& pos, uint32_t& neg) {
+  if constexpr (MAJ) {
+    uint32_t w[kMaxSliced], tb;
+#pragma unroll
+    for (int k = 0; k < kMaxSliced; ++k)
+      w[k] = (v.live_mask >> k) & 1 ? reinterpret_cast<const uint32_t*>(v.planes + k * v.plane_stride)[word] : 0u;
+    sliced_vote(w, v.world, v.n_live, v.tie, pos, neg, tb);
+  } else {
+    pos = reinterpret_cast<const uint32_t*>(v.planes)[word];
+    neg = v.neg_plane ? reinterpret_cast<const uint32_t*>(v.neg_plane)[word] : ~pos;
+  }
+}
+
 template <int DT>
-__device__ __forceinline__ void prevoted_chunk(const SegRow& r, int64_t start, const uint8_t* __restrict__ planes,
-                                               const uint8_t* __restrict__ neg_plane, float decay, float neg_lr) {
-  using E = Elem<DT>;
-  using S = typename E::S;
+__device__ __forceinline__ void apply8(float (&pv)[8], uint32_t pos, uint32_t neg, float decay, float neg_lr) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float delta = static_cast<float>(static_cast<int>((pos >> j) & 1) - static_cast<int>((neg >> j) & 1));
+    pv[j] = __fmaf_rn(neg_lr, delta, Elem<DT>::rnd(pv[j] * decay));
+  }
+}
+
+template <int DT, bool MAJ>
+__device__ __forceinline__ void apply_chunk(const SegRow& r, int64_t start, const VoteCtx& v, float decay,
+                                            float neg_lr) {
+  using S = typename Elem<DT>::S;
   S* p = const_cast<S*>(static_cast<const S*>(r.p));
   const int sub = threadIdx.x & 3;
 #pragma unroll
   for (int it = 0; it < kIters; ++it) {
     const int64_t e = start + it * kSpan + threadIdx.x * 8;
     if (e >= r.n) break;
-    const int64_t word = (r.bit_off + e) >> 5;
-    uint32_t pos = reinterpret_cast<const uint32_t*>(planes)[word];
-    uint32_t neg = neg_plane ? reinterpret_cast<const uint32_t*>(neg_plane)[word] : ~pos;
-    pos = (pos >> (8 * sub)) & 0xffu;
-    neg = (neg >> (8 * sub)) & 0xffu;
+    uint32_t pos, neg;
+    vote_word<MAJ>(v, (r.bit_off + e) >> 5, pos, neg);
     float pv[8];
     load8g<DT>(p, e, r.n, r.vec, pv);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float delta = static_cast<float>(static_cast<int>((pos >> j) & 1) - static_cast<int>((neg >> j) & 1));
-      pv[j] = __fmaf_rn(neg_lr, delta, E::rnd(pv[j] * decay));
-    }
+    apply8<DT>(pv, (pos >> (8 * sub)) & 0xffu, (neg >> (8 * sub)) & 0xffu, decay, neg_lr);
     store8g<DT>(p, e, r.n, r.vec, pv);
   }
 }
 
-template <int DT>
+template <int DT, bool MAJ>
 __global__ void __launch_bounds__(kThreads)
-lion_apply_prevoted2_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ chunks, int64_t n_chunks,
-                            const uint8_t* __restrict__ planes, const uint8_t* __restrict__ neg_plane, float decay,
-                            float neg_lr) {
+lion_apply_pair_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ chunks, int64_t n_chunks,
+                       const uint8_t* __restrict__ planes, int64_t plane_stride, const uint8_t* __restrict__ alive,
+                       int world, int tie, const uint8_t* __restrict__ neg_plane, float decay, float neg_lr) {
   using E = Elem<DT>;
   using S = typename E::S;
   const int64_t c0 = 2 * static_cast<int64_t>(blockIdx.x);
@@ -569,6 +597,14 @@ lion_apply_prevoted2_kernel(const int64_t* __restrict__ seg, const int64_t* __re
   const int64_t s1 = has1 ? chunks[2 * c0 + 2] : s0, st1 = has1 ? chunks[2 * c0 + 3] : st0;
   const SegRow r0 = load_seg(seg, s0);
   const SegRow r1 = load_seg(seg, s1);
+  VoteCtx v{planes, plane_stride, neg_plane, 0u, world, 0, tie};
+  if constexpr (MAJ) {
+    for (int k = 0; k < world && k < kMaxSliced; ++k)
+      if (alive[k]) {
+        v.live_mask |= 1u << k;
+        ++v.n_live;
+      }
+  }
   const bool full0 = r0.vec && st0 + kChunk <= r0.n, full1 = has1 && r1.vec && st1 + kChunk <= r1.n;
   if (full0 && full1) {  // block-uniform
     S* p0 = const_cast<S*>(static_cast<const S*>(r0.p));
@@ -578,30 +614,25 @@ lion_apply_prevoted2_kernel(const int64_t* __restrict__ seg, const int64_t* __re
     uint32_t pw[2 * kIters], nw[2 * kIters];
 #pragma unroll
     for (int q = 0; q < 2 * kIters; ++q) {
-      const SegRow& r = q < kIters ? r0 : r1;
       const int64_t e = (q < kIters ? st0 : st1) + (q % kIters) * kSpan + threadIdx.x * 8;
-      const int64_t word = (r.bit_off + e) >> 5;
       rp[q].load((q < kIters ? p0 : p1) + e);
-      pw[q] = reinterpret_cast<const uint32_t*>(planes)[word];
-      nw[q] = neg_plane ? reinterpret_cast<const uint32_t*>(neg_plane)[word] : ~pw[q];
+      // pre-voted: the plane words join the hoisted loads; majority: voted
+      // below, one iteration's W words at a time (hoisting all of them spilled)
+      if constexpr (!MAJ) vote_word<false>(v, ((q < kIters ? r0 : r1).bit_off + e) >> 5, pw[q], nw[q]);
     }
 #pragma unroll
     for (int q = 0; q < 2 * kIters; ++q) {
       const int64_t e = (q < kIters ? st0 : st1) + (q % kIters) * kSpan + threadIdx.x * 8;
-      const uint32_t pos = (pw[q] >> (8 * sub)) & 0xffu, neg = (nw[q] >> (8 * sub)) & 0xffu;
+      if constexpr (MAJ) vote_word<true>(v, ((q < kIters ? r0 : r1).bit_off + e) >> 5, pw[q], nw[q]);
       float pv[8];
       rp[q].unpack(pv);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float delta = static_cast<float>(static_cast<int>((pos >> j) & 1) - static_cast<int>((neg >> j) & 1));
-        pv[j] = __fmaf_rn(neg_lr, delta, E::rnd(pv[j] * decay));
-      }
+      apply8<DT>(pv, (pw[q] >> (8 * sub)) & 0xffu, (nw[q] >> (8 * sub)) & 0xffu, decay, neg_lr);
       E::store8((q < kIters ? p0 : p1) + e, pv);
     }
     return;
   }
-  prevoted_chunk<DT>(r0, st0, planes, neg_plane, decay, neg_lr);
-  if (has1) prevoted_chunk<DT>(r1, st1, planes, neg_plane, decay, neg_lr);
+  apply_chunk<DT, MAJ>(r0, st0, v, decay, neg_lr);
+  if (has1) apply_chunk<DT, MAJ>(r1, st1, v, decay, neg_lr);
 }
 
 // ----------------------------------------------------------------------- K4
@@ -805,8 +836,15 @@ hipError_t launch_lion_vote_apply(int dt, const int64_t* seg, const int64_t* chu
                                   const uint8_t* own, unsigned long long* agree, hipStream_t st) {
   if (n_chunks == 0) return hipSuccess;
   if (DLION_K2_PAIR && mode == 2 && agree == nullptr) {
-    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_apply_prevoted2_kernel<DT>), dim3((n_chunks + 1) / 2), dim3(kThreads),
-                                          0, st, seg, chunks, n_chunks, planes, neg, decay, neg_lr));
+    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_apply_pair_kernel<DT, false>), dim3((n_chunks + 1) / 2),
+                                          dim3(kThreads), 0, st, seg, chunks, n_chunks, planes, plane_stride, alive,
+                                          world, tie, neg, decay, neg_lr));
+    return hipGetLastError();
+  }
+  if (DLION_K2_PAIR_MAJ && mode == 0 && world <= kMaxSliced && agree == nullptr) {
+    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_apply_pair_kernel<DT, true>), dim3((n_chunks + 1) / 2),
+                                          dim3(kThreads), 0, st, seg, chunks, n_chunks, planes, plane_stride, alive,
+                                          world, tie, neg, decay, neg_lr));
     return hipGetLastError();
   }
   if (mode == 2 || (mode == 0 && world <= kMaxSliced)) {

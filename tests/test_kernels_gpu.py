@@ -159,6 +159,31 @@ def test_prevoted_apply_matches_oracle(dtype, tie, cuda):
         _assert_close(a, b, dtype)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("world", [3, 8])
+@pytest.mark.parametrize("tie", [ref.TIE_NEGATIVE, ref.TIE_ZERO])
+def test_majority_apply_without_telemetry(dtype, world, tie, cuda):
+    """K2 majority (all-gather exchange) without the agreement counters: the
+    two-chunks-per-block kernel when built with it, else the one-chunk kernel."""
+    ps, gs, ms = _tensors(dtype, cuda, seed=4)
+    plan = FlatPlan([(p, 0) for p in ps], world=world, bucket_bytes=1 << 16, device=cuda)
+    hp = HParams(lr=3e-3, wd=0.05, beta1=0.9, beta2=0.99)
+    gen = torch.Generator(device="cpu").manual_seed(11 * world + tie)
+    planes = torch.randint(0, 256, (world * plan.total_bytes,), generator=gen, dtype=torch.uint8).to(cuda)
+    alive = torch.ones(world, dtype=torch.uint8, device=cuda)
+    alive[1] = 0
+    p2 = _clone(ps)
+    hx, tx = HipExecutor(plan), TorchExecutor(plan)
+    meta = plan.meta(gs, ms)
+    for b in plan.buckets:
+        pl = planes[world * b.byte_off: world * (b.byte_off + b.nbytes)]
+        hx.apply(meta, b, pl, b.nbytes, alive, ref.VOTE_MAJORITY, tie, None, hp)
+        tx.apply(None, _rebind(b, p2, plan), pl, b.nbytes, alive, ref.VOTE_MAJORITY, tie, None, hp)
+    torch.cuda.synchronize()
+    for a, b in zip(ps, p2):
+        _assert_close(a, b, dtype)
+
+
 def _rebind(bucket, new_params, plan):
     import copy
 
