@@ -1,4 +1,7 @@
-"""Summarize a rocprofv3 kernel_stats.csv per micro-batch: python tools/prof_summary.py <csv> [micro_batches] [top]"""
+"""Summarize a rocprofv3 kernel_stats.csv per micro-batch:
+python tools/prof_summary.py <csv> [micro_batches] [top] [steady]
+steady: drop hipBLASLt rows that ran less than once per micro-batch (the
+first step's algorithm search / candidate timing), recompute the total."""
 import csv
 import sys
 
@@ -6,6 +9,11 @@ path = sys.argv[1]
 mb = int(sys.argv[2]) if len(sys.argv) > 2 else 24
 top = int(sys.argv[3]) if len(sys.argv) > 3 else 30
 rows = list(csv.DictReader(open(path)))
+if len(sys.argv) > 4 and sys.argv[4] == "steady":
+    rows = [r for r in rows if not (r["Name"].startswith("Cijk_") and int(r["Calls"]) < 0.95 * mb)]
+    t = sum(float(r["TotalDurationNs"]) for r in rows)
+    for r in rows:
+        r["Percentage"] = str(100.0 * float(r["TotalDurationNs"]) / t)
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
 print(f"total {tot / 1e6:.1f} ms = {tot / 1e6 / mb:.2f} ms per micro-batch")
 for r in rows[:top]:
