@@ -155,18 +155,33 @@ def resolve_device(args) -> str:
 def launch_local(args) -> int:
     """``--gpus N`` without a launcher: start N rank processes (one per GPU,
     127.0.0.1 rendezvous, store hosted by this parent) and relay rank 0's JSON
-    line; any rank failing fails the run.  This parent never initialises the
-    GPU (``device_count`` only counts devices), so no HIP context is ever
-    forked or exec'd over; the children are fresh interpreters."""
+    line; any rank failing fails the run.  This parent makes no HIP call at
+    all: GPUs are counted through amdsmi or the KFD sysfs topology
+    (utils/devices.py), never ``hipGetDeviceCount`` -- so no HIP context is
+    ever forked or exec'd over; the children are fresh interpreters and
+    validate their own device (``setup_dist``)."""
     from distributed_lion_pytorch_amd.launch import run
+    from distributed_lion_pytorch_amd.utils.devices import visible_gpu_count
 
-    device = resolve_device(args)
-    if device == "cuda" and args.backend == "nccl" and torch.cuda.device_count() < args.gpus:
-        print(f"bench.py: --gpus {args.gpus} but only {torch.cuda.device_count()} GPU(s) visible; refusing to "
-              "report a smaller run", file=sys.stderr)
-        return 2
+    device = args.device
+    if device != "cpu":
+        n = visible_gpu_count()
+        if n is None and os.path.exists("/dev/kfd"):
+            print("bench.py: cannot count the GPUs without a HIP call (amdsmi and /sys/class/kfd both failed); "
+                  "run under torchrun, or pass --device cpu", file=sys.stderr)
+            return 2
+        n = n or 0
+        if device == "auto":
+            device = "cuda" if n > 0 else "cpu"
+        if device == "cuda" and args.backend == "nccl" and n < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {n} GPU(s) visible; refusing to report a smaller run",
+                  file=sys.stderr)
+            return 2
+    argv = list(sys.argv[1:])
+    if args.device == "auto":  # the children use the parent's answer (no second detection)
+        argv += ["--device", device]
     env = dict(os.environ, DLION_BENCH_LAUNCHER="bench.py")
-    return run([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus, max_failures=0,
+    return run([sys.executable, os.path.abspath(__file__)] + argv, args.gpus, max_failures=0,
                quiet_ranks=True, env=env)
 
 

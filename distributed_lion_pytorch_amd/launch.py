@@ -30,6 +30,7 @@ import argparse
 import datetime
 import json
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -68,30 +69,63 @@ def run(cmd: Sequence[str], nproc: int, max_failures: int = 0, host: str = "127.
     codes: List[Optional[int]] = [None] * nproc
     failed: List[int] = []
     rc = 0
-    while any(c is None for c in codes):
-        for r, p in enumerate(procs):
-            if codes[r] is not None:
-                continue
-            c = p.poll()
-            if c is None:
-                continue
-            codes[r] = c
-            if c != 0:
-                failed.append(r)
-                # death notice for parallel/elastic.py: survivors stop waiting for r at once
-                store.set(f"{DEATH_KEY}/{r}", str(c))
-                store.add(DEATH_COUNT_KEY, 1)
-                if len(failed) > max_failures and rc == 0:
-                    rc = c if c > 0 else 128 - c
-                    print(f"launch: rank {r} exited with {c} ({len(failed)} failures > {max_failures} tolerated); "
-                          "stopping the other ranks", file=sys.stderr, flush=True)
-                    for q in procs:
-                        if q.poll() is None:
-                            q.terminate()
-                else:
-                    print(f"launch: rank {r} exited with {c}; tolerated ({len(failed)}/{max_failures}), the other "
-                          "ranks continue", file=sys.stderr, flush=True)
-        time.sleep(0.05)
+    # a launcher that is itself signalled (scheduler SIGTERM, Ctrl-C) or fails
+    # must not orphan rank processes holding GPUs: forward the signal, then
+    # terminate / kill whatever is left (finally block)
+    prev = {}
+
+    def _forward(signum, _frame):
+        for q in procs:
+            if q.poll() is None:
+                try:
+                    q.send_signal(signum)
+                except OSError:
+                    pass
+        raise KeyboardInterrupt if signum == signal.SIGINT else SystemExit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        try:
+            prev[sig] = signal.signal(sig, _forward)
+        except ValueError:  # not the main thread: no handler, the finally block still cleans up
+            pass
+    try:
+        while any(c is None for c in codes):
+            for r, p in enumerate(procs):
+                if codes[r] is not None:
+                    continue
+                c = p.poll()
+                if c is None:
+                    continue
+                codes[r] = c
+                if c != 0:
+                    failed.append(r)
+                    # death notice for parallel/elastic.py: survivors stop waiting for r at once
+                    store.set(f"{DEATH_KEY}/{r}", str(c))
+                    store.add(DEATH_COUNT_KEY, 1)
+                    if len(failed) > max_failures and rc == 0:
+                        rc = c if c > 0 else 128 - c
+                        print(f"launch: rank {r} exited with {c} ({len(failed)} failures > {max_failures} "
+                              "tolerated); stopping the other ranks", file=sys.stderr, flush=True)
+                        for q in procs:
+                            if q.poll() is None:
+                                q.terminate()
+                    else:
+                        print(f"launch: rank {r} exited with {c}; tolerated ({len(failed)}/{max_failures}), the "
+                              "other ranks continue", file=sys.stderr, flush=True)
+            time.sleep(0.05)
+    finally:
+        for sig, h in prev.items():
+            signal.signal(sig, h)
+        live = [q for q in procs if q.poll() is None]
+        for q in live:
+            q.terminate()
+        deadline = time.monotonic() + 10.0
+        for q in live:
+            try:
+                q.wait(timeout=max(0.1, deadline - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                q.kill()
+                q.wait()
     del store
     if report:
         with open(report, "w") as f:

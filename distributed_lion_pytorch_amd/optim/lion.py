@@ -320,7 +320,7 @@ class Lion(Optimizer):
         alive = self._alive(world, plan.device)
         self._telemetry_setup(plan, xch)
         # encode bucket i, then its collective overlaps the encode of i+1
-        states = self._encode_launch(plan, ex, meta, hps, grads, moms, rank, gscale, alive)
+        states, _ = self._encode_launch(plan, ex, meta, hps, grads, moms, rank, gscale, alive)
         with phase_of(t, "exchange"):
             states = [xch.advance(b, s, alive) for b, s in zip(plan.buckets, states)]
         for b, s in zip(plan.buckets, states):
@@ -346,20 +346,39 @@ class Lion(Optimizer):
             self._tie_coords += sum(s.numel for s in plan.segments)
         self._agree_coords += sum(s.numel for s in plan.segments)
 
-    def _encode_launch(self, plan, ex, meta, hps, grads, moms, rank, gscale, alive):
+    def _encode_launch(self, plan, ex, meta, hps, grads, moms, rank, gscale, alive, guarded=False):
+        """Encode bucket i, then launch its collective (it overlaps the encode
+        of bucket i+1).  ``guarded`` (elastic mode): a launch that raises (a
+        broken group reports a dead peer at issue time) stops further launches
+        but NOT the encodes -- every bucket's momentum must advance exactly
+        once and every sign plane must be this step's, because the survivors'
+        re-vote all-gathers the whole send buffer as it stands.  Returns
+        ``(states, launch_error)``."""
         xch, stochastic, t = self._exchange, self.max_grad_norm is not None, self.phase_timer
         seed = (self.seed * 0x9E3779B1 + rank * 0x632BE59BD9B4E019 + 1) & 0x7FFFFFFFFFFFFFFF
-        states = []
+        states, err = [], None
         for b in plan.buckets:
             hp = hps[b.group]
             rr = (1.0 + 1.0 / hp.beta1) * self.max_grad_norm if stochastic else 0.0
             with phase_of(t, "encode"):
                 ex.encode(meta, b, xch.send_view(b), hp, update_m=True, stochastic=stochastic, rr=rr, seed=seed,
                           step=self._n_steps, grads=grads, moms=moms, gscale=gscale)
-                states.append(xch.launch(b, alive))
+                if err is not None:
+                    states.append(None)
+                    continue
+                try:
+                    if b.index == 1:
+                        inject_fault("raise_in_launch", self._n_steps)
+                    states.append(xch.launch(b, alive))
+                except Exception as e:  # noqa: BLE001 - re-raised unless guarded
+                    if not guarded:
+                        raise
+                    err = e
+                    states.append(None)
+                    continue
             if b.index == 0:
                 inject_fault("after_launch", self._n_steps)
-        return states
+        return states, err
 
     def _elastic_step(self, plan, ex, meta, hps, grads, moms, world, rank, gscale=None):
         """The vote as guarded collectives: the host polls each phase to
@@ -377,7 +396,9 @@ class Lion(Optimizer):
         tie = ref.TIE_CODES[self.tie_break]
         ok = True
         try:
-            states = self._encode_launch(plan, ex, meta, hps, grads, moms, rank, gscale, alive)
+            states, err = self._encode_launch(plan, ex, meta, hps, grads, moms, rank, gscale, alive, guarded=True)
+            if err is not None:
+                raise err
             with phase_of(t, "exchange"):
                 ok = el.wait_works(flatten_works(states))
                 if ok:

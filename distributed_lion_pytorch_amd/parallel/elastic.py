@@ -63,6 +63,7 @@ import torch.distributed as dist
 log = logging.getLogger(__name__)
 
 DEFAULT_GRACE_S = 5.0
+GLOO_DRAIN_S = 2.0  # after a failure signal: time gloo works get to fail on their own before being abandoned
 DEATH_KEY = "dlion/dead"  # + "/<rank>", in the root rendezvous store (written by ..launch)
 DEATH_COUNT_KEY = "dlion/dead_count"
 
@@ -167,10 +168,6 @@ class ElasticGroup:
         self._root = root
         self._dead: set = set()
         self._dead_count = 0
-        # gloo completes a collective with an error as soon as a peer's socket
-        # closes (abandoning it instead leaves a work thread that terminate()s
-        # the process at exit); RCCL kernels spin on a dead peer until aborted
-        self._spins = self.backend != "gloo"
 
     @classmethod
     def get(cls, timeout_s: float = 60.0, **kw) -> "ElasticGroup":
@@ -205,7 +202,9 @@ class ElasticGroup:
             return self._grace_fixed
         if not self._intervals:
             return min(self.timeout, DEFAULT_GRACE_S)
-        return min(self.timeout, max(1.0, 3.0 * max(self._intervals)))
+        # a gloo survivor may spend GLOO_DRAIN_S draining its works before it checks in
+        floor = 1.0 + (GLOO_DRAIN_S if self.backend == "gloo" else 0.0)
+        return min(self.timeout, max(floor, 3.0 * max(self._intervals)))
 
     def dead_members(self) -> List[int]:
         """Members the launcher reported dead (one store round trip when
@@ -229,29 +228,52 @@ class ElasticGroup:
     def wait_works(self, works) -> bool:
         """True when every work completed without error before the deadline.
         Only then is ``work.wait()`` called (it is what makes the compute
-        stream depend on the collective)."""
+        stream depend on the collective).
+
+        The launcher's death notices are consulted on EVERY backend: RCCL
+        kernels spin on a dead peer until aborted, and gloo does not reliably
+        fail a pending collective either -- with CUDA tensors a survivor whose
+        peers had already pushed their bytes sat in the bounded wait for the
+        whole ``elastic_timeout`` (round 3's 3-rank Llama-3-8B rehearsal:
+        ``regroup_s`` 120.1 s = the deadline), so a death notice ends the wait
+        within one 20 ms poll instead.  Under gloo the pending works then get
+        a short drain (``GLOO_DRAIN_S``) to fail on the closed sockets by
+        themselves: a gloo work abandoned while still running leaves a worker
+        thread that ``terminate()``s the process at exit."""
         start = time.monotonic()
         deadline = start + self.timeout
         next_check = start + 0.02
         dec = f"{self.gen}/{self.seq}/decision"
+        drain_until = None
         for w in works:
             if w is None:
                 continue
             try:
                 while not w.is_completed():
                     now = time.monotonic()
-                    if now > deadline:
+                    if now > deadline or (drain_until is not None and now > drain_until):
                         return False
-                    if now > next_check:  # a peer declared this collective failed, or died
+                    if drain_until is None and now > next_check:  # a peer declared this collective failed, or died
                         next_check = now + 0.02
-                        if self.store.check([dec]) or (self._spins and self.dead_members()):
-                            return False
+                        if self.store.check([dec]) or self.dead_members():
+                            if self.backend != "gloo":
+                                return False
+                            drain_until = now + GLOO_DRAIN_S
                     time.sleep(self._poll)
+                if drain_until is not None:  # completed after a death: do not use it
+                    try:
+                        w.wait()
+                    except Exception:  # noqa: BLE001 - expected on a closed peer
+                        pass
+                    continue
                 w.wait()
             except Exception as e:  # noqa: BLE001 - a failed collective is what this detects
                 log.warning("dlion elastic: collective failed on rank %d: %s", self.me, str(e)[:200])
+                if drain_until is None and self.backend == "gloo":
+                    drain_until = time.monotonic() + GLOO_DRAIN_S  # let the other works fail too
+                    continue
                 return False
-        return True
+        return drain_until is None
 
     # --------------------------------------------------------------- commit
     def commit(self, ok: bool) -> bool:
@@ -406,7 +428,11 @@ def flatten_works(states) -> list:
 
 
 # ---------------------------------------------------------------- fault injection
-_FAULT_PHASES = ("before_step", "backward", "after_launch", "in_allgather", "after_vote")
+_FAULT_PHASES = ("before_step", "backward", "after_launch", "in_allgather", "after_vote", "raise_in_launch")
+
+
+class InjectedLaunchError(RuntimeError):
+    """``raise_in_launch``: issuing bucket 1's vote collective failed (the rank lives on)."""
 
 
 def parse_fault(spec: Optional[str]) -> list:
@@ -415,7 +441,9 @@ def parse_fault(spec: Optional[str]) -> list:
     sockets just close) at optimizer step ``step`` in ``phase`` -- one of
     before_step, backward (inside autograd), after_launch (vote all-to-all
     issued, not completed), in_allgather (vote all-gather issued), after_vote
-    (step applied)."""
+    (step applied) -- or, for ``raise_in_launch``, raises
+    :class:`InjectedLaunchError` where bucket 1's vote collective is issued
+    (a broken group reporting at issue time; nobody dies)."""
     out = []
     for item in (spec or "").split(","):
         if not item.strip():
@@ -444,6 +472,8 @@ def inject(phase: str, step: int) -> None:
     eg = ElasticGroup.active()
     me = eg.me if eg is not None else dist.get_rank()
     if (me, step, phase) in faults:
+        if phase == "raise_in_launch":
+            raise InjectedLaunchError(f"injected launch failure on rank {me} at step {step}")
         import signal
         import sys
 

@@ -148,8 +148,13 @@ class AsyncMixin:
         :class:`ElasticGroup`: Lion's vote is guarded by it, and so are the
         collectives HF / accelerate issue on their own -- the per-step
         ``num_items_in_batch`` gather, the logging loss gather, evaluation
-        gathers -- so a worker dying anywhere leaves the survivors a
-        regrouped default group instead of a hang (parallel/elastic.py)."""
+        gathers, accelerate's ``wait_for_everyone`` -- so a worker dying in
+        the training loop leaves the survivors a regrouped default group
+        instead of a hang (parallel/elastic.py).  Not guarded: barriers outside
+        the loop -- ``main_process_first`` in the entrypoints' data
+        preparation (before training starts) and HF's ``dist.barrier()`` for
+        ``load_best_model_at_end`` -- a death there still waits for the
+        backend's timeout."""
         t = getattr(self.args, "lion_elastic_timeout", None)
         if t is None or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
             return None
@@ -341,24 +346,44 @@ class AsyncMixin:
             logger.info("restored per-rank optimizer state from %s", path)
 
 
-def replicas_identical(model: torch.nn.Module, elastic=None) -> bool:
-    """Do all ranks hold bit-identical parameters?  (an int64 digest per rank,
-    gathered -- guarded when ``elastic`` is given)."""
-    import hashlib
-
+def param_digest(model: torch.nn.Module, chunk: int = 1 << 24) -> torch.Tensor:
+    """Order-dependent digest of every parameter's raw bits, computed ON the
+    parameters' device (a 2-element int64 tensor).  Per tensor: the sum and the
+    sum of squares of the bit patterns (integer view, int64 arithmetic,
+    wrapping), mixed with the tensor's position.  Chunked, so the int64
+    temporaries stay <= 128 MB even for 8B-parameter replicas (the host
+    SHA-256 it replaces copied every parameter to the host as fp32: ~32 GB
+    per rank at Llama-3-8B)."""
     inner = getattr(model, "module", model)
-    h = hashlib.sha256()
-    for p in inner.parameters():
-        h.update(p.detach().float().cpu().numpy().tobytes())
+    acc = None
+    for i, p in enumerate(inner.parameters()):
+        x = p.detach().reshape(-1)
+        x = x.view(torch.int16) if x.element_size() == 2 else (x.view(torch.int32) if x.element_size() == 4 else
+                                                               x.view(torch.int64) if x.element_size() == 8 else
+                                                               x.view(torch.uint8))
+        s = torch.zeros(2, dtype=torch.int64, device=x.device)
+        for c in range(0, x.numel(), chunk):
+            v = x[c:c + chunk].to(torch.int64)
+            s[0] += v.sum()
+            s[1] += (v * v).sum()
+        s = s * (2 * i + 1) + i
+        acc = s if acc is None else acc * 31 + s
+    return acc if acc is not None else torch.zeros(2, dtype=torch.int64)
+
+
+def replicas_identical(model: torch.nn.Module, elastic=None) -> bool:
+    """Do all ranks hold bit-identical parameters?  (:func:`param_digest` per
+    rank, gathered -- guarded when ``elastic`` is given)."""
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
-    d = torch.tensor([int.from_bytes(h.digest()[:7], "little")], dtype=torch.int64, device=dev)
+    d = param_digest(model).to(dev)
     if elastic is not None:
         allv = elastic.all_gather(d)
     else:
         parts = [torch.empty_like(d) for _ in range(dist.get_world_size())]
         dist.all_gather(parts, d)
         allv = torch.cat(parts)
-    return len(set(allv.tolist())) == 1
+    rows = allv.reshape(-1, 2).tolist()
+    return all(r == rows[0] for r in rows)
 
 
 def _install_guarded_gathers(trainer, el) -> None:
@@ -381,6 +406,8 @@ def _install_guarded_gathers(trainer, el) -> None:
 
     trainer.accelerator.gather = guarded_gather
     hf_trainer.nested_gather = guarded_nested_gather
+    # accelerate's barrier (save_model / checkpoint paths) through the guard too
+    trainer.accelerator.wait_for_everyone = el.barrier
 
 
 class AsyncTrainer(AsyncMixin, Trainer):

@@ -96,7 +96,9 @@ class DPOTrainer(Trainer):
         super().__init__(model=model, args=args, train_dataset=train_dataset, eval_dataset=eval_dataset,
                          processing_class=tok, data_collator=DPOCollator(tok, max_length, max_prompt_length),
                          **kwargs)
-        self._stored = {}
+        self._reward_acc = None  # device [chosen, rejected, accuracy, margin, micro-batches] since the last log
+
+    _REWARD_KEYS = ("rewards/chosen", "rewards/rejected", "rewards/accuracies", "rewards/margins")
 
     def compute_loss(self, model, inputs, return_outputs=False, num_items_in_batch=None):
         ids, labels = inputs["input_ids"], inputs["labels"]
@@ -109,13 +111,27 @@ class DPOTrainer(Trainer):
             ref_logp = sequence_logps(self.ref_model, ids, labels)
         loss, r_c, r_r = dpo_loss(logp[:n], logp[n:], ref_logp[:n], ref_logp[n:], self.beta, self.loss_type,
                                   self.label_smoothing)
-        self._stored = {"rewards/chosen": r_c.mean().item(), "rewards/rejected": r_r.mean().item(),
-                        "rewards/accuracies": (r_c > r_r).float().mean().item(),
-                        "rewards/margins": (r_c - r_r).mean().item()}
+        # reward statistics stay on the device (no .item() per micro-batch: each
+        # one drained the queue, the host sync the HF nan filter fix removed);
+        # log() reads the window's means with one transfer
+        stats = torch.stack([r_c.float().mean(), r_r.float().mean(), (r_c > r_r).float().mean(),
+                             (r_c - r_r).float().mean(), torch.ones((), device=r_c.device)])
+        self._reward_acc = stats if self._reward_acc is None else self._reward_acc + stats
         return (loss, {"loss": loss}) if return_outputs else loss
 
+    def reward_stats(self, reset: bool = True) -> Dict[str, float]:
+        """Means of the reward statistics over the micro-batches since the last
+        call (one device-to-host copy)."""
+        if self._reward_acc is None:
+            return {}
+        v = self._reward_acc.tolist()
+        if reset:
+            self._reward_acc = None
+        n = max(v[4], 1.0)
+        return {k: x / n for k, x in zip(self._REWARD_KEYS, v[:4])}
+
     def log(self, logs, *args, **kwargs):
-        logs.update(self._stored)
+        logs.update(self.reward_stats())
         return super().log(logs, *args, **kwargs)
 
 

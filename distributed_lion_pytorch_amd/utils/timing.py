@@ -52,8 +52,23 @@ class PhaseTimer:
             finally:
                 self._wall[name] += 1000.0 * (time.perf_counter() - t0)
 
+    # event pairs kept before step() folds them into host sums: a timer that
+    # nobody drains (library use of the HF path without the metrics callback)
+    # must not grow without bound over a long run
+    MAX_PENDING = 4096
+
     def step(self) -> None:
         self.count += 1
+        if self.cuda and sum(len(v) for v in self._events.values()) > self.MAX_PENDING:
+            self._fold()
+
+    def _fold(self) -> None:
+        """Move the recorded event pairs into the millisecond sums (one device
+        synchronisation every ~MAX_PENDING phases)."""
+        torch.cuda.synchronize(self.device)
+        for k, v in self._events.items():
+            self._wall[k] += sum(s.elapsed_time(e) for s, e in v)
+        self._events.clear()
 
     def totals_ms(self) -> Dict[str, float]:
         """Summed milliseconds per phase (synchronises the device)."""

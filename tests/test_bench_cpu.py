@@ -89,3 +89,20 @@ def test_reference_model_keeps_hf_default_attention():
     args = argparse.Namespace(model="gpt2-tiny", dropout=None, lr=1e-4, weight_decay=0.1)
     model, _, cfg = bench.build_reference(args, torch.device("cpu"))
     assert model.config._attn_implementation == "sdpa"
+
+
+def test_kfd_topology_gpu_count(tmp_path, monkeypatch):
+    """The HIP-free GPU count's sysfs path: CPU nodes (simd_count 0) are not
+    GPUs; a visibility variable caps the count."""
+    from distributed_lion_pytorch_amd.utils import devices
+
+    for i, simds in enumerate([0, 1024, 1024, 0]):
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count {simds}\nmax_waves_per_simd 8\n")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert devices._kfd_count(str(tmp_path)) == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
+    assert devices._kfd_count(str(tmp_path)) == 1
+    assert devices._kfd_count(str(tmp_path / "missing")) is None

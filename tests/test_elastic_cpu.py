@@ -35,7 +35,7 @@ def _launch(nproc, script_args, max_failures=1, env_extra=None, timeout=300):
 
 def _stress(nproc, fault_args, steps=5):
     r = _launch(nproc, ["dropout_stress.py", "--model", "gpt2-tiny", "--device", "cpu", "--seq_len", "32",
-                        "--micro_batch", "2", "--steps", str(steps), "--elastic_timeout", "20"] + fault_args,
+                        "--micro_batch", "2", "--steps", str(steps), "--elastic_timeout", "120"] + fault_args,
                 max_failures=2)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]
@@ -60,7 +60,9 @@ def test_dropout_at_phase(phase, victim, nproc):
     # a death after the step-2 vote is applied is noticed in step 3's vote
     assert ev[0]["step"] == (3 if phase == "after_vote" else 2)
     assert [s["world"] for s in res["steps"]][-1] == nproc - 1 and len(res["steps"]) == 5
-    assert res["elastic_stall_s"] < 15.0  # bounded: well under the 20 s collective deadline
+    # bounded by the launcher's death notice, not by the 120 s collective deadline
+    # (round 3's GPU rehearsal stalled for the whole deadline: gloo never failed the wait)
+    assert res["elastic_stall_s"] < 5.0, ev
 
 
 def test_two_workers_drop_at_different_steps():
@@ -133,6 +135,43 @@ def _train(rank, world, exchange, steps):
     dist.all_reduce(t)
     return {"same_as_plain": same, "events": st["dropout_events"], "world": st["world"], "commits": st["elastic_commits"],
             "sum": float(t)}
+
+
+def _train_multibucket(rank, world, fault, steps):
+    """4 tensors, one bucket each (256-byte buckets); ``fault`` set: rank 1's
+    launch of bucket 1 raises at step 2 (nobody dies: all three regroup and
+    re-vote that step from their send buffers)."""
+    if fault:
+        os.environ["DLION_FAULT"] = "1:2:raise_in_launch"
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 4))
+    opt = Lion(model.parameters(), lr=1e-2, weight_decay=0.1, exchange="a2a", elastic_timeout=20.0,
+               backend="torch", bucket_mb=256 / (1 << 20))
+    gen = torch.Generator().manual_seed(100 + rank)
+    for _ in range(steps):
+        x = torch.randn(8, 16, generator=gen)
+        opt.zero_grad()
+        model(x).pow(2).mean().backward()
+        opt.step()
+    st = opt.stats()
+    return {"params": [p.detach().clone() for p in model.parameters()],
+            "moms": [opt.state[p]["exp_avg"].clone() for p in model.parameters()],
+            "events": st["dropout_events"], "n_buckets": st["n_buckets"]}
+
+
+def test_launch_error_at_later_bucket_encodes_every_bucket():
+    """a launch failing at bucket i>0 must not leave buckets i+1..
+    unencoded on that rank (stale sign planes in the survivors' re-vote, a
+    momentum that skips the step).  The regrouped re-vote must equal the plain
+    vote bit for bit, parameters and momenta."""
+    plain = run_world(_train_multibucket, 3, False, 4)
+    faulty = run_world(_train_multibucket, 3, True, 4)
+    assert faulty[0]["n_buckets"] >= 3, faulty[0]["n_buckets"]
+    for r in range(3):
+        assert len(faulty[r]["events"]) == 1 and faulty[r]["events"][0]["step"] == 2
+        assert faulty[r]["events"][0]["survivors"] == [0, 1, 2]
+        for a, b in zip(plain[r]["params"] + plain[r]["moms"], faulty[r]["params"] + faulty[r]["moms"]):
+            assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("exchange", ["a2a", "allgather"])

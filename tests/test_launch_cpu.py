@@ -1,0 +1,44 @@
+"""The failure-tolerant launcher (distributed_lion_pytorch_amd.launch) never
+orphans its ranks: a SIGTERM to the launcher reaches every rank process and
+the launcher reaps them before it exits."""
+import os
+import signal
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    # a zombie still answers kill(0); check its state
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().split()[2] != "Z"
+    except FileNotFoundError:
+        return False
+
+
+def test_sigterm_to_launcher_stops_every_rank(tmp_path):
+    script = tmp_path / "sleeper.py"
+    script.write_text("import os, time\n"
+                      f"open(os.path.join({str(tmp_path)!r}, 'pid' + os.environ['RANK']), 'w').write(str(os.getpid()))\n"
+                      "time.sleep(120)\n")
+    p = subprocess.Popen([sys.executable, "-m", "distributed_lion_pytorch_amd.launch", "--nproc", "2", str(script)],
+                         cwd=ROOT)
+    pids = []
+    deadline = time.monotonic() + 60
+    while time.monotonic() < deadline and len(pids) < 2:
+        pids = [int((tmp_path / f"pid{r}").read_text()) for r in range(2)
+                if (tmp_path / f"pid{r}").exists() and (tmp_path / f"pid{r}").read_text()]
+        time.sleep(0.1)
+    assert len(pids) == 2
+    p.send_signal(signal.SIGTERM)
+    rc = p.wait(timeout=30)
+    assert rc != 0
+    time.sleep(0.2)
+    assert not any(_alive(x) for x in pids), pids

@@ -93,3 +93,33 @@ def test_bench_contract_two_ranks_under_torchrun(tmp_path):
     assert out["value"] > 0 and out["higher_is_better"] is True
     assert out["wire_bytes_per_step_per_rank"] > 0
     assert abs(out["value"] - 2 * 2 * 2 * 128 * 2 / (out["ms_per_step"] * 2 / 1000)) / out["value"] < 0.01
+
+
+def test_bench_self_launch_two_ranks(tmp_path):
+    """``python bench.py --gpus 2`` with no launcher (the driver's N > 1 form
+    minus torchrun): the parent counts GPUs without a HIP call
+    (utils/devices.py), starts two rank processes itself, and rank 0's JSON
+    line reports both ranks (gloo on the one GPU) with measured wire bytes."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--backend", "gloo",
+           "--model", "gpt2-tiny", "--micro_batch", "2", "--grad_accum", "2", "--seq_len", "128"]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["launcher"] == "bench.py" and out["device"].startswith("cuda")
+    assert out["wire_bytes_per_step_per_rank"] > 0
+
+
+def test_visible_gpu_count_without_hip():
+    """The launcher-side GPU count (amdsmi / KFD sysfs) sees the box's GPU."""
+    from distributed_lion_pytorch_amd.utils.devices import visible_gpu_count
+
+    assert visible_gpu_count() == torch.cuda.device_count() >= 1
