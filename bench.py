@@ -92,7 +92,8 @@ def parse():
     ap.add_argument("--fuse_accum", type=int, default=1, help="gradient-accumulation fusion (ops/linear.py)")
     ap.add_argument("--max_grad_norm", type=float, default=1.0)
     ap.add_argument("--exchange", default="a2a", help="allgather | a2a | ref_int64")
-    ap.add_argument("--bucket_mb", type=float, default=32.0)
+    ap.add_argument("--bucket_mb", type=float, default=None,
+                    help="vote bucket size in MB (default: automatic, >= 4 buckets of 1-32 MB at W > 1)")
     ap.add_argument("--impl", default="native", choices=["native", "reference"])
     ap.add_argument("--fused", default="auto", choices=["auto", "torch", "hip"])
     ap.add_argument("--dropout", type=float, default=None, help="override GPT-2 dropout (default 0.1)")

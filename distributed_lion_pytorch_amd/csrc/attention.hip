@@ -47,26 +47,9 @@
 #ifndef DLION_ATTN_NT
 #define DLION_ATTN_NT 0
 #endif
-// software-pipelined forward (D = 64) and dQ main loops
 // key tiles per barrier in the D = 64 forward
 #ifndef DLION_FWD_NT64
 #define DLION_FWD_NT64 2
-#endif
-#ifndef DLION_FWD_PIPE
-#define DLION_FWD_PIPE 0
-#endif
-// dQ with NT > 1: process the NT tiles of a barrier interval one after the other
-#ifndef DLION_DQ_SEQ
-#define DLION_DQ_SEQ 0
-#endif
-#ifndef DLION_DQ_PIPE
-#define DLION_DQ_PIPE 0
-#endif
-#ifndef DLION_DKV_PIPE
-#define DLION_DKV_PIPE 0
-#endif
-#ifndef DLION_DKV_PIPE_WAVES64
-#define DLION_DKV_PIPE_WAVES64 1
 #endif
 #ifndef DLION_DKV_WAVES128
 #define DLION_DKV_WAVES128 1
@@ -97,23 +80,54 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-// drop hash: 32 random bits shared by keys (2i, 2i+1) of query q, in two
-// stages so the per-pair cost is one full-rate 24-bit multiply (v_mul_lo_u32
-// is a quarter-rate op and the attention kernels are VALU-bound at D=64: ~22
-// VALU instructions per MFMA; the first version's two per pair cost ~20% of
-// the backward):
+// drop hash (v2): 32 random bits shared by keys (2i, 2i+1) of query q, in two
+// stages so the per-pair cost is one full-rate 24-bit multiply:
 //   arow(bh, q)  = lowbias32(seed ^ bh*0x9E3779B9 ^ q*0x85EBCA6B)   (per row)
-//   hash(q, key) = mix1(arow ^ (key>>1)*0xC2B2AE35),
+//   hash(q, key) = mix1(arow + (key>>1)*kKeyMul),
 //   mix1(x) = y ^ (y >> 16),  y = (x mod 2^24) * 0x9E3779  (v_mul_u32_u24)
-// low 16 bits for the even key.  Keep tests run in the high half (one shift
-// for the low half, none for the high one): with thr_hi = thresh16 << 16,
-//   keep(even) = (hash << 16) >= thr_hi,  keep(odd) = hash >= thr_hi.
+// The key enters by ADDITION (v1 xored it in): per tile the row constant and
+// the tile's pair base fold into one register, and each pair costs one
+// v_add with a literal + v_mul_u32_u24 + v_xor_b32_sdwa.
+// Keep test, two keys at once on the packed halves (low = even key): the
+// halves are read as SIGNED 16-bit values s and a key is kept iff
+// s >= thresh16 - 32768 (same keep probability 1 - thresh16/65536 as an
+// unsigned compare).  keep_mask2 gives 0xFFFF per kept half with a saturating
+// v_pk_sub_i16 and a v_pk_ashrrev_i16 -- no v_cmp / VCC / v_cndmask (v1's
+// per-element compare + select, with the VCC-hazard s_nops between them, was
+// ~45 % of the forward's VALU work) -- and is applied to the packed bf16
+// operand dword with one v_and (P) or v_bfi_b32 (dS).
+constexpr uint32_t kKeyMul = 0xC2B2AE35u;
 __device__ __forceinline__ uint32_t drop_row(uint32_t seed, uint32_t bh, uint32_t q) {
   return lowbias32(seed ^ (bh * 0x9E3779B9u) ^ (q * 0x85EBCA6Bu));
 }
 __device__ __forceinline__ uint32_t mix1(uint32_t x) {
   x = __umul24(x, 0x9E3779u);
   return x ^ (x >> 16);
+}
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// tm1 = (thresh16 - 32769) mod 2^16 in both halves (thresh16 >= 1)
+__device__ __forceinline__ uint32_t drop_tm1(uint32_t thresh16) {
+  const uint32_t t = (thresh16 - 32769u) & 0xFFFFu;
+  return t | (t << 16);
+}
+// 0xFFFF per half whose signed random u16 is >= tm1 + 1 (kept), else 0
+__device__ __forceinline__ uint32_t keep_mask2(uint32_t u, uint32_t tm1) {
+  const s16x2 d = __builtin_elementwise_sub_sat(__builtin_bit_cast(s16x2, tm1), __builtin_bit_cast(s16x2, u));
+  const s16x2 m = d >> (s16x2){15, 15};
+  return __builtin_bit_cast(uint32_t, m);
+}
+// (m & a) | (~m & b) as one v_bfi_b32 (written as C, hipcc turns it back
+// into per-half compares and selects)
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+// two floats -> packed bf16 (v_cvt_pk_bf16_f32, RNE), low half = a
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+  const bf16x2 v = {static_cast<__bf16>(a), static_cast<__bf16>(b)};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 // x op x(lane ^ 32) via v_permlane32_swap (guide T12): no LDS round trip,
@@ -149,6 +163,43 @@ __device__ __forceinline__ bf16x8 acc_frag(const f32x16& x, int s) {
   return r;
 }
 __device__ __forceinline__ int acc_row(int reg, int hf) { return (reg & 3) + 8 * (reg >> 2) + 4 * hf; }
+// key-pair index, relative to the tile's pair base (key >> 1 of the lane's
+// first key: kt*16 + 2hf), of the two keys in dword i (regs 8s+2i, 8s+2i+1)
+// of acc_frag(x, s)
+__device__ __forceinline__ constexpr int frag_pair(int s, int i) { return (i & 1) + 4 * (i >> 1) + 8 * s; }
+
+// P^T operand (query on the lane, keys in registers) with the dropout mask
+// applied to the packed bf16 pairs.  pbase = arow + (kt*16 + 2hf) * kKeyMul.
+template <bool DROP>
+__device__ __forceinline__ bf16x8 p_frag(const f32x16& x, int s, uint32_t pbase, uint32_t tm1) {
+  bf16x8 f = acc_frag(x, s);
+  if constexpr (DROP) {
+    i32x4 d = __builtin_bit_cast(i32x4, f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[i] &= keep_mask2(mix1(pbase + frag_pair(s, i) * kKeyMul), tm1);
+    f = __builtin_bit_cast(bf16x8, d);
+  }
+  return f;
+}
+// dS^T operand of the dQ kernel: dS = P (keep ? dP : 0) - P delta, built as
+// both packed candidates and merged per half by the keep mask (one v_bfi_b32)
+template <bool DROP>
+__device__ __forceinline__ bf16x8 ds_frag(const f32x16& p, const f32x16& dp, float dlt, int s, uint32_t pbase,
+                                          uint32_t tm1) {
+  i32x4 d;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r0 = 8 * s + 2 * i;
+    if constexpr (DROP) {
+      const float a0 = p[r0] * dlt, a1 = p[r0 + 1] * dlt;
+      const uint32_t kv = pk2(__builtin_fmaf(p[r0], dp[r0], -a0), __builtin_fmaf(p[r0 + 1], dp[r0 + 1], -a1));
+      d[i] = bfi(keep_mask2(mix1(pbase + frag_pair(s, i) * kKeyMul), tm1), kv, pk2(-a0, -a1));
+    } else {
+      d[i] = pk2(p[r0] * (dp[r0] - dlt), p[r0 + 1] * (dp[r0 + 1] - dlt));
+    }
+  }
+  return __builtin_bit_cast(bf16x8, d);
+}
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -307,16 +358,13 @@ struct QBlock {
 // NT key tiles (32 keys each) per barrier: with NT = 2 every wave has two
 // independent QK^T chains and two PV chains per iteration, so hipcc can put one
 // tile's MFMAs beside the other's softmax VALU work; with NT = 1 each step of
-// the QK -> max -> exp -> PV chain waits for the previous one.
-// PIPE (NT = 1): software-pipelined -- tile kt+1's QK^T MFMAs are issued
-// before tile kt's softmax VALU work and PV MFMAs (4-slot K/V ring: kt for PV,
-// kt+1 for QK^T, kt+2 / kt+3 in flight).
-template <int D, bool DROP, int NT, bool PIPE = false>
+// the QK -> max -> exp -> PV chain waits for the previous one.  (Software-
+// pipelined variants -- QK^T of the next tile issued before this tile's
+// softmax -- measured neutral to -1 % in round 3 and were removed.)
+template <int D, bool DROP, int NT>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
-  static_assert(!PIPE || NT == 1, "the pipelined forward streams single key tiles");
-  constexpr int NB = PIPE ? 4 : 2;
-  __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[NB][NT];
-  __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[NB][NT];
+  __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[2][NT];
+  __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[2][NT];
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
   const QBlock blk(a.B * a.H, ntiles32(a.T));
   const int bh = blk.bh, qtile = blk.qtile, last = blk.last;
@@ -339,84 +387,10 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 
   const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
   const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
-  const uint32_t arow = drop_row(a.seed, bh, q);
-  const uint32_t thr_hi = a.thresh16 << 16;
+  // dropout: the row's pair base, advanced by 16 pairs per key tile
+  const uint32_t prow = drop_row(a.seed, bh, q) + static_cast<uint32_t>(2 * hf) * kKeyMul;
+  const uint32_t tm1 = drop_tm1(a.thresh16);
   const DmaTile<D> kd(a.k_st), vd(a.v_st);
-  if constexpr (PIPE) {
-    auto stage1 = [&](int kt) {
-      const int row = kt * 32;
-      kd.issue(kg + static_cast<int64_t>(row) * a.k_st, ks_[kt & 3][0], a.T - row);
-      vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[kt & 3][0], a.T - row);
-    };
-    auto qk = [&](int kt, f32x16& sc) {
-      sc = zero16();
-#pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) sc = mfma32(row_frag<D>(ks_[kt & 3][0], r, ks, hf), qf[ks], sc);
-    };
-    auto softmax_pv = [&](int kt, f32x16& sc) {
-      if (kt == qtile) {  // causal mask on the diagonal tile only (scalar branch)
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg)
-          if (kt * 32 + acc_row(reg, hf) > q) sc[reg] = -INFINITY;
-      }
-      float tmax = sc[0];
-#pragma unroll
-      for (int reg = 1; reg < 16; ++reg) tmax = fmaxf(tmax, sc[reg]);
-      tmax = xmax32(tmax) * a.scale_log2;
-      float alpha = 1.f;
-      if (!__all(tmax - m <= kDeferLog2)) {  // deferred rescale, as below
-        const float mn = fmaxf(m, tmax);
-        alpha = __builtin_amdgcn_exp2f(m - mn);
-        m = mn;
-#pragma unroll
-        for (int t = 0; t < D / 32; ++t)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) oacc[t][i] *= alpha;
-      }
-      float rs = 0.f;
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[reg], a.scale_log2, -m));
-        rs += p;
-        sc[reg] = p;
-      }
-      l = l * alpha + xsum32(rs);
-      if constexpr (DROP) {
-#pragma unroll
-        for (int reg = 0; reg < 16; reg += 2) {
-          const uint32_t key = kt * 32 + acc_row(reg, hf);
-          const uint32_t hsh = mix1(arow ^ ((key >> 1) * 0xC2B2AE35u));
-          if ((hsh << 16) < thr_hi) sc[reg] = 0.f;
-          if (hsh < thr_hi) sc[reg + 1] = 0.f;
-        }
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pf = acc_frag(sc, s2);
-#pragma unroll
-        for (int t = 0; t < D / 32; ++t) oacc[t] = mfma32(tr_frag<D>(vs_[kt & 3][0], s2, t, lane), pf, oacc[t]);
-      }
-    };
-    for (int j = 0; j < 3 && j <= last; ++j) stage1(j);
-    vm_wait_n(min(last, 2) * 2 * DmaTile<D>::PPW);  // tile 0 landed (tiles 1, 2 may be in flight)
-    __syncthreads();
-    f32x16 sA, sB;
-    if (blk.active) qk(0, sA);
-    auto step = [&](int kt, f32x16& sc, f32x16& sn) {
-      // tile kt+1 landed (kt+2 may be in flight); every wave is done with tile kt-1's slot
-      vm_wait_n((last - kt - 1 >= 1 ? 1 : 0) * 2 * DmaTile<D>::PPW);
-      __syncthreads();
-      if (kt + 3 <= last) stage1(kt + 3);
-      if (blk.active && kt <= qtile) {  // wave-uniform
-        if (kt + 1 <= qtile) qk(kt + 1, sn);
-        softmax_pv(kt, sc);
-      }
-    };
-    for (int kt = 0; kt <= last; kt += 2) {  // unrolled by two: the score registers swap roles
-      step(kt, sA, sB);
-      if (kt + 1 <= last) step(kt + 1, sB, sA);
-    }
-  } else {
   // tiles past `last` re-read tile `last` (valid memory); the causal mask
   // zeroes them, since they lie beyond every query of the block
   auto stage = [&](int first, int buf) {
@@ -479,22 +453,13 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
           s[j][reg] = p;
         }
       l = l * alpha + xsum32(rs);
-      if constexpr (DROP) {  // 1/(1-p) is applied once to O at the end
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-          for (int reg = 0; reg < 16; reg += 2) {  // regs (2i, 2i+1) hold keys (2j, 2j+1)
-            const uint32_t key = (kt + j) * 32 + acc_row(reg, hf);
-            const uint32_t hsh = mix1(arow ^ ((key >> 1) * 0xC2B2AE35u));
-            if ((hsh << 16) < thr_hi) s[j][reg] = 0.f;
-            if (hsh < thr_hi) s[j][reg + 1] = 0.f;
-          }
-      }
+      // PV with the dropout mask on the packed bf16 P pairs (1/(1-p) is
+      // applied once to O at the end)
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 pf = acc_frag(s[j], s2);
+          const bf16x8 pf = p_frag<DROP>(s[j], s2, prow + static_cast<uint32_t>((kt + j) * 16) * kKeyMul, tm1);
 #pragma unroll
           for (int t = 0; t < D / 32; ++t)
             oacc[t] = mfma32(tr_frag<D>(vs_[buf][j], s2, t, lane), pf, oacc[t]);
@@ -502,7 +467,6 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     }
     vm_wait0();  // this wave's pieces of the next tiles have landed
     __syncthreads();
-  }
   }
   if (!blk.active || q >= a.T) return;
   const float inv_l = (DROP ? a.inv_keep : 1.f) / l;
@@ -525,16 +489,12 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 }
 
 // --------------------------------------------------------------- backward dQ
-// NT key tiles per barrier (see the forward).  PIPE: software-pipelined single
-// tiles -- S^T / dP^T of tile kt+1 are issued to the MFMA pipe before tile kt's
-// exp / dropout / dS VALU work and its dQ MFMAs, so the two overlap inside one
-// basic block; a 4-slot ring keeps tile kt (K for dQ), kt+1 (K, V for S / dP)
-// resident and kt+2, kt+3 in flight.
-template <int D, bool DROP, int NT, bool PIPE>
+// NT key tiles per barrier (see the forward).  (Round 3's software-pipelined
+// and sequential-NT variants measured neutral and were removed.)
+template <int D, bool DROP, int NT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? DLION_DQ_WAVES64 : 1)))
 attn_bwd_dq_kernel(AttnArgs a) {
-  static_assert(!PIPE || NT == 1, "the pipelined dQ loop streams single key tiles");
-  constexpr int NB = PIPE ? 4 : DLION_ATTN_STAGES;
+  constexpr int NB = DLION_ATTN_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[NB][NT];
   __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[NB][NT];
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
@@ -572,77 +532,14 @@ attn_bwd_dq_kernel(AttnArgs a) {
     if (a.thresh16) dlt /= a.inv_keep;  // delta * (1-p), see the forward's lse note
     if (hf == 0 && q < a.T) const_cast<float*>(a.delta)[static_cast<int64_t>(bh) * a.T + q] = dlt;
   }
-  const uint32_t thr_hi = a.thresh16 << 16;
-  const uint32_t arow = drop_row(a.seed, bh, q);
+  const uint32_t prow = drop_row(a.seed, bh, q) + static_cast<uint32_t>(2 * hf) * kKeyMul;
+  const uint32_t tm1 = drop_tm1(a.thresh16);
   f32x16 dq[D / 32];
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) dq[t] = zero16();
   const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
   const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
   const DmaTile<D> kd(a.k_st), vd(a.v_st);
-  if constexpr (PIPE) {
-    auto stage1 = [&](int kt) {
-      const int row = kt * 32;
-      kd.issue(kg + static_cast<int64_t>(row) * a.k_st, ks_[kt & 3][0], a.T - row);
-      vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[kt & 3][0], a.T - row);
-    };
-    auto sdp = [&](int kt, f32x16& s, f32x16& dp) {  // S^T = K Q^T, dP^T = V dO^T of key tile kt
-      s = zero16();
-      dp = zero16();
-#pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) {
-        s = mfma32(row_frag<D>(ks_[kt & 3][0], r, ks, hf), qf[ks], s);
-        dp = mfma32(row_frag<D>(vs_[kt & 3][0], r, ks, hf), dof[ks], dp);
-      }
-    };
-    auto finish = [&](int kt, f32x16& s, const f32x16& dp) {  // dS^T of tile kt, then dQ += dS K
-      const int kb = kt * 32;
-      if (kt == qtile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg)
-          if (kb + acc_row(reg, hf) > q) s[reg] = -INFINITY;
-      }
-#pragma unroll
-      for (int reg = 0; reg < 16; reg += 2) {
-        const int key = kb + acc_row(reg, hf);
-        uint32_t hsh = 0;
-        if constexpr (DROP) hsh = mix1(arow ^ ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u));
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg + e], a.scale_log2, -lse2));
-          float dpv = dp[reg + e];
-          if constexpr (DROP) dpv = ((e == 0 ? hsh << 16 : hsh) >= thr_hi) ? dpv : 0.f;
-          s[reg + e] = p * (dpv - dlt);
-        }
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 dsf = acc_frag(s, s2);
-#pragma unroll
-        for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tr_frag<D>(ks_[kt & 3][0], s2, t, lane), dq[t]);
-      }
-    };
-    for (int j = 0; j < 3 && j <= last; ++j) stage1(j);
-    vm_wait_n(min(last, 2) * 2 * DmaTile<D>::PPW);  // tile 0 landed (tiles 1, 2 may be in flight)
-    __syncthreads();
-    f32x16 sA, dpA, sB, dpB;
-    if (blk.active) sdp(0, sA, dpA);
-    // step kt: (sc, dc) hold tile kt's S^T / dP^T; tile kt+1's go to (sn, dn)
-    auto step = [&](int kt, f32x16& sc, f32x16& dc, f32x16& sn, f32x16& dn) {
-      // tile kt+1 landed (kt+2 may be in flight); every wave is done with tile kt-1's slot
-      vm_wait_n((last - kt - 1 >= 1 ? 1 : 0) * 2 * DmaTile<D>::PPW);
-      __syncthreads();
-      if (kt + 3 <= last) stage1(kt + 3);
-      if (blk.active && kt <= qtile) {  // wave-uniform
-        if (kt + 1 <= qtile) sdp(kt + 1, sn, dn);
-        finish(kt, sc, dc);
-      }
-    };
-    for (int kt = 0; kt <= last; kt += 2) {  // unrolled by two: the register sets swap roles, no copies
-      step(kt, sA, dpA, sB, dpB);
-      if (kt + 1 <= last) step(kt + 1, sB, dpB, sA, dpA);
-    }
-  } else {
   // super-tile st = key tiles st*NT .. st*NT+NT-1, one LDS slot each; tiles
   // past `last` re-read tile `last` (valid memory) and are masked below
   auto stage = [&](int st, int buf) {
@@ -662,46 +559,7 @@ attn_bwd_dq_kernel(AttnArgs a) {
     __syncthreads();  // ... for every wave; and every wave is done with the buffer restaged next
     if (st + NB - 1 < ns) stage(st + NB - 1, (st + NB - 1) % NB);
     const int kt0 = st * NT;
-    if (DLION_DQ_SEQ && NT > 1) {
-      // NT tiles per barrier processed one after the other in one register
-      // set: only the barrier count drops (no second S / dP chain)
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int kt = kt0 + j;
-        if (!(blk.active && kt <= qtile)) continue;  // wave-uniform (past-the-diagonal tiles: skipped)
-        const int kb = kt * 32;
-        f32x16 s = zero16(), dp = zero16();
-#pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          s = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), qf[ks], s);
-          dp = mfma32(row_frag<D>(vs_[buf][j], r, ks, hf), dof[ks], dp);
-        }
-        if (kt == qtile) {
-#pragma unroll
-          for (int reg = 0; reg < 16; ++reg)
-            if (kb + acc_row(reg, hf) > q) s[reg] = -INFINITY;
-        }
-#pragma unroll
-        for (int reg = 0; reg < 16; reg += 2) {
-          const int key = kb + acc_row(reg, hf);
-          uint32_t hsh = 0;
-          if constexpr (DROP) hsh = mix1(arow ^ ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u));
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg + e], a.scale_log2, -lse2));
-            float dpv = dp[reg + e];
-            if constexpr (DROP) dpv = ((e == 0 ? hsh << 16 : hsh) >= thr_hi) ? dpv : 0.f;
-            s[reg + e] = p * (dpv - dlt);
-          }
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 dsf = acc_frag(s, s2);
-#pragma unroll
-          for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tr_frag<D>(ks_[buf][j], s2, t, lane), dq[t]);
-        }
-      }
-    } else if (blk.active && kt0 <= qtile) {
+    if (blk.active && kt0 <= qtile) {
       // NT independent S / dP chains: one tile's exp / hash VALU work can sit
       // beside the other's MFMAs
       f32x16 s[NT], dp[NT];
@@ -725,28 +583,18 @@ attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
-        for (int reg = 0; reg < 16; reg += 2) {
-          const int key = (kt0 + j) * 32 + acc_row(reg, hf);  // even: regs (reg, reg+1) = keys (key, key+1)
-          uint32_t hsh = 0;
-          if constexpr (DROP) hsh = mix1(arow ^ ((static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u));
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][reg + e], a.scale_log2, -lse2));
-            float dpv = dp[j][reg + e];
-            if constexpr (DROP) dpv = ((e == 0 ? hsh << 16 : hsh) >= thr_hi) ? dpv : 0.f;  // p, dlt carry 1/(1-p)
-            s[j][reg + e] = p * (dpv - dlt);  // dS^T
-          }
-        }
+        for (int reg = 0; reg < 16; ++reg)
+          s[j][reg] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][reg], a.scale_log2, -lse2));  // p, carries 1/(1-p)
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 dsf = acc_frag(s[j], s2);
+          const bf16x8 dsf = ds_frag<DROP>(s[j], dp[j], dlt, s2,
+                                           prow + static_cast<uint32_t>((kt0 + j) * 16) * kKeyMul, tm1);  // dS^T
 #pragma unroll
           for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tr_frag<D>(ks_[buf][j], s2, t, lane), dq[t]);  // dQ += dS K
         }
     }
-  }
   }
   if (!blk.active) return;
   // dq[t]: rows = q (registers), cols = d (lane)
@@ -777,17 +625,16 @@ attn_bwd_dq_kernel(AttnArgs a) {
 // -------------------------------------------------------------- backward dKV
 // 4 waves = 4 consecutive key tiles of one (b, kv-head); every query tile of
 // every head in the GQA group is staged once per block (Q, dO and the 32
-// lse / delta values).  Low key groups (most query tiles) go first.
-// PIPE: software-pipelined -- step i+1's S / dP MFMAs are issued before step
-// i's softmax-gradient VALU work and its dV / dK MFMAs (4-slot ring: i for the
-// transposed reads and row statistics, i+1 for S / dP, i+2 / i+3 in flight).
-template <int D, bool DROP, bool PIPE = false>
+// lse / delta values).  Low key groups (most query tiles) go first.  (Round
+// 3's software-pipelined variant measured -1 % and was removed.)
+template <int D, bool DROP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    D == 64 ? (PIPE ? DLION_DKV_PIPE_WAVES64 : DLION_DKV_WAVES64) : DLION_DKV_WAVES128)))
+    D == 64 ? DLION_DKV_WAVES64 : DLION_DKV_WAVES128)))
 attn_bwd_dkv_kernel(AttnArgs a) {
-  constexpr int NB = PIPE ? 4 : DLION_ATTN_STAGES;
+  constexpr int NB = DLION_ATTN_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> qs_[NB];
   __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[NB];
+  __shared__ __attribute__((aligned(16))) LdsTile<D> kvs_[2][4];  // [K | V][wave's key tile]
   __shared__ __attribute__((aligned(16))) float ls_[NB][3][32];  // [buf][lse | delta | drop row key][row]
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntiles = ntiles32(a.T), nbhk = a.B * a.Hkv;
@@ -798,16 +645,21 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   const int first = grp * 4;  // the block's first query tile = its lowest key tile
   const int b = bhk / a.Hkv, hk = bhk % a.Hkv, group = a.H / a.Hkv;
   const int kb = ktile * 32, key = kb + r;
-  const int kc = min(key, a.T - 1);  // tail keys: a copy of key T-1, never stored
 
-  bf16x8 kf[D / 16], vf[D / 16];
-  if (active) {
-    const __bf16* kp = a.k + b * a.k_sb + static_cast<int64_t>(kc) * a.k_st + hk * a.k_sh + 8 * hf;
-    const __bf16* vp = a.v + b * a.v_sb + static_cast<int64_t>(kc) * a.v_st + hk * a.v_sh + 8 * hf;
+  // the block's 4 key tiles of K and V go to LDS once (LDS-DMA, issued before
+  // the first Q / dO stage, so the first step's wait covers them): the
+  // B operands of S = Q K^T and dP = dO V^T are read from there per step
+  // instead of living in 16 * D / 32 VGPRs for the whole kernel (round 3 held
+  // them in registers: 168 VGPRs at the 3-wave floor, no room left)
+  {
+    const DmaTile<D> kd(a.k_st), vd(a.v_st);
 #pragma unroll
-    for (int s = 0; s < D / 16; ++s) {
-      kf[s] = ld8(kp + 16 * s);
-      vf[s] = ld8(vp + 16 * s);
+    for (int j = 0; j < 4; ++j) {
+      const int row = (first + j) * 32;
+      if (row < a.T) {  // block-uniform
+        kd.issue(a.k + b * a.k_sb + hk * a.k_sh + static_cast<int64_t>(row) * a.k_st, kvs_[0][j], a.T - row);
+        vd.issue(a.v + b * a.v_sb + hk * a.v_sh + static_cast<int64_t>(row) * a.v_st, kvs_[1][j], a.T - row);
+      }
     }
   }
   f32x16 dk[D / 32], dv[D / 32];
@@ -816,7 +668,12 @@ attn_bwd_dkv_kernel(AttnArgs a) {
     dk[t] = zero16();
     dv[t] = zero16();
   }
-  const uint32_t thr_hi = a.thresh16 << 16, kshift = (key & 1) ? 0u : 16u;
+  // dropout: the lane is the key, so each element needs its own hash (the key
+  // pair's other key is in the neighbouring lane); v_perm_b32 gathers the
+  // lane's 16-bit halves of two rows' hashes into one packed pair (low half
+  // for an even key, high half for an odd one)
+  const uint32_t tm1 = drop_tm1(a.thresh16), sel = (key & 1) ? 0x07060302u : 0x05040100u;
+  const uint32_t kmix = (static_cast<uint32_t>(key) >> 1) * kKeyMul;
   const DmaTile<D> qd(a.q_st), dd(a.o_st);
   const int nq = ntiles - first;   // query tiles per head
   const int total = group * nq;    // (head, query tile) steps, head-major
@@ -837,126 +694,45 @@ attn_bwd_dkv_kernel(AttnArgs a) {
       ls_[buf][2][lane] = __uint_as_float(drop_row(a.seed, bh, qt * 32 + lane));
     }
   };
-  const uint32_t kmix = (static_cast<uint32_t>(key) >> 1) * 0xC2B2AE35u;
   for (int j = 0; j < NB - 1 && j < total; ++j) stage(j, j);
   // LDS-DMA pieces per stage: Q + dO tiles, and wave 0's lse / delta row values
   const int per_stage = 2 * DmaTile<D>::PPW + (w == 0 ? 1 : 0);
-  // S = Q K^T (rows q, cols key) and dP = dO V^T of step i from its slot
-  auto sdp = [&](int i, f32x16& s, f32x16& dp) {
+  for (int i = 0; i < total; ++i) {
     const int buf = i % NB;
-    s = zero16();
-    dp = zero16();
+    vm_wait_n(min(total - 1 - i, NB - 2) * per_stage);  // step i landed (later steps may be in flight)
+    __syncthreads();  // for every wave; and every wave is done with the buffer restaged next
+    if (i + NB - 1 < total) stage(i + NB - 1, (i + NB - 1) % NB);
+    const int qt = first + i % nq;
+    if (active && qt >= ktile) {  // wave-uniform
+      const int qb = qt * 32;
+      f32x16 s = zero16(), dp = zero16();
 #pragma unroll
-    for (int ks = 0; ks < D / 16; ++ks) {
-      s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), kf[ks], s);
-      dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), vf[ks], dp);
-    }
-  };
-  // masks, P / dS from the step's row statistics, dV += Pd^T dO, dK += dS^T Q
-  auto finish = [&](int i, f32x16& s, const f32x16& dp) {
-    const int buf = i % NB;
-    const int qt = first + i % nq, qb = qt * 32;
-    if (qt == ktile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg)
-        if (key > qb + acc_row(reg, hf)) s[reg] = -INFINITY;
-    }
-    if (qb + 32 > a.T) {  // tail query tile: rows past T contribute nothing (p = 0, dS = 0)
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg)
-        if (qb + acc_row(reg, hf) >= a.T) s[reg] = -INFINITY;
-    }
-    // row statistics of the lane's 16 query rows: rows (reg&3) + 8(reg>>2) + 4hf
-    // come in 4 runs of 4 consecutive rows -> 16-byte LDS reads (broadcast),
-    // consumed run by run (not all 48 values staged up front: that held the
-    // kernel at 212 VGPRs, two waves per SIMD)
-    f32x16 pd;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float4 lv = *reinterpret_cast<const float4*>(&ls_[buf][0][8 * g + 4 * hf]);
-      const float4 dv4 = *reinterpret_cast<const float4*>(&ls_[buf][1][8 * g + 4 * hf]);
-      uint4 av = make_uint4(0, 0, 0, 0);
-      if constexpr (DROP) av = *reinterpret_cast<const uint4*>(&ls_[buf][2][8 * g + 4 * hf]);
-      const float lse_g[4] = {lv.x, lv.y, lv.z, lv.w};
-      const float dl_g[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
-      const uint32_t ar_g[4] = {av.x, av.y, av.z, av.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int reg = 4 * g + e;
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -lse_g[e]));
-        float dpv = dp[reg];
-        float pdv = p;
-        if constexpr (DROP) {  // the lane is the key here: one (cheap) hash per element;
-                               // p and the delta row values already carry 1/(1-p)
-          const bool kp_ = (mix1(ar_g[e] ^ kmix) << kshift) >= thr_hi;
-          dpv = kp_ ? dpv : 0.f;
-          pdv = kp_ ? p : 0.f;
-        }
-        pd[reg] = pdv;
-        s[reg] = p * (dpv - dl_g[e]);  // dS
+      for (int ks = 0; ks < D / 16; ++ks) {
+        s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), row_frag<D>(kvs_[0][w], r, ks, hf), s);   // S = Q K^T
+        dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), row_frag<D>(kvs_[1][w], r, ks, hf), dp);  // dP = dO V^T
       }
-    }
+      if (qt == ktile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 pf = acc_frag(pd, s2);
-      const bf16x8 dsf = acc_frag(s, s2);
-#pragma unroll
-      for (int t = 0; t < D / 32; ++t) {
-        dv[t] = mfma32(pf, tr_frag<D>(ds_[buf], s2, t, lane), dv[t]);   // dV += Pd^T dO
-        dk[t] = mfma32(dsf, tr_frag<D>(qs_[buf], s2, t, lane), dk[t]);  // dK += dS^T Q
+        for (int reg = 0; reg < 16; ++reg)
+          if (key > qb + acc_row(reg, hf)) s[reg] = -INFINITY;
       }
-    }
-  };
-  auto live = [&](int i) { return active && first + i % nq >= ktile; };  // wave-uniform
-  if constexpr (PIPE) {
-    f32x16 sA, dpA, sB, dpB;
-    vm_wait_n(min(total - 1, NB - 2) * per_stage);  // step 0 landed (steps 1, 2 may be in flight)
-    __syncthreads();
-    if (live(0)) sdp(0, sA, dpA);
-    auto step = [&](int i, f32x16& sc, f32x16& dc, f32x16& sn, f32x16& dn) {
-      // step i+1 landed (i+2 may be in flight); every wave is done with step i-1's slot
-      vm_wait_n((total - 1 - i >= 2 ? 1 : 0) * per_stage);
-      __syncthreads();
-      if (i + NB - 1 < total) stage(i + NB - 1, (i + NB - 1) % NB);
-      if (i + 1 < total && live(i + 1)) sdp(i + 1, sn, dn);
-      if (live(i)) finish(i, sc, dc);
-    };
-    for (int i = 0; i < total; i += 2) {  // unrolled by two: the register sets swap roles, no copies
-      step(i, sA, dpA, sB, dpB);
-      if (i + 1 < total) step(i + 1, sB, dpB, sA, dpA);
-    }
-  } else {  // (the straight loop, kept verbatim: routing it through the lambdas above spills 16 dwords)
-    for (int i = 0; i < total; ++i) {
-      const int buf = i % NB;
-      vm_wait_n(min(total - 1 - i, NB - 2) * per_stage);  // step i landed (later steps may be in flight)
-      __syncthreads();  // for every wave; and every wave is done with the buffer restaged next
-      if (i + NB - 1 < total) stage(i + NB - 1, (i + NB - 1) % NB);
-      const int qt = first + i % nq;
-      if (active && qt >= ktile) {  // wave-uniform
-        const int qb = qt * 32;
-        f32x16 s = zero16(), dp = zero16();
-  #pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), kf[ks], s);   // S  = Q K^T : rows q, cols key
-          dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), vf[ks], dp);  // dP = dO V^T
-        }
-        if (qt == ktile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
-  #pragma unroll
-          for (int reg = 0; reg < 16; ++reg)
-            if (key > qb + acc_row(reg, hf)) s[reg] = -INFINITY;
-        }
-        if (qb + 32 > a.T) {  // tail query tile: rows past T contribute nothing (p = 0, dS = 0)
-  #pragma unroll
-          for (int reg = 0; reg < 16; ++reg)
-            if (qb + acc_row(reg, hf) >= a.T) s[reg] = -INFINITY;
-        }
-        // row statistics of the lane's 16 query rows: rows (reg&3) + 8(reg>>2) + 4hf
-        // come in 4 runs of 4 consecutive rows -> 16-byte LDS reads (broadcast),
-        // consumed run by run (not all 48 values staged up front: that held the
-        // kernel at 212 VGPRs, two waves per SIMD)
-        f32x16 pd;
-  #pragma unroll
-        for (int g = 0; g < 4; ++g) {
+      if (qb + 32 > a.T) {  // tail query tile: rows past T contribute nothing (p = 0, dS = 0)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+          if (qb + acc_row(reg, hf) >= a.T) s[reg] = -INFINITY;
+      }
+      // row statistics of the lane's 16 query rows: rows (reg&3) + 8(reg>>2) + 4hf
+      // come in 4 runs of 4 consecutive rows -> 16-byte LDS reads (broadcast),
+      // consumed run by run (not all 48 values staged up front: that held the
+      // kernel at 212 VGPRs, two waves per SIMD).  Runs 2s2, 2s2+1 = operand
+      // fragment s2 (two row pairs each); each fragment's MFMAs are issued as
+      // soon as it is built, so only one fragment pair is live at a time.
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        i32x4 pw, dw;
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg) {
+          const int g = 2 * s2 + gg;
           const float4 lv = *reinterpret_cast<const float4*>(&ls_[buf][0][8 * g + 4 * hf]);
           const float4 dv4 = *reinterpret_cast<const float4*>(&ls_[buf][1][8 * g + 4 * hf]);
           uint4 av = make_uint4(0, 0, 0, 0);
@@ -964,32 +740,38 @@ attn_bwd_dkv_kernel(AttnArgs a) {
           const float lse_g[4] = {lv.x, lv.y, lv.z, lv.w};
           const float dl_g[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
           const uint32_t ar_g[4] = {av.x, av.y, av.z, av.w};
-  #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int reg = 4 * g + i;
-            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[reg], a.scale_log2, -lse_g[i]));
-            float dpv = dp[reg];
-            float pdv = p;
-            if constexpr (DROP) {  // the lane is the key here: one (cheap) hash per element;
-                                   // p and the delta row values already carry 1/(1-p)
-              const bool kp_ = (mix1(ar_g[i] ^ kmix) << kshift) >= thr_hi;
-              dpv = kp_ ? dpv : 0.f;
-              pdv = kp_ ? p : 0.f;
+#pragma unroll
+          for (int pi = 0; pi < 2; ++pi) {
+            const int e0 = 2 * pi, r0 = 4 * g + e0;
+            // p and the delta row values already carry 1/(1-p)
+            const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r0], a.scale_log2, -lse_g[e0]));
+            const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r0 + 1], a.scale_log2, -lse_g[e0 + 1]));
+            uint32_t pv, dsv;
+            if constexpr (DROP) {
+              const uint32_t mk = keep_mask2(
+                  __builtin_amdgcn_perm(mix1(ar_g[e0 + 1] + kmix), mix1(ar_g[e0] + kmix), sel), tm1);
+              pv = pk2(p0, p1) & mk;  // Pd
+              const float a0 = p0 * dl_g[e0], a1 = p1 * dl_g[e0 + 1];
+              dsv = bfi(mk, pk2(__builtin_fmaf(p0, dp[r0], -a0), __builtin_fmaf(p1, dp[r0 + 1], -a1)),
+                        pk2(-a0, -a1));
+            } else {
+              pv = pk2(p0, p1);
+              dsv = pk2(p0 * (dp[r0] - dl_g[e0]), p1 * (dp[r0 + 1] - dl_g[e0 + 1]));
             }
-            pd[reg] = pdv;
-            s[reg] = p * (dpv - dl_g[i]);  // dS
+            pw[2 * gg + pi] = static_cast<int>(pv);
+            dw[2 * gg + pi] = static_cast<int>(dsv);
           }
         }
-  #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 pf = acc_frag(pd, s2);
-          const bf16x8 dsf = acc_frag(s, s2);
-  #pragma unroll
-          for (int t = 0; t < D / 32; ++t) {
-            dv[t] = mfma32(pf, tr_frag<D>(ds_[buf], s2, t, lane), dv[t]);   // dV += Pd^T dO
-            dk[t] = mfma32(dsf, tr_frag<D>(qs_[buf], s2, t, lane), dk[t]);  // dK += dS^T Q
-          }
+        const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);
+        const bf16x8 dsf = __builtin_bit_cast(bf16x8, dw);
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) {
+          dv[t] = mfma32(pf, tr_frag<D>(ds_[buf], s2, t, lane), dv[t]);   // dV += Pd^T dO
+          dk[t] = mfma32(dsf, tr_frag<D>(qs_[buf], s2, t, lane), dk[t]);  // dK += dS^T Q
         }
+        // keep the second fragment's LDS reads from being hoisted above this
+        // point (their registers pushed the kernel past 168 VGPRs: spills)
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
@@ -1035,17 +817,13 @@ hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
   const dim3 grid(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T))), block(256);
   // NT = 2 key tiles per barrier at D=64 (GPT-2 shape fwd 0.067 -> 0.065 ms);
   // at D=128 the extra 64 VGPRs cost a wave of occupancy and it was neutral
-#define FWD(DD, NT, PIPE)                                                                        \
-  if (drop) hipLaunchKernelGGL((attn_fwd_kernel<DD, true, NT, PIPE>), grid, block, 0, st, a); \
-  else hipLaunchKernelGGL((attn_fwd_kernel<DD, false, NT, PIPE>), grid, block, 0, st, a);
+#define FWD(DD, NT)                                                                        \
+  if (drop) hipLaunchKernelGGL((attn_fwd_kernel<DD, true, NT>), grid, block, 0, st, a); \
+  else hipLaunchKernelGGL((attn_fwd_kernel<DD, false, NT>), grid, block, 0, st, a);
   if (D == 64) {
-#if DLION_FWD_PIPE
-    FWD(64, 1, true)
-#else
-    FWD(64, DLION_FWD_NT64, false)
-#endif
+    FWD(64, DLION_FWD_NT64)
   } else if (D == 128) {
-    FWD(128, 1, false)
+    FWD(128, 1)
   } else {
     return hipErrorInvalidValue;
   }
@@ -1057,18 +835,18 @@ hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
   const dim3 bq(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T)));
   const dim3 bkv(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.Hkv, a.T)));
   // dQ first: it also computes delta = rowsum(dO * O), which dKV reads
-#define BWD(DD, NT, PIPE, KPIPE)                                                                                  \
-  if (drop) {                                                                                             \
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, true, NT, PIPE>), bq, dim3(256), 0, st, a);                     \
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true, KPIPE>), bkv, dim3(256), 0, st, a);                       \
-  } else {                                                                                                \
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, false, NT, PIPE>), bq, dim3(256), 0, st, a);                    \
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false, KPIPE>), bkv, dim3(256), 0, st, a);                      \
+#define BWD(DD, NT)                                                                      \
+  if (drop) {                                                                            \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, true, NT>), bq, dim3(256), 0, st, a);    \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), bkv, dim3(256), 0, st, a);      \
+  } else {                                                                               \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, false, NT>), bq, dim3(256), 0, st, a);   \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), bkv, dim3(256), 0, st, a);     \
   }
   if (D == 64) {
-    BWD(64, DLION_DQ_NT64, DLION_DQ_PIPE != 0, DLION_DKV_PIPE != 0)
+    BWD(64, DLION_DQ_NT64)
   } else if (D == 128) {
-    BWD(128, 1, false, false)
+    BWD(128, 1)
   } else {
     return hipErrorInvalidValue;
   }

@@ -989,17 +989,21 @@ def _lowbias32(x: torch.Tensor) -> torch.Tensor:
 
 
 def attention_dropout_keep(B: int, H: int, T: int, p: float, seed: int, device=None) -> torch.Tensor:
-    """bool keep-mask [B, H, T(q), T(key)] exactly as the HIP kernels draw it."""
+    """bool keep-mask [B, H, T(q), T(key)] exactly as the HIP kernels draw it
+    (csrc/attention.hip, drop hash v2): one 32-bit hash per (row, key pair),
+    the low half for the even key; a key is kept iff its half, read as a
+    signed 16-bit value, is >= thresh16 - 32768."""
     th = min(65535, int(round(p * 65536)))
     bh = torch.arange(B * H, device=device, dtype=torch.int64).view(B * H, 1, 1)
     q = torch.arange(T, device=device, dtype=torch.int64).view(1, T, 1)
     key = torch.arange(T, device=device, dtype=torch.int64).view(1, 1, T)
     # per-(head, query) row key: full hash; per key pair: one multiply round
     arow = _lowbias32(((bh * 0x9E3779B9) & _M32) ^ ((q * 0x85EBCA6B) & _M32) ^ (seed & _M32))
-    x = ((arow ^ (((key >> 1) * 0xC2B2AE35) & _M32)) & 0xFFFFFF) * 0x9E3779  # v_mul_u32_u24
+    x = ((arow + (((key >> 1) * 0xC2B2AE35) & _M32)) & 0xFFFFFF) * 0x9E3779  # v_mul_u32_u24
     x = (x & _M32) ^ ((x & _M32) >> 16)
     u16 = (x >> ((key & 1) * 16)) & 0xFFFF
-    return (u16 >= th).view(B, H, T, T)
+    s16 = u16 - ((u16 >> 15) << 16)
+    return (s16 >= th - 32768).view(B, H, T, T)
 
 
 def reference_attention(q, k, v, dropout_p: float = 0.0, seed: int = 0) -> torch.Tensor:

@@ -19,7 +19,11 @@ Keyword-only extensions (all optional):
   vote         "majority" (reference) | "average" (paper's server averaging)
   tie_break    "negative" (reference parity) | "zero" | "positive"
   exchange     vote exchange strategy, see parallel/exchange.py
-  bucket_mb    packed-bit bucket size (MB) -- one collective per bucket
+  bucket_mb    packed-bit bucket size (MB) -- one collective per bucket.  None
+               (default): at W > 1 the sign planes are cut into >= 4 buckets
+               (each >= 1 MB, <= 32 MB) so bucket i's exchange overlaps bucket
+               i+1's encode (and its shard vote / apply the neighbours'
+               collectives); at W = 1 one 32 MB bucket size
   group        torch.distributed process group (default: WORLD)
   backend      "auto" | "hip" | "torch"
   seed         base seed of the stochastic-binarization RNG
@@ -67,7 +71,7 @@ class Lion(Optimizer):
         vote: str = "majority",
         tie_break: str = "negative",
         exchange: str = "a2a",
-        bucket_mb: float = 32.0,
+        bucket_mb: Optional[float] = None,
         group=None,
         backend: str = "auto",
         seed: int = 0,
@@ -92,7 +96,7 @@ class Lion(Optimizer):
         self.vote = vote
         self.tie_break = tie_break
         self.exchange_name = canonical_strategy(exchange)
-        self.bucket_bytes = int(bucket_mb * (1 << 20))
+        self.bucket_bytes = None if bucket_mb is None else int(bucket_mb * (1 << 20))
         self.process_group = group
         self.backend = backend
         self.seed = int(seed)
@@ -192,7 +196,7 @@ class Lion(Optimizer):
         key = (FlatPlan.make_key(entries), world, self.exchange_name)
         if self._plan is not None and getattr(self._plan, "_full_key", None) == key:
             return self._plan
-        plan = FlatPlan(entries, world=world, bucket_bytes=self.bucket_bytes)
+        plan = FlatPlan(entries, world=world, bucket_bytes=self._bucket_bytes(entries, world))
         plan._full_key = key
         self._plan = plan
         self._executor = make_executor(plan, self.backend)
@@ -205,6 +209,25 @@ class Lion(Optimizer):
         else:
             self._exchange = None
         return plan
+
+    # automatic bucket size (bucket_mb=None): 32 MB planes at most (Llama-3-8B:
+    # 1 GB of sign bits -> 32 buckets), at least MIN_BUCKETS per step at W > 1
+    # (GPT-2: 15.6 MB -> one 32 MB bucket would serialise encode -> a2a ->
+    # shard vote -> all-gather -> apply), and no collective payload under 1 MB
+    MAX_BUCKET_BYTES = 32 << 20
+    MIN_BUCKET_BYTES = 1 << 20
+    MIN_BUCKETS = 4
+
+    def _bucket_bytes(self, entries, world: int) -> int:
+        if self.bucket_bytes is not None:
+            return self.bucket_bytes
+        if world <= 1 and not self._force_vote:
+            return self.MAX_BUCKET_BYTES
+        from .plan import ALIGN_ELEMS
+
+        total = sum((p.numel() + ALIGN_ELEMS - 1) // ALIGN_ELEMS * ALIGN_ELEMS // 8 for p, _ in entries)
+        per = -(-total // self.MIN_BUCKETS)
+        return int(min(self.MAX_BUCKET_BYTES, max(self.MIN_BUCKET_BYTES, per)))
 
     def _check_consistency(self, plan: FlatPlan) -> None:
         """All ranks must vote on the same tensors in the same order, or the

@@ -154,3 +154,26 @@ def test_dropping_every_worker_is_refused():
             proc.kill()
     assert status == "ok", out
     assert "dropped" in out
+
+
+def test_auto_buckets_pipeline_gpt2_at_w_gt_1():
+    """bucket_mb=None: GPT-2 small's 15.6 MB of sign planes become >= 4
+    buckets of >= 1 MB at W > 1 (encode i+1 overlaps exchange i); one bucket
+    at W = 1; Llama-3-8B-sized planes are capped at 32 MB per bucket."""
+    from distributed_lion_pytorch_amd import Lion
+    from distributed_lion_pytorch_amd.models.registry import build_model, load_config
+    from distributed_lion_pytorch_amd.optim.plan import FlatPlan
+
+    with torch.device("meta"):
+        model = build_model(load_config("gpt2"), native=True)
+    ps = list(model.parameters())
+    opt = Lion(ps)
+    entries = [(p, 0) for p in ps]
+    for w, lo, hi in ((1, 1, 1), (2, 4, 8), (8, 4, 8)):
+        plan = FlatPlan(entries, world=w, bucket_bytes=opt._bucket_bytes(entries, w), device=torch.device("cpu"))
+        assert lo <= len(plan.buckets) <= hi, (w, [b.nbytes for b in plan.buckets])
+        if w > 1:
+            assert min(b.nbytes for b in plan.buckets) >= 1 << 20
+    big = [(torch.empty(128256 * 4096 // 8, device="meta"), 0)] * 64  # 4.2B params: 525 MB of bits
+    assert opt._bucket_bytes(big, 8) == 32 << 20
+    assert Lion(ps, bucket_mb=2.0)._bucket_bytes(entries, 8) == 2 << 20
