@@ -237,15 +237,167 @@ class ConstantLengthDataset(Dataset):
         return {"input_ids": self.data[i], "labels": self.data[i].clone()}
 
 
-def chars_token_ratio(dataset: Sequence[Dict], tokenizer, formatting_func=prepare_sample_text,
+def chars_token_ratio(dataset: Iterable[Dict], tokenizer, formatting_func=prepare_sample_text,
                       nb_examples: int = 400) -> float:
-    """Average characters per token (sft_llama2.py:62-75)."""
+    """Average characters per token over the first ``nb_examples`` rows
+    (sft_llama2.py:62-75); reads only those rows of a stream."""
+    import itertools
+
     chars = toks = 0
-    for ex in list(dataset)[:nb_examples]:
+    for ex in itertools.islice(iter(dataset), nb_examples):
         text = formatting_func(ex)
         chars += len(text)
         toks += len(tokenizer(text)["input_ids"])
     return chars / max(1, toks)
+
+
+# ------------------------------------------------------- streaming SFT data
+# The reference streams its SFT corpus from the hub (sft_llama2.py:99-138):
+# ``take(size_valid_set)`` is the validation set, ``skip(size_valid_set)``
+# shuffled through a ``shuffle_buffer``-row buffer is the training set, and
+# trl's ConstantLengthDataset packs it with ``infinite=True`` from a character
+# buffer sized seq_length * chars_per_token * num_of_sequences.  Offline the
+# rows come from a local json-lines file read lazily (constant memory -- a
+# corpus larger than host RAM streams), each rank keeps its own 1/W of the
+# rows (no rank-0 read + broadcast per batch), and the shuffle is seeded by the
+# training seed (the reference's seed=None is not reproducible).
+class Rows:
+    """Re-iterable row source: a list, or a json-lines / json file read lazily
+    (a ``.json`` array is loaded whole -- it cannot be streamed)."""
+
+    def __init__(self, source):
+        self.source = source
+
+    def __iter__(self):
+        if isinstance(self.source, str):
+            if not self.source.endswith(".jsonl"):
+                with open(self.source) as f:
+                    yield from json.load(f)
+                return
+            with open(self.source) as f:
+                for line in f:
+                    if line.strip():
+                        yield json.loads(line)
+        else:
+            yield from self.source
+
+
+class RowSlice:
+    """``datasets`` take / skip on a re-iterable: rows [start, stop)."""
+
+    def __init__(self, rows, start: int = 0, stop: Optional[int] = None):
+        self.rows, self.start, self.stop = rows, start, stop
+
+    def __iter__(self):
+        import itertools
+
+        return itertools.islice(iter(self.rows), self.start, self.stop)
+
+
+class ShuffledRows:
+    """Buffer shuffle (``IterableDataset.shuffle(buffer_size, seed)``): a
+    ``buffer_size``-row reservoir, each row emitted from a random slot.  Pass
+    ``epoch`` k reshuffles with seed + k (``set_epoch``)."""
+
+    def __init__(self, rows, buffer_size: int, seed: int = 0):
+        self.rows, self.buffer_size, self.seed, self.epoch = rows, max(1, int(buffer_size)), int(seed), 0
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = int(epoch)
+
+    def __iter__(self):
+        rng = random.Random(self.seed * 1_000_003 + self.epoch)
+        buf: List = []
+        for row in self.rows:
+            if len(buf) < self.buffer_size:
+                buf.append(row)
+                continue
+            i = rng.randrange(self.buffer_size)
+            buf[i], row = row, buf[i]
+            yield row
+        rng.shuffle(buf)
+        yield from buf
+
+
+def random_split(rows: Sequence, test_size: float, seed: int = 0):
+    """``Dataset.train_test_split(test_size)`` (sft_llama2.py:114): a seeded
+    random permutation, the first ceil(test_size * n) rows for validation."""
+    import math
+
+    rows = list(rows)
+    order = list(range(len(rows)))
+    random.Random(seed).shuffle(order)
+    n_test = max(1, math.ceil(test_size * len(rows))) if rows else 0
+    return [rows[i] for i in order[n_test:]], [rows[i] for i in order[:n_test]]
+
+
+def _dist_shard():
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+class PackedStream(torch.utils.data.IterableDataset):
+    """trl ``ConstantLengthDataset(infinite=...)`` semantics on a row stream:
+    rows are formatted into a character buffer of seq_length *
+    chars_per_token * num_of_sequences, tokenized, joined with EOS and cut
+    into ``seq_length`` chunks (a partial tail chunk is dropped); with
+    ``infinite`` the rows restart (next shuffle epoch) when exhausted.  Each
+    rank reads every row but keeps rows i % W == rank (``shard``), so ranks
+    train on disjoint data with no broadcast.  ``peak_buffer_chars`` records
+    the largest character buffer held (memory is bounded by it, not by the
+    corpus)."""
+
+    def __init__(self, tokenizer, rows, formatting_func=prepare_sample_text, seq_length: int = 1024,
+                 infinite: bool = False, chars_per_token: float = 3.6, num_of_sequences: int = 1024,
+                 eos_token_id: Optional[int] = None, shard: bool = True):
+        self.tok, self.rows, self.fmt = tokenizer, rows, formatting_func
+        self.seq_length, self.infinite = seq_length, infinite
+        self.max_buffer_size = int(seq_length * chars_per_token * num_of_sequences)
+        self.eos = tokenizer.eos_token_id if eos_token_id is None else eos_token_id
+        self.shard = shard
+        self.peak_buffer_chars = 0
+
+    def _rows(self, epoch: int, rank: int, world: int):
+        if hasattr(self.rows, "set_epoch"):
+            self.rows.set_epoch(epoch)
+        for i, row in enumerate(self.rows):
+            if i % world == rank:
+                yield row
+
+    def __iter__(self):
+        rank, world = _dist_shard() if self.shard else (0, 1)
+        epoch, seen = 0, 0  # rows taken in the current epoch
+        it = self._rows(epoch, rank, world)
+        more = True
+        while more:
+            buf: List[str] = []
+            n = 0
+            while n < self.max_buffer_size:
+                try:
+                    text = self.fmt(next(it))
+                    seen += 1
+                except StopIteration:
+                    if not self.infinite or seen == 0:  # finite, or a source with no rows for this rank
+                        more = False
+                        break
+                    epoch, seen = epoch + 1, 0
+                    it = self._rows(epoch, rank, world)
+                    continue
+                buf.append(text)
+                n += len(text)
+            self.peak_buffer_chars = max(self.peak_buffer_chars, n)
+            if not buf:
+                break
+            ids: List[int] = []
+            for t in self.tok(buf, add_special_tokens=False)["input_ids"]:
+                ids.extend(t)
+                ids.append(self.eos)
+            for i in range(0, len(ids) - self.seq_length + 1, self.seq_length):
+                x = torch.tensor(ids[i:i + self.seq_length], dtype=torch.long)
+                yield {"input_ids": x, "labels": x.clone()}
 
 
 # ---------------------------------------------------------------- DPO data

@@ -12,7 +12,9 @@
   trains all weights;
 * the optimizer is built over the trainable (adapter) parameters AFTER
   injection (the reference builds it over the frozen base: no-op, D12);
-* packed "Question: ...\\n\\nAnswer: ..." samples (ConstantLengthDataset);
+* packed "Question: ...\\n\\nAnswer: ..." samples, the reference's data
+  semantics (take / skip + seeded shuffle buffer, or a seeded random split;
+  an infinite packed training stream read lazily and sharded per rank);
   offline: the stack-exchange-paired data is replaced by a synthetic corpus of
   the same format unless ``--dataset_name`` points at a local json/jsonl file;
 * saves the adapter (final_checkpoint/) and the merged model
@@ -38,8 +40,9 @@ from distributed_lion_pytorch_amd.models.lora import (LoraConfig, load_adapter, 
 from distributed_lion_pytorch_amd.models.registry import build_model, load_config  # noqa: E402
 from distributed_lion_pytorch_amd.trainer.async_trainer import build_lion, warn_unsynced  # noqa: E402
 from distributed_lion_pytorch_amd.trainer.sft import AsyncSFTTrainer, SFTTrainer  # noqa: E402
-from distributed_lion_pytorch_amd.utils.data import (ConstantLengthDataset, chars_token_ratio,  # noqa: E402
-                                                     load_tokenizer, prepare_sample_text, synthetic_qa)
+from distributed_lion_pytorch_amd.utils.data import (ConstantLengthDataset, PackedStream, RowSlice,  # noqa: E402
+                                                     Rows, ShuffledRows, chars_token_ratio, load_tokenizer,
+                                                     prepare_sample_text, random_split, synthetic_qa)
 from distributed_lion_pytorch_amd.utils.metrics import JsonlMetricsCallback  # noqa: E402
 
 logger = logging.getLogger(__name__)
@@ -83,27 +86,41 @@ def build_base(script_args, seed):
     return build_model(config, model_name_or_path=script_args.model_name, torch_dtype=script_args.torch_dtype)
 
 
-def load_samples(script_args, seed):
+def load_samples(script_args, seed) -> Rows:
+    """Row source: a local json-lines file (read lazily) or json array, else
+    the synthetic corpus of the reference's format (offline)."""
     path = script_args.dataset_name
     if path and os.path.isfile(path):
-        with open(path) as f:
-            rows = [json.loads(line) for line in f] if path.endswith(".jsonl") else json.load(f)
-        return rows
-    return synthetic_qa(script_args.synthetic_samples, seed=seed)
+        return Rows(path)
+    return Rows(synthetic_qa(script_args.synthetic_samples, seed=seed))
+
+
+def _count_rows(rows: Rows) -> int:
+    return len(rows.source) if isinstance(rows.source, list) else sum(1 for _ in rows)
 
 
 def create_datasets(tokenizer, script_args, seed):
-    if script_args.streaming:
-        # the reference streams the hub dataset (sft_llama2.py:100-112); offline the rows come from a
-        # local json/jsonl file or the synthetic generator and are packed up front in host memory
-        logger.warning("--streaming has no effect offline: the samples are read from a local file (or generated) "
-                       "and packed in host memory; pass --streaming false to silence this")
+    """The reference's splits (sft_llama2.py:99-138):
+    * ``--streaming`` (default): the first ``size_valid_set`` rows are the
+      validation set (``take``), the rest (``skip``) go through a
+      ``shuffle_buffer``-row shuffle buffer, seeded by the training seed;
+    * otherwise a seeded random ``train_test_split(test_size=0.005)``.
+    Training data is an infinite packed stream (ConstantLengthDataset
+    ``infinite=True``, buffer sized by the measured chars/token) read lazily
+    and sharded per rank; the (bounded) validation set is packed up front."""
     rows = load_samples(script_args, seed)
-    n_valid = min(script_args.size_valid_set, max(1, len(rows) // 20))
-    train_rows, valid_rows = rows[n_valid:], rows[:n_valid]
+    if script_args.streaming:
+        # a corpus smaller than size_valid_set would leave nothing to train on: keep 95 % for training
+        n_valid = min(script_args.size_valid_set, max(1, _count_rows(rows) // 20))
+        valid_rows = list(RowSlice(rows, 0, n_valid))
+        train_rows = ShuffledRows(RowSlice(rows, n_valid), script_args.shuffle_buffer, seed)
+    else:
+        train_rows, valid_rows = random_split(rows, 0.005, seed)
+        logger.info(f"Size of the train set: {len(train_rows)}. Size of the validation set: {len(valid_rows)}")
     ratio = chars_token_ratio(train_rows, tokenizer)
     logger.info(f"The character to token ratio of the dataset is: {ratio:.2f}")
-    train = ConstantLengthDataset(tokenizer, train_rows, prepare_sample_text, seq_length=script_args.seq_length)
+    train = PackedStream(tokenizer, train_rows, prepare_sample_text, seq_length=script_args.seq_length,
+                         infinite=True, chars_per_token=ratio)
     valid = ConstantLengthDataset(tokenizer, valid_rows, prepare_sample_text, seq_length=script_args.seq_length)
     return train, valid
 
