@@ -69,8 +69,11 @@ def _flags():
 
 # per-source extras: the attention kernels keep MFMA accumulators in arch VGPRs
 # (no v_accvgpr_read/write round trips around the softmax VALU work; measured
-# 48 accvgpr reads + 32 writes + 64 moves per forward tile without it)
-EXTRA_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+# 48 accvgpr reads + 32 writes + 64 moves per forward tile without it), and are
+# built without SLP vectorisation: hipcc packed adjacent fp32 multiplies / FMAs
+# of the dS and exponent math into v_pk_mul_f32 / v_pk_fma_f32, which issue
+# slower than two plain ops beside MFMAs (dQ 88 -> 86 us at the GPT-2 shape)
+EXTRA_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"]}
 
 
 def _sources():
@@ -106,17 +109,19 @@ def _compile(src: Path, flags, verbose: bool, force: bool, bdir: Path = BUILD_DI
     return obj
 
 
-def build(verbose: bool = False, force: bool = False, defines=(), out: Path | None = None) -> Path:
+def build(verbose: bool = False, force: bool = False, defines=(), out: Path | None = None, flags_extra=()) -> Path:
     """Compile every HIP/C++ source in csrc/ for gfx950 and link _dlion_C.so.
 
-    ``defines`` (``NAME=VALUE`` strings) and ``out`` build a variant of the
-    extension (tuning macros, e.g. ``DLION_DKV_WAVES128=1``) into its own
-    object directory and shared object, loadable with ``DLION_LIB=<out>``."""
+    ``defines`` (``NAME=VALUE`` strings), ``flags_extra`` (compiler flags)
+    and ``out`` build a variant of the extension (tuning macros, e.g.
+    ``DLION_DKV_WAVES128=1``) into its own object directory and shared
+    object, loadable with ``DLION_LIB=<out>``."""
     out = Path(out) if out else LIB_PATH
     bdir = BUILD_DIR
-    flags = _flags() + [f"-D{d}" for d in defines]
-    if defines or out != LIB_PATH:
-        bdir = BUILD_DIR.parent / ("dlion_C-" + hashlib.sha256(" ".join(defines).encode()).hexdigest()[:8])
+    flags = _flags() + [f"-D{d}" for d in defines] + list(flags_extra)
+    if defines or flags_extra or out != LIB_PATH:
+        key = " ".join(list(defines) + list(flags_extra))
+        bdir = BUILD_DIR.parent / ("dlion_C-" + hashlib.sha256(key.encode()).hexdigest()[:8])
     bdir.mkdir(parents=True, exist_ok=True)
     srcs = _sources()
     jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", "8"))))
@@ -148,6 +153,7 @@ if __name__ == "__main__":
     ap.add_argument("-v", action="store_true")
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--define", "-D", action="append", default=[], help="NAME=VALUE macro for a variant build")
+    ap.add_argument("--flag", action="append", default=[], help="extra compiler flag for a variant build")
     ap.add_argument("--out", default=None, help="shared object path for a variant build")
     a = ap.parse_args()
-    print(build(verbose=a.v, force=a.force, defines=tuple(a.define), out=a.out))
+    print(build(verbose=a.v, force=a.force, defines=tuple(a.define), out=a.out, flags_extra=tuple(a.flag)))

@@ -62,6 +62,29 @@
 #ifndef DLION_ATTN_STAGES
 #define DLION_ATTN_STAGES 2
 #endif
+// LDS fragment prefetch (bit mask, A/B switch): 1 = the second MFMA phase's
+// operands (V^T for PV, K for dQ, dO / Q for dV / dK) are read into registers
+// before the softmax / dS VALU section instead of right before each MFMA;
+// 2 = the first phase's row fragments (K for QK^T, K / V for S / dP, Q / dO)
+// are all read before its MFMA chain
+#ifndef DLION_ATTN_PF
+#define DLION_ATTN_PF 0
+#endif
+// s_setprio 1 around the first (1) / second (2) MFMA phase of each tile, per
+// kernel.  At the GPT-2 shape (interleaved, 2 rounds) the second phase at
+// priority 1 took fwd 69.3-69.9 -> 67.9-68.2 us and dK/dV 117-119 -> 115 us,
+// but dQ 85-86 -> 92 us (its dS VALU then waits behind the other waves' MFMAs)
+#ifndef DLION_FWD_PRIO
+#define DLION_FWD_PRIO 2
+#endif
+#ifndef DLION_DQ_PRIO
+#define DLION_DQ_PRIO 0
+#endif
+#ifndef DLION_DKV_PRIO
+#define DLION_DKV_PRIO 2
+#endif
+#define DLION_PRIO_ON(mask, bit) if constexpr (((mask) & (bit)) != 0) __builtin_amdgcn_s_setprio(1)
+#define DLION_PRIO_OFF(mask, bit) if constexpr (((mask) & (bit)) != 0) __builtin_amdgcn_s_setprio(0)
 
 namespace dlion {
 
@@ -409,11 +432,37 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     if (kt + NT <= last) stage(kt + NT, buf ^ 1);  // the other buffer was last read before the previous barrier
     if (blk.active && kt <= qtile) {  // wave-uniform
       f32x16 s[NT];
+      if constexpr ((DLION_ATTN_PF & 2) != 0) {
+        bf16x8 kfr[NT][D / 16];
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        s[j] = zero16();
+        for (int j = 0; j < NT; ++j)
 #pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) s[j] = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), qf[ks], s[j]);
+          for (int ks = 0; ks < D / 16; ++ks) kfr[j][ks] = row_frag<D>(ks_[buf][j], r, ks, hf);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          s[j] = zero16();
+#pragma unroll
+          for (int ks = 0; ks < D / 16; ++ks) s[j] = mfma32(kfr[j][ks], qf[ks], s[j]);
+        }
+      } else {
+        DLION_PRIO_ON(DLION_FWD_PRIO, 1);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          s[j] = zero16();
+#pragma unroll
+          for (int ks = 0; ks < D / 16; ++ks) s[j] = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), qf[ks], s[j]);
+        }
+        DLION_PRIO_OFF(DLION_FWD_PRIO, 1);
+      }
+      // V^T operands of this group's PV, in flight during the softmax (PF & 1)
+      bf16x8 vfr[NT][2][D / 32];
+      if constexpr ((DLION_ATTN_PF & 1) != 0) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int t = 0; t < D / 32; ++t) vfr[j][s2][t] = tr_frag<D>(vs_[buf][j], s2, t, lane);
       }
       if (kt + NT - 1 >= qtile) {  // the diagonal (or tiles past it) in this group: causal mask
 #pragma unroll
@@ -455,6 +504,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
       l = l * alpha + xsum32(rs);
       // PV with the dropout mask on the packed bf16 P pairs (1/(1-p) is
       // applied once to O at the end)
+      DLION_PRIO_ON(DLION_FWD_PRIO, 2);
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -462,8 +512,9 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
           const bf16x8 pf = p_frag<DROP>(s[j], s2, prow + static_cast<uint32_t>((kt + j) * 16) * kKeyMul, tm1);
 #pragma unroll
           for (int t = 0; t < D / 32; ++t)
-            oacc[t] = mfma32(tr_frag<D>(vs_[buf][j], s2, t, lane), pf, oacc[t]);
+            oacc[t] = mfma32((DLION_ATTN_PF & 1) ? vfr[j][s2][t] : tr_frag<D>(vs_[buf][j], s2, t, lane), pf, oacc[t]);
         }
+      DLION_PRIO_OFF(DLION_FWD_PRIO, 2);
     }
     vm_wait0();  // this wave's pieces of the next tiles have landed
     __syncthreads();
@@ -563,15 +614,48 @@ attn_bwd_dq_kernel(AttnArgs a) {
       // NT independent S / dP chains: one tile's exp / hash VALU work can sit
       // beside the other's MFMAs
       f32x16 s[NT], dp[NT];
+      if constexpr ((DLION_ATTN_PF & 2) != 0) {
+        bf16x8 kfr[NT][D / 16], vfr2[NT][D / 16];
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        s[j] = zero16();
-        dp[j] = zero16();
+        for (int j = 0; j < NT; ++j)
 #pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          s[j] = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), qf[ks], s[j]);    // S^T  = K Q^T
-          dp[j] = mfma32(row_frag<D>(vs_[buf][j], r, ks, hf), dof[ks], dp[j]);  // dP^T = V dO^T
+          for (int ks = 0; ks < D / 16; ++ks) {
+            kfr[j][ks] = row_frag<D>(ks_[buf][j], r, ks, hf);
+            vfr2[j][ks] = row_frag<D>(vs_[buf][j], r, ks, hf);
+          }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          s[j] = zero16();
+          dp[j] = zero16();
+#pragma unroll
+          for (int ks = 0; ks < D / 16; ++ks) {
+            s[j] = mfma32(kfr[j][ks], qf[ks], s[j]);
+            dp[j] = mfma32(vfr2[j][ks], dof[ks], dp[j]);
+          }
         }
+      } else {
+        DLION_PRIO_ON(DLION_DQ_PRIO, 1);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          s[j] = zero16();
+          dp[j] = zero16();
+#pragma unroll
+          for (int ks = 0; ks < D / 16; ++ks) {
+            s[j] = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), qf[ks], s[j]);    // S^T  = K Q^T
+            dp[j] = mfma32(row_frag<D>(vs_[buf][j], r, ks, hf), dof[ks], dp[j]);  // dP^T = V dO^T
+          }
+        }
+        DLION_PRIO_OFF(DLION_DQ_PRIO, 1);
+      }
+      // K operands of this group's dQ MFMAs, in flight during the dS VALU work (PF & 1)
+      bf16x8 kt_fr[NT][2][D / 32];
+      if constexpr ((DLION_ATTN_PF & 1) != 0) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int t = 0; t < D / 32; ++t) kt_fr[j][s2][t] = tr_frag<D>(ks_[buf][j], s2, t, lane);
       }
       if (kt0 + NT - 1 >= qtile) {  // the diagonal (or tiles past it) in this group: exp2(-inf) = 0
 #pragma unroll
@@ -585,6 +669,7 @@ attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg)
           s[j][reg] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][reg], a.scale_log2, -lse2));  // p, carries 1/(1-p)
+      DLION_PRIO_ON(DLION_DQ_PRIO, 2);
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -592,8 +677,11 @@ attn_bwd_dq_kernel(AttnArgs a) {
           const bf16x8 dsf = ds_frag<DROP>(s[j], dp[j], dlt, s2,
                                            prow + static_cast<uint32_t>((kt0 + j) * 16) * kKeyMul, tm1);  // dS^T
 #pragma unroll
-          for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tr_frag<D>(ks_[buf][j], s2, t, lane), dq[t]);  // dQ += dS K
+          for (int t = 0; t < D / 32; ++t)
+            dq[t] = mfma32(dsf, (DLION_ATTN_PF & 1) ? kt_fr[j][s2][t] : tr_frag<D>(ks_[buf][j], s2, t, lane),
+                           dq[t]);  // dQ += dS K
         }
+      DLION_PRIO_OFF(DLION_DQ_PRIO, 2);
     }
   }
   if (!blk.active) return;
@@ -680,10 +768,12 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   // step i -> buffer i&1: Q and dO tiles by LDS-DMA; wave 0 also DMAs the 32
   // lse (lanes 0..31) and delta (lanes 32..63) values into ls_[buf][0..1];
   // with dropout, wave 1 writes the 32 per-row hash keys into ls_[buf][2]
-  auto stage = [&](int i, int buf) {
-    const int gh = i / nq, qt = first + i % nq;
-    const int h = hk * group + gh, bh = b * a.H + h;
-    const int qrow = qt * 32;
+  // (head in the group, query tile) of the next step to stage: advanced by
+  // counters, not i / nq and i % nq (a runtime division is ~40 SALU per step)
+  int sg = 0, sq = first;
+  auto stage_next = [&](int buf) {
+    const int h = hk * group + sg, bh = b * a.H + h;
+    const int qrow = sq * 32;
     qd.issue(a.q + b * a.q_sb + h * a.q_sh + static_cast<int64_t>(qrow) * a.q_st, qs_[buf], a.T - qrow);
     dd.issue(a.dout + b * a.o_sb + h * a.o_sh + static_cast<int64_t>(qrow) * a.o_st, ds_[buf], a.T - qrow);
     if (w == 0) {
@@ -691,25 +781,58 @@ attn_bwd_dkv_kernel(AttnArgs a) {
                          min(qrow + (lane & 31), a.T - 1);
       glds4(src, &ls_[buf][0][0]);
     } else if (DROP && w == 1 && lane < 32) {
-      ls_[buf][2][lane] = __uint_as_float(drop_row(a.seed, bh, qt * 32 + lane));
+      ls_[buf][2][lane] = __uint_as_float(drop_row(a.seed, bh, qrow + lane));
+    }
+    if (++sq == ntiles) {
+      sq = first;
+      ++sg;
     }
   };
-  for (int j = 0; j < NB - 1 && j < total; ++j) stage(j, j);
+  for (int j = 0; j < NB - 1 && j < total; ++j) stage_next(j);
   // LDS-DMA pieces per stage: Q + dO tiles, and wave 0's lse / delta row values
   const int per_stage = 2 * DmaTile<D>::PPW + (w == 0 ? 1 : 0);
-  for (int i = 0; i < total; ++i) {
+  int qt = first;  // query tile of step i
+  for (int i = 0; i < total; ++i, qt = (qt + 1 == ntiles ? first : qt + 1)) {
     const int buf = i % NB;
     vm_wait_n(min(total - 1 - i, NB - 2) * per_stage);  // step i landed (later steps may be in flight)
     __syncthreads();  // for every wave; and every wave is done with the buffer restaged next
-    if (i + NB - 1 < total) stage(i + NB - 1, (i + NB - 1) % NB);
-    const int qt = first + i % nq;
+    if (i + NB - 1 < total) stage_next((i + NB - 1) % NB);
     if (active && qt >= ktile) {  // wave-uniform
       const int qb = qt * 32;
       f32x16 s = zero16(), dp = zero16();
+      if constexpr ((DLION_ATTN_PF & 2) != 0) {
+        bf16x8 qa[D / 16], kb_[D / 16], da[D / 16], vb[D / 16];
 #pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) {
-        s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), row_frag<D>(kvs_[0][w], r, ks, hf), s);   // S = Q K^T
-        dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), row_frag<D>(kvs_[1][w], r, ks, hf), dp);  // dP = dO V^T
+        for (int ks = 0; ks < D / 16; ++ks) {
+          qa[ks] = row_frag<D>(qs_[buf], r, ks, hf);
+          kb_[ks] = row_frag<D>(kvs_[0][w], r, ks, hf);
+          da[ks] = row_frag<D>(ds_[buf], r, ks, hf);
+          vb[ks] = row_frag<D>(kvs_[1][w], r, ks, hf);
+        }
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) {
+          s = mfma32(qa[ks], kb_[ks], s);
+          dp = mfma32(da[ks], vb[ks], dp);
+        }
+      } else {
+        DLION_PRIO_ON(DLION_DKV_PRIO, 1);
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) {
+          s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), row_frag<D>(kvs_[0][w], r, ks, hf), s);   // S = Q K^T
+          dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), row_frag<D>(kvs_[1][w], r, ks, hf), dp);  // dP = dO V^T
+        }
+        DLION_PRIO_OFF(DLION_DKV_PRIO, 1);
+      }
+      // dO^T / Q^T operands of dV / dK, in flight during the dS VALU work (PF & 1)
+      bf16x8 dtr[2][D / 32], qtr[2][D / 32];
+      if constexpr ((DLION_ATTN_PF & 1) != 0) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int t = 0; t < D / 32; ++t) {
+            dtr[s2][t] = tr_frag<D>(ds_[buf], s2, t, lane);
+            qtr[s2][t] = tr_frag<D>(qs_[buf], s2, t, lane);
+          }
       }
       if (qt == ktile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
 #pragma unroll
@@ -764,14 +887,16 @@ attn_bwd_dkv_kernel(AttnArgs a) {
         }
         const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);
         const bf16x8 dsf = __builtin_bit_cast(bf16x8, dw);
+        DLION_PRIO_ON(DLION_DKV_PRIO, 2);
 #pragma unroll
         for (int t = 0; t < D / 32; ++t) {
-          dv[t] = mfma32(pf, tr_frag<D>(ds_[buf], s2, t, lane), dv[t]);   // dV += Pd^T dO
-          dk[t] = mfma32(dsf, tr_frag<D>(qs_[buf], s2, t, lane), dk[t]);  // dK += dS^T Q
+          dv[t] = mfma32(pf, (DLION_ATTN_PF & 1) ? dtr[s2][t] : tr_frag<D>(ds_[buf], s2, t, lane), dv[t]);   // dV += Pd^T dO
+          dk[t] = mfma32(dsf, (DLION_ATTN_PF & 1) ? qtr[s2][t] : tr_frag<D>(qs_[buf], s2, t, lane), dk[t]);  // dK += dS^T Q
         }
+        DLION_PRIO_OFF(DLION_DKV_PRIO, 2);
         // keep the second fragment's LDS reads from being hoisted above this
         // point (their registers pushed the kernel past 168 VGPRs: spills)
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr ((DLION_ATTN_PF & 1) == 0) __builtin_amdgcn_sched_barrier(0);
       }
     }
   }

@@ -97,12 +97,15 @@ class DPOTrainer(Trainer):
                          processing_class=tok, data_collator=DPOCollator(tok, max_length, max_prompt_length),
                          **kwargs)
         self._reward_acc = None  # device [chosen, rejected, accuracy, margin, micro-batches] since the last log
+        self.tokens_seen = 0  # training tokens through the policy (chosen + rejected, padded), host-side count
 
     _REWARD_KEYS = ("rewards/chosen", "rewards/rejected", "rewards/accuracies", "rewards/margins")
 
     def compute_loss(self, model, inputs, return_outputs=False, num_items_in_batch=None):
         ids, labels = inputs["input_ids"], inputs["labels"]
         n = ids.shape[0] // 2
+        if model.training:
+            self.tokens_seen += ids.numel()
         if next(self.ref_model.parameters()).device != ids.device:
             self.ref_model.to(ids.device)
         policy = self.accelerator.unwrap_model(model)

@@ -401,10 +401,27 @@ class PackedStream(torch.utils.data.IterableDataset):
 
 
 # ---------------------------------------------------------------- DPO data
-def synthetic_paired(n: int, seed: int = 0) -> List[Dict[str, str]]:
-    """prompt / chosen / rejected triples in the reference's format (dpo_llama2.py:84-125)."""
+def synthetic_paired(n: int, seed: int = 0, target_chars: Optional[int] = None) -> List[Dict[str, str]]:
+    """prompt / chosen / rejected triples in the reference's format (dpo_llama2.py:84-125).
+    ``target_chars``: every prompt + response is padded with words to just
+    under that many characters (throughput runs at the full ``max_length``;
+    the default rows are a few hundred characters)."""
     out = []
+    rng = random.Random(seed + 1)
     for ex in synthetic_qa(n, seed):
-        out.append({"prompt": "Question: " + ex["question"] + "\n\nAnswer: ",
-                    "chosen": ex["response_j"], "rejected": ex["response_k"]})
+        row = {"prompt": "Question: " + ex["question"] + "\n\nAnswer: ",
+               "chosen": ex["response_j"], "rejected": ex["response_k"]}
+        if target_chars:
+            # prompt ~ 40 % of the budget, each response the rest
+            row["prompt"] = _fill(rng, row["prompt"], int(0.4 * target_chars))
+            for k in ("chosen", "rejected"):
+                row[k] = _fill(rng, row[k], target_chars - len(row["prompt"]))
+        out.append(row)
     return out
+
+
+def _fill(rng: random.Random, text: str, n: int) -> str:
+    """``text`` extended with random words to at most ``n`` characters (at least n - 12)."""
+    while len(text) < n - 12:
+        text += " " + rng.choice(_WORDS)
+    return text[:n]

@@ -30,15 +30,22 @@ def is_rank0() -> bool:
 
 
 class JsonlMetricsCallback(TrainerCallback):
-    def __init__(self, output_dir: str, seq_len: Optional[int] = None, filename: str = "metrics.jsonl"):
+    def __init__(self, output_dir: str, seq_len: Optional[int] = None, filename: str = "metrics.jsonl",
+                 token_count=None):
+        """``token_count``: optional callable returning this rank's cumulative
+        training tokens (variable-length batches, e.g. DPO); otherwise tokens
+        = steps x batch x accumulation x world x ``seq_len``."""
         self.path = os.path.join(output_dir, filename)
         self.seq_len = seq_len
+        self.token_count = token_count
         self._t = None
         self._step = 0
+        self._tok = 0
 
     def on_train_begin(self, args, state, control, **kw):
         self._t = time.perf_counter()
         self._step = state.global_step
+        self._tok = self.token_count() if self.token_count else 0
 
     def on_log(self, args, state, control, logs=None, optimizer=None, **kw):
         if not is_rank0():
@@ -49,9 +56,13 @@ class JsonlMetricsCallback(TrainerCallback):
         now = time.perf_counter()
         rec = {"step": state.global_step, "time": time.time()}
         rec.update(logs or {})
-        if self._t is not None and state.global_step > self._step and self.seq_len:
+        world = max(1, args.world_size)
+        if self._t is not None and state.global_step > self._step and self.token_count is not None:
+            tok = self.token_count()
+            rec["tokens_per_s"] = (tok - self._tok) * world / max(now - self._t, 1e-9)
+            self._tok = tok
+        elif self._t is not None and state.global_step > self._step and self.seq_len:
             steps = state.global_step - self._step
-            world = max(1, args.world_size)
             toks = steps * args.per_device_train_batch_size * args.gradient_accumulation_steps * world * self.seq_len
             rec["tokens_per_s"] = toks / max(now - self._t, 1e-9)
         self._t, self._step = now, state.global_step

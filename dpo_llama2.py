@@ -81,10 +81,14 @@ class ScriptArguments:
     lion_wire: Optional[str] = field(default="a2a")
     dataset_name: Optional[str] = field(default=None, metadata={"help": "local json/jsonl of prompt/chosen/rejected"})
     synthetic_samples: Optional[int] = field(default=10000)
+    synthetic_chars: Optional[int] = field(default=None, metadata={
+        "help": "pad every synthetic prompt + response to about this many characters (throughput runs)"})
     model_overrides: Optional[str] = field(default=None)
     torch_dtype: Optional[str] = field(default="bfloat16")
     load_in_4bit: Optional[bool] = field(default=False, metadata={"help": "4-bit frozen bases (dpo_llama2.py:133-152)"})
     bnb_4bit_quant_type: Optional[str] = field(default="nf4")
+    final_save: Optional[bool] = field(default=True, metadata={
+        "help": "save the trained model / adapter at the end (false: throughput runs of 7B models)"})
     bf16: Optional[bool] = field(default=True)
     seed: Optional[int] = field(default=0)
     use_cpu: Optional[bool] = field(default=False)
@@ -95,7 +99,7 @@ def load_pairs(args):
         with open(args.dataset_name) as f:
             rows = [json.loads(line) for line in f] if args.dataset_name.endswith(".jsonl") else json.load(f)
     else:
-        rows = synthetic_paired(args.synthetic_samples, seed=args.seed)
+        rows = synthetic_paired(args.synthetic_samples, seed=args.seed, target_chars=args.synthetic_chars)
     if args.sanity_check:
         rows = rows[:1000]
     # length filter (dpo_llama2.py:157-168)
@@ -181,10 +185,14 @@ def main(argv=None):
     trainer = trainer_class(model, model_ref, args=training_args, beta=script_args.beta, train_dataset=train_rows,
                             eval_dataset=eval_rows, tokenizer=tokenizer, max_prompt_length=script_args.max_prompt_length,
                             max_length=script_args.max_length, peft_config=None, optimizers=(optimizer, sched),
-                            callbacks=[JsonlMetricsCallback(script_args.output_dir, script_args.max_length)])
+                            callbacks=[])
+    # tokens/s counts what the policy actually processed (chosen + rejected, padded), not max_length
+    trainer.add_callback(JsonlMetricsCallback(script_args.output_dir, token_count=lambda: trainer.tokens_seen))
     training_args.lion, training_args.async_grad = script_args.lion, script_args.async_grad
     warn_unsynced(training_args)
     trainer.train()
+    if not script_args.final_save:
+        return trainer
     trainer.save_model(script_args.output_dir)
     if trainer.is_world_process_zero():
         from distributed_lion_pytorch_amd.models.lora import save_adapter

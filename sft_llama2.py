@@ -74,6 +74,8 @@ class ScriptArguments:
     load_in_4bit: Optional[bool] = field(default=False, metadata={
         "help": "frozen base weights in 4-bit (the reference's BitsAndBytesConfig, sft_llama2.py:141-145)"})
     bnb_4bit_quant_type: Optional[str] = field(default="nf4", metadata={"help": "nf4 | fp4"})
+    final_save: Optional[bool] = field(default=True, metadata={
+        "help": "save the trained model / adapter at the end (false: throughput runs of 7B models)"})
 
 
 def build_base(script_args, seed):
@@ -173,6 +175,8 @@ def main(argv=None):
                             callbacks=[JsonlMetricsCallback(training_args.output_dir, script_args.seq_length)])
     warn_unsynced(training_args)
     trainer.train()
+    if not script_args.final_save:
+        return trainer
     trainer.save_model(training_args.output_dir)
 
     if trainer.is_world_process_zero():
