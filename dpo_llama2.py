@@ -120,6 +120,7 @@ def main(argv=None):
     model_ref = build_model(config, model_name_or_path=script_args.model_name_or_path,
                             torch_dtype=script_args.torch_dtype)
     model_ref.load_state_dict(model.state_dict())  # identical frozen reference (also for random init)
+    model_ref.requires_grad_(False)
     if script_args.load_in_4bit:
         from distributed_lion_pytorch_amd.models.quant import QuantConfig, quantize_model
 
@@ -127,15 +128,6 @@ def main(argv=None):
                          bnb_4bit_compute_dtype=getattr(torch, script_args.torch_dtype))
         quantize_model(model, qc)
         quantize_model(model_ref, qc)
-    from distributed_lion_pytorch_amd.trainer.memory import should_checkpoint
-
-    tokens = 2 * script_args.per_device_train_batch_size * script_args.max_length  # chosen + rejected
-    if should_checkpoint(script_args.gradient_checkpointing, script_args.checkpointing_policy, config, tokens,
-                         model, model_ref):
-        model.gradient_checkpointing_enable()
-    elif script_args.gradient_checkpointing:
-        logger.info("gradient checkpointing not needed: activations fit in device memory (--checkpointing_policy auto)")
-
     rows = load_pairs(script_args)
     n_eval = max(1, min(len(rows) // 20, 1000))
     train_rows, eval_rows = rows[n_eval:], rows[:n_eval]
@@ -147,7 +139,7 @@ def main(argv=None):
         logging_steps=script_args.logging_steps,
         save_steps=script_args.save_steps,
         gradient_accumulation_steps=script_args.gradient_accumulation_steps,
-        gradient_checkpointing=False,  # handled on the native model above
+        gradient_checkpointing=False,  # decided on the native model below
         learning_rate=script_args.learning_rate,
         eval_strategy="steps" if script_args.eval_steps else "no",
         eval_steps=script_args.eval_steps,
@@ -174,6 +166,18 @@ def main(argv=None):
 
         inject_lora(model, peft_config)
     print_trainable_parameters(model)
+    # decided after LoRA injection and with the reference frozen: the estimate counts a
+    # gradient + momentum only for what trains (all-trainable counting overstated it 3x
+    # and checkpointed a batch that fits)
+    from distributed_lion_pytorch_amd.trainer.memory import should_checkpoint
+
+    tokens = 2 * script_args.per_device_train_batch_size * script_args.max_length  # chosen + rejected
+    if should_checkpoint(script_args.gradient_checkpointing, script_args.checkpointing_policy, config, tokens,
+                         model, model_ref):
+        model.gradient_checkpointing_enable()
+    elif script_args.gradient_checkpointing:
+        logger.info("gradient checkpointing not needed: activations fit in device memory (--checkpointing_policy auto)")
+
     params = [p for p in model.parameters() if p.requires_grad]
     if script_args.lion:
         optimizer = build_lion(model, training_args)  # weight_decay = script_args.weight_decay (D10)

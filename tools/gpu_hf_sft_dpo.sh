@@ -7,7 +7,7 @@ OUT=gpurun_out/hf_sft_dpo; mkdir -p $OUT
 rm -rf /tmp/hf_sft /tmp/hf_dpo
 timeout -k 10 600 python -u sft_llama2.py --model_name llama-2-7b --output_dir /tmp/hf_sft --max_steps 12 \
   --logging_steps 1 --save_strategy no --per_device_train_batch_size 4 --per_device_eval_batch_size 1 \
-  --gradient_accumulation_steps 2 --gradient_checkpointing False --group_by_length False --learning_rate 1e-4 \
+  --gradient_accumulation_steps 2 --gradient_checkpointing False --learning_rate 1e-4 \
   --lr_scheduler_type cosine --warmup_steps 2 --weight_decay 0.05 --bf16 True --remove_unused_columns False \
   --report_to none --lion --async_grad --final_save false --synthetic_samples 4000 > $OUT/sft.log 2>&1 || { tail -30 $OUT/sft.log; exit 1; }
 cp /tmp/hf_sft/metrics.jsonl $OUT/sft_metrics.jsonl
