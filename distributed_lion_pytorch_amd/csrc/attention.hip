@@ -301,6 +301,13 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 __device__ __forceinline__ void glds16(const __bf16* src, const void* dst) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr(dst)));
 }
+// scalar-base form: SGPR-pair tile base + per-lane 32-bit byte offset -- the
+// address costs no VALU (the 64-bit form paid a v_mul_lo_u32 + two
+// v_lshl_add_u64 per piece on a tile row that is wave-uniform anyway)
+__device__ __forceinline__ void glds16s(const __bf16* base, uint32_t boff, const void* dst) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(boff), "s"(base),
+               "s"(lds_addr(dst)));
+}
 __device__ __forceinline__ void glds4(const float* src, const void* dst) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(lds_addr(dst)));
 }
@@ -332,6 +339,7 @@ struct DmaTile {
   static constexpr int CPR = D / 8, PPW = D / 64;  // 16-byte chunks per row, 1 KiB pieces per wave
   static_assert(D == 64 || D == 128, "head dim");
   int off0, off1, lds;  // source element offsets (tile-relative) of the lane's chunks; wave's LDS byte offset
+  uint32_t boff0, boff1;  // the same as byte offsets (scalar-base DMA)
   int r0, r1, c0, c1, st;  // the lane's tile rows / swizzled chunk offsets, for partial (tail) tiles
   __device__ __forceinline__ DmaTile(int64_t stride) {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -343,16 +351,19 @@ struct DmaTile {
     st = static_cast<int>(stride);
     off0 = r0 * st + c0;
     off1 = r1 * st + c1;
+    boff0 = 2u * static_cast<uint32_t>(off0);
+    boff1 = 2u * static_cast<uint32_t>(off1);
     lds = 1024 * PPW * w;
   }
   // `valid` = rows of the sequence left from this tile's first row: a tail
   // tile (valid < 32) re-reads row valid-1 for its missing rows -- memory
-  // that exists; those rows are masked or dropped by every consumer
+  // that exists; those rows are masked or dropped by every consumer.
+  // `tile` is wave-uniform (the full-tile form passes it in SGPRs).
   __device__ __forceinline__ void issue(const __bf16* tile, LdsTile<D>& t, int valid = 32) const {
     char* dst = reinterpret_cast<char*>(&t[0]) + lds;
     if (valid >= 32) {  // block-uniform
-      glds16(tile + off0, dst);
-      if constexpr (PPW == 2) glds16(tile + off1, dst + 1024);
+      glds16s(tile, boff0, dst);
+      if constexpr (PPW == 2) glds16s(tile, boff1, dst + 1024);
     } else {
       glds16(tile + min(r0, valid - 1) * st + c0, dst);
       if constexpr (PPW == 2) glds16(tile + min(r1, valid - 1) * st + c1, dst + 1024);
@@ -419,7 +430,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   auto stage = [&](int first, int buf) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      const int row = min(first + j, last) * 32;
+      const int row = __builtin_amdgcn_readfirstlane(min(first + j, last) * 32);
       kd.issue(kg + static_cast<int64_t>(row) * a.k_st, ks_[buf][j], a.T - row);
       vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[buf][j], a.T - row);
     }
@@ -596,7 +607,7 @@ attn_bwd_dq_kernel(AttnArgs a) {
   auto stage = [&](int st, int buf) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      const int row = min(st * NT + j, last) * 32;
+      const int row = __builtin_amdgcn_readfirstlane(min(st * NT + j, last) * 32);
       kd.issue(kg + static_cast<int64_t>(row) * a.k_st, ks_[buf][j], a.T - row);
       vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[buf][j], a.T - row);
     }
@@ -743,7 +754,7 @@ attn_bwd_dkv_kernel(AttnArgs a) {
     const DmaTile<D> kd(a.k_st), vd(a.v_st);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int row = (first + j) * 32;
+      const int row = __builtin_amdgcn_readfirstlane((first + j) * 32);
       if (row < a.T) {  // block-uniform
         kd.issue(a.k + b * a.k_sb + hk * a.k_sh + static_cast<int64_t>(row) * a.k_st, kvs_[0][j], a.T - row);
         vd.issue(a.v + b * a.v_sb + hk * a.v_sh + static_cast<int64_t>(row) * a.v_st, kvs_[1][j], a.T - row);
@@ -773,7 +784,7 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   int sg = 0, sq = first;
   auto stage_next = [&](int buf) {
     const int h = hk * group + sg, bh = b * a.H + h;
-    const int qrow = sq * 32;
+    const int qrow = __builtin_amdgcn_readfirstlane(sq * 32);
     qd.issue(a.q + b * a.q_sb + h * a.q_sh + static_cast<int64_t>(qrow) * a.q_st, qs_[buf], a.T - qrow);
     dd.issue(a.dout + b * a.o_sb + h * a.o_sh + static_cast<int64_t>(qrow) * a.o_st, ds_[buf], a.T - qrow);
     if (w == 0) {

@@ -181,6 +181,24 @@ lion_local_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ c
 }
 
 // ----------------------------------------------------------------- K1 / K3
+// The 4 lanes of a quad own 32 consecutive coordinates (bit_off % 2048 == 0,
+// lane stride 8): their sign bytes are gathered with DPP quad broadcasts (VALU,
+// no LDS) and the quad's first lane stores the dword -- 16 dword stores per
+// wave instead of 64 byte stores.  Every lane of the wave must be active.
+__device__ __forceinline__ uint32_t quad_pack(uint32_t b) {
+  const int v = static_cast<int>(b);
+  const uint32_t b1 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(v, 0x55, 0xf, 0xf, false));
+  const uint32_t b2 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(v, 0xaa, 0xf, 0xf, false));
+  const uint32_t b3 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(v, 0xff, 0xf, 0xf, false));
+  const uint32_t b0 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(v, 0x00, 0xf, 0xf, false));
+  return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+}
+
+__device__ __forceinline__ void store_quad_bits(uint8_t* bits, int64_t bit, uint32_t byte) {
+  const uint32_t w = quad_pack(byte);
+  if ((threadIdx.x & 3) == 0) reinterpret_cast<uint32_t*>(bits)[bit >> 5] = w;
+}
+
 // bits: this rank's packed sign plane for the bucket (bucket-relative bit_off).
 // stochastic: bit = Bernoulli(clamp((u + rr) / (2 rr), 0, 1)) with
 //   rr = (1 + 1/b1) * max_grad_norm  (ref :106-108, clamped: SURVEY D4).
@@ -222,7 +240,7 @@ lion_encode_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ 
         for (int j = 0; j < 8; ++j) mv[j] = __fmaf_rn(gv[j], omb2, E::rnd(mv[j] * b2));
         E::store8(m + e, mv);
       }
-      bits[(r.bit_off + e) >> 3] = static_cast<uint8_t>(byte);
+      store_quad_bits(bits, r.bit_off + e, byte);
     }
     return;
   }
@@ -267,7 +285,7 @@ lion_encode_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ 
         store8g<DT>(m, e, r.n, r.vec, mv);
       }
     }
-    bits[(r.bit_off + e) >> 3] = static_cast<uint8_t>(byte);
+    store_quad_bits(bits, r.bit_off + e, byte);  // all lanes reach here (the break above is block-uniform)
   }
 }
 

@@ -4,7 +4,7 @@ plain (EPI 0), + bias (1), GELU with z aux (2), GELU with gelu' aux (6), the
 backward's multiply-by-gelu' drain with bias-gradient partials (8), against
 hipBLASLt's plain GEMM.  Prints median us and TF/s.
 
-  python tools/bench_gemm_epi.py [M]
+  python tools/bench_gemm_epi.py [M [N [K]]]
 """
 import statistics
 import sys
@@ -27,7 +27,8 @@ def timed(fn, reps=20):
 
 def main():
     M = int(sys.argv[1]) if len(sys.argv) > 1 else 20480
-    N, K = 3072, 768
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 3072
+    K = int(sys.argv[3]) if len(sys.argv) > 3 else 768
     ops = hip.ops()
     dt = torch.bfloat16
     a = torch.rand(M, K, device="cuda", dtype=dt) * 2 - 1
@@ -43,6 +44,14 @@ def main():
         "own EPI6 gelu,gelu'": lambda: ops.gemm_nt_gelu_d(a, b, bias, False),
         "own EPI8 *gelu',colsum": lambda: ops.gemm_nt_dmul(a, b, d),
     }
+    if hasattr(ops, "set_gemm_persist"):  # the persistent kernel of the same epilogues
+        def persist(f):
+            def g():
+                prev = ops.set_gemm_persist(1)
+                f()
+                ops.set_gemm_persist(prev)
+            return g
+        variants.update({"P " + k[4:]: persist(f) for k, f in list(variants.items()) if k.startswith("own")})
     for f in variants.values():
         f()
     torch.cuda.synchronize()
