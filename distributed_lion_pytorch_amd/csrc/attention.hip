@@ -767,11 +767,15 @@ attn_bwd_dkv_kernel(AttnArgs a) {
     dk[t] = zero16();
     dv[t] = zero16();
   }
-  // dropout: the lane is the key, so each element needs its own hash (the key
-  // pair's other key is in the neighbouring lane); v_perm_b32 gathers the
-  // lane's 16-bit halves of two rows' hashes into one packed pair (low half
-  // for an even key, high half for an odd one)
-  const uint32_t tm1 = drop_tm1(a.thresh16), sel = (key & 1) ? 0x07060302u : 0x05040100u;
+  // dropout: the lane is the key.  The hash of (row q, key pair) covers both
+  // keys of the pair, which sit in neighbouring lanes: for a row pair (q0, q1)
+  // the even lane hashes q0 and the odd lane q1, the two swap their words with
+  // one DPP quad_perm, and v_perm_b32 gathers the lane's 16-bit halves (low
+  // half for an even key, high half for an odd one) -- one hash per lane and
+  // row pair instead of two.  perm(other, own, sel): even lane [own.lo, other.lo],
+  // odd lane [other.hi, own.hi]; the row keys sit in LDS parity-interleaved.
+  const uint32_t tm1 = drop_tm1(a.thresh16), sel = (key & 1) ? 0x03020706u : 0x05040100u;
+  const int par2 = 2 * (key & 1);
   const uint32_t kmix = (static_cast<uint32_t>(key) >> 1) * kKeyMul;
   const DmaTile<D> qd(a.q_st), dd(a.o_st);
   const int nq = ntiles - first;   // query tiles per head
@@ -792,7 +796,9 @@ attn_bwd_dkv_kernel(AttnArgs a) {
                          min(qrow + (lane & 31), a.T - 1);
       glds4(src, &ls_[buf][0][0]);
     } else if (DROP && w == 1 && lane < 32) {
-      ls_[buf][2][lane] = __uint_as_float(drop_row(a.seed, bh, qrow + lane));
+      // rows 4i..4i+3 stored as [4i, 4i+2, 4i+1, 4i+3]: an even lane reads the
+      // pair heads, an odd lane the pair tails, as one 8-byte read
+      ls_[buf][2][(lane & ~3) | ((lane & 1) << 1) | ((lane >> 1) & 1)] = __uint_as_float(drop_row(a.seed, bh, qrow + lane));
     }
     if (++sq == ntiles) {
       sq = first;
@@ -869,11 +875,20 @@ attn_bwd_dkv_kernel(AttnArgs a) {
           const int g = 2 * s2 + gg;
           const float4 lv = *reinterpret_cast<const float4*>(&ls_[buf][0][8 * g + 4 * hf]);
           const float4 dv4 = *reinterpret_cast<const float4*>(&ls_[buf][1][8 * g + 4 * hf]);
-          uint4 av = make_uint4(0, 0, 0, 0);
-          if constexpr (DROP) av = *reinterpret_cast<const uint4*>(&ls_[buf][2][8 * g + 4 * hf]);
+          uint2 av = make_uint2(0, 0);
+          if constexpr (DROP) av = *reinterpret_cast<const uint2*>(&ls_[buf][2][8 * g + 4 * hf + par2]);
           const float lse_g[4] = {lv.x, lv.y, lv.z, lv.w};
           const float dl_g[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
-          const uint32_t ar_g[4] = {av.x, av.y, av.z, av.w};
+          // this lane's hash word of row pair pi, and the neighbour's (both
+          // hashes before either swap: no DPP read-after-write stall)
+          uint32_t own[2], other[2];
+          if constexpr (DROP) {
+            own[0] = mix1(av.x + kmix);
+            own[1] = mix1(av.y + kmix);
+#pragma unroll
+            for (int pi = 0; pi < 2; ++pi)  // lanes 0<->1, 2<->3
+              other[pi] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(own[pi]), 0xB1, 0xF, 0xF, false));
+          }
 #pragma unroll
           for (int pi = 0; pi < 2; ++pi) {
             const int e0 = 2 * pi, r0 = 4 * g + e0;
@@ -882,8 +897,7 @@ attn_bwd_dkv_kernel(AttnArgs a) {
             const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r0 + 1], a.scale_log2, -lse_g[e0 + 1]));
             uint32_t pv, dsv;
             if constexpr (DROP) {
-              const uint32_t mk = keep_mask2(
-                  __builtin_amdgcn_perm(mix1(ar_g[e0 + 1] + kmix), mix1(ar_g[e0] + kmix), sel), tm1);
+              const uint32_t mk = keep_mask2(__builtin_amdgcn_perm(other[pi], own[pi], sel), tm1);
               pv = pk2(p0, p1) & mk;  // Pd
               const float a0 = p0 * dl_g[e0], a1 = p1 * dl_g[e0 + 1];
               dsv = bfi(mk, pk2(__builtin_fmaf(p0, dp[r0], -a0), __builtin_fmaf(p1, dp[r0 + 1], -a1)),

@@ -118,6 +118,11 @@ __device__ __forceinline__ uint4 ld16(const uint16_t* p) {
   return make_uint4(x[0], x[1], x[2], x[3]);
 }
 constexpr bool kNtAux = DLION_GEMM_NT_AUX != 0, kNtC = DLION_GEMM_NT_C != 0;
+// diagnostic builds only (tools/bench_gemm_epi.py on variant libraries): 1 = EPI 6/7
+// skip the GELU math (both outputs get z), 2 = EPI 6/7 skip the aux store
+#ifndef DLION_EPI_DIAG
+#define DLION_EPI_DIAG 0
+#endif
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -428,11 +433,15 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             float gv, dgv;
-            gelu_and_grad(z[j] + b8[j], EPI == 7, gv, dgv);
+            if constexpr (DLION_EPI_DIAG == 1) {
+              gv = dgv = z[j];
+            } else {
+              gelu_and_grad(z[j] + b8[j], EPI == 7, gv, dgv);
+            }
             hb[j] = static_cast<__bf16>(gv);
             db[j] = static_cast<__bf16>(dgv);
           }
-          st16<kNtAux>(g.aux + (int64_t)gm * g.ldaux + gn, db);
+          if constexpr (DLION_EPI_DIAG != 2) st16<kNtAux>(g.aux + (int64_t)gm * g.ldaux + gn, db);
         }
         st16<kNtC>(g.C + (int64_t)gm * g.ldc + gn, hb);
       }

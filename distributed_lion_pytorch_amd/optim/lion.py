@@ -196,7 +196,13 @@ class Lion(Optimizer):
         key = (FlatPlan.make_key(entries), world, self.exchange_name)
         if self._plan is not None and getattr(self._plan, "_full_key", None) == key:
             return self._plan
-        plan = FlatPlan(entries, world=world, bucket_bytes=self._bucket_bytes(entries, world))
+        backend = None
+        if world > 1 and dist.is_initialized():
+            try:
+                backend = dist.get_backend(self.process_group)
+            except (RuntimeError, ValueError):  # a simulated group has no c10d backend name
+                backend = None
+        plan = FlatPlan(entries, world=world, bucket_bytes=self._bucket_bytes(entries, world, backend))
         plan._full_key = key
         self._plan = plan
         self._executor = make_executor(plan, self.backend)
@@ -213,15 +219,19 @@ class Lion(Optimizer):
     # automatic bucket size (bucket_mb=None): 32 MB planes at most (Llama-3-8B:
     # 1 GB of sign bits -> 32 buckets), at least MIN_BUCKETS per step at W > 1
     # (GPT-2: 15.6 MB -> one 32 MB bucket would serialise encode -> a2a ->
-    # shard vote -> all-gather -> apply), and no collective payload under 1 MB
+    # shard vote -> all-gather -> apply), and no collective payload under 1 MB.
+    # gloo runs every collective on the host (device -> host copy, TCP, back):
+    # each extra bucket costs tens of ms there, so gloo keeps the largest
+    # buckets (8 gloo ranks on one GPU, GPT-2: exposed exchange 51 ms with one
+    # bucket, 277-413 ms with 4, 1016 ms with 13 -- profiles/r4/bucket_sweep_w8_gloo.txt)
     MAX_BUCKET_BYTES = 32 << 20
     MIN_BUCKET_BYTES = 1 << 20
     MIN_BUCKETS = 4
 
-    def _bucket_bytes(self, entries, world: int) -> int:
+    def _bucket_bytes(self, entries, world: int, backend: Optional[str] = None) -> int:
         if self.bucket_bytes is not None:
             return self.bucket_bytes
-        if world <= 1 and not self._force_vote:
+        if (world <= 1 and not self._force_vote) or backend == "gloo":
             return self.MAX_BUCKET_BYTES
         from .plan import ALIGN_ELEMS
 

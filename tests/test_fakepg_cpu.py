@@ -177,3 +177,6 @@ def test_auto_buckets_pipeline_gpt2_at_w_gt_1():
     big = [(torch.empty(128256 * 4096 // 8, device="meta"), 0)] * 64  # 4.2B params: 525 MB of bits
     assert opt._bucket_bytes(big, 8) == 32 << 20
     assert Lion(ps, bucket_mb=2.0)._bucket_bytes(entries, 8) == 2 << 20
+    # host-side collectives (gloo): the fewest buckets; an explicit size still wins
+    assert opt._bucket_bytes(entries, 8, backend="gloo") == 32 << 20
+    assert Lion(ps, bucket_mb=2.0)._bucket_bytes(entries, 8, backend="gloo") == 2 << 20
