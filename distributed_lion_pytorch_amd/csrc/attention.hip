@@ -62,6 +62,13 @@
 #ifndef DLION_ATTN_STAGES
 #define DLION_ATTN_STAGES 2
 #endif
+// per-kernel overrides (A/B): the dQ kernel's K/V ring, the dK/dV kernel's Q/dO ring
+#ifndef DLION_DQ_STAGES
+#define DLION_DQ_STAGES DLION_ATTN_STAGES
+#endif
+#ifndef DLION_DKV_STAGES
+#define DLION_DKV_STAGES DLION_ATTN_STAGES
+#endif
 // LDS fragment prefetch (bit mask, A/B switch): 1 = the second MFMA phase's
 // operands (V^T for PV, K for dQ, dO / Q for dV / dK) are read into registers
 // before the softmax / dS VALU section instead of right before each MFMA;
@@ -556,7 +563,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 template <int D, bool DROP, int NT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? DLION_DQ_WAVES64 : 1)))
 attn_bwd_dq_kernel(AttnArgs a) {
-  constexpr int NB = DLION_ATTN_STAGES;
+  constexpr int NB = DLION_DQ_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[NB][NT];
   __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[NB][NT];
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
@@ -730,7 +737,7 @@ template <int D, bool DROP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     D == 64 ? DLION_DKV_WAVES64 : DLION_DKV_WAVES128)))
 attn_bwd_dkv_kernel(AttnArgs a) {
-  constexpr int NB = DLION_ATTN_STAGES;
+  constexpr int NB = DLION_DKV_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> qs_[NB];
   __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[NB];
   __shared__ __attribute__((aligned(16))) LdsTile<D> kvs_[2][4];  // [K | V][wave's key tile]
