@@ -40,6 +40,28 @@
 #ifndef DLION_DQ_WAVES64
 #define DLION_DQ_WAVES64 1
 #endif
+// Start stagger (A/B): the first resident round of blocks (blockIdx < 1024, ~4 per CU)
+// sleeps ((blockIdx >> 8) & 3) * DLION_ATTN_STAGGER * 64 cycles at entry, so the waves
+// that share a SIMD (one per block) start a quarter-period apart instead of in lock
+// step (all in their MFMA phase together, then all in their VALU phase); kernel
+// mask: 1 = fwd, 2 = dQ, 4 = dK/dV
+#ifndef DLION_ATTN_STAGGER
+#define DLION_ATTN_STAGGER 0
+#endif
+#ifndef DLION_STAGGER_MASK
+#define DLION_STAGGER_MASK 7
+#endif
+#define DLION_STAGGER(bit)                                                         \
+  if constexpr (DLION_ATTN_STAGGER > 0 && (DLION_STAGGER_MASK & (bit)) != 0) {     \
+    if (blockIdx.x < 1024u) {                                                      \
+      for (unsigned i_ = (blockIdx.x >> 8) & 3u; i_ > 0; --i_) __builtin_amdgcn_s_sleep(DLION_ATTN_STAGGER); \
+    }                                                                              \
+  }
+// dK/dV (A/B): the wave's K-tile row fragments (S = Q K^T's B operand, the
+// same every step) held in 16 VGPRs instead of re-read from LDS each step
+#ifndef DLION_DKV_KREG
+#define DLION_DKV_KREG 0
+#endif
 #ifndef DLION_DQ_NT64
 #define DLION_DQ_NT64 1
 #endif
@@ -404,6 +426,7 @@ struct QBlock {
 // softmax -- measured neutral to -1 % in round 3 and were removed.)
 template <int D, bool DROP, int NT>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
+  DLION_STAGGER(1)
   __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[2][NT];
   __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[2][NT];
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
@@ -563,6 +586,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 template <int D, bool DROP, int NT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? DLION_DQ_WAVES64 : 1)))
 attn_bwd_dq_kernel(AttnArgs a) {
+  DLION_STAGGER(2)
   constexpr int NB = DLION_DQ_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[NB][NT];
   __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[NB][NT];
@@ -737,6 +761,7 @@ template <int D, bool DROP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     D == 64 ? DLION_DKV_WAVES64 : DLION_DKV_WAVES128)))
 attn_bwd_dkv_kernel(AttnArgs a) {
+  DLION_STAGGER(4)
   constexpr int NB = DLION_DKV_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> qs_[NB];
   __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[NB];
@@ -816,11 +841,18 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   // LDS-DMA pieces per stage: Q + dO tiles, and wave 0's lse / delta row values
   const int per_stage = 2 * DmaTile<D>::PPW + (w == 0 ? 1 : 0);
   int qt = first;  // query tile of step i
+  bf16x8 kreg[DLION_DKV_KREG ? D / 16 : 1];
   for (int i = 0; i < total; ++i, qt = (qt + 1 == ntiles ? first : qt + 1)) {
     const int buf = i % NB;
     vm_wait_n(min(total - 1 - i, NB - 2) * per_stage);  // step i landed (later steps may be in flight)
     __syncthreads();  // for every wave; and every wave is done with the buffer restaged next
     if (i + NB - 1 < total) stage_next((i + NB - 1) % NB);
+    if constexpr (DLION_DKV_KREG != 0) {
+      if (i == 0) {  // the K / V tiles landed with step 0's wait
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) kreg[ks] = row_frag<D>(kvs_[0][w], r, ks, hf);
+      }
+    }
     if (active && qt >= ktile) {  // wave-uniform
       const int qb = qt * 32;
       f32x16 s = zero16(), dp = zero16();
@@ -842,7 +874,8 @@ attn_bwd_dkv_kernel(AttnArgs a) {
         DLION_PRIO_ON(DLION_DKV_PRIO, 1);
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) {
-          s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), row_frag<D>(kvs_[0][w], r, ks, hf), s);   // S = Q K^T
+          s = mfma32(row_frag<D>(qs_[buf], r, ks, hf),
+                     DLION_DKV_KREG ? kreg[DLION_DKV_KREG ? ks : 0] : row_frag<D>(kvs_[0][w], r, ks, hf), s);  // S = Q K^T
           dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), row_frag<D>(kvs_[1][w], r, ks, hf), dp);  // dP = dO V^T
         }
         DLION_PRIO_OFF(DLION_DKV_PRIO, 1);
