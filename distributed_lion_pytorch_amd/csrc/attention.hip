@@ -40,6 +40,13 @@
 #ifndef DLION_DQ_WAVES64
 #define DLION_DQ_WAVES64 1
 #endif
+// dQ (A/B): the wave's dO rows (1) and also its Q rows (2) read from LDS per
+// tile instead of held in 16 VGPRs each for the whole kernel, leaving the
+// registers to the fragment loads (the S / dP phase otherwise waits on each
+// LDS read right before its MFMA: the fragments share one register quad)
+#ifndef DLION_DQ_OPS_LDS
+#define DLION_DQ_OPS_LDS 0
+#endif
 // Start stagger (A/B): the first resident round of blocks (blockIdx < 1024, ~4 per CU)
 // sleeps ((blockIdx >> 8) & 3) * DLION_ATTN_STAGGER * 64 cycles at entry, so the waves
 // that share a SIMD (one per block) start a quarter-period apart instead of in lock
@@ -590,7 +597,11 @@ attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int NB = DLION_DQ_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[NB][NT];
   __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[NB][NT];
+  constexpr int kOps = DLION_DQ_OPS_LDS;
+  constexpr int kDoSlot = (kOps & 2) != 0 ? 1 : 0;  // dO's slot: after Q when Q is staged too
+  __shared__ __attribute__((aligned(16))) LdsTile<D> qo_[kDoSlot + 1][kOps != 0 ? 4 : 1];  // [Q | dO][wave]
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
+  const int wq = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nt = ntiles32(a.T);
   const QBlock blk(a.B * a.H, nt);
   const int bh = blk.bh, qtile = blk.qtile, last = blk.last;
@@ -605,7 +616,7 @@ attn_bwd_dq_kernel(AttnArgs a) {
     const __bf16* dop = a.dout + b * a.o_sb + static_cast<int64_t>(qc) * a.o_st + h * a.o_sh + 8 * hf;
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
-      qf[s] = ld8(qp + 16 * s);
+      if constexpr ((kOps & 2) == 0) qf[s] = ld8(qp + 16 * s);
       dof[s] = ld8(dop + 16 * s);
     }
     lse2 = a.lse[static_cast<int64_t>(bh) * a.T + qc];
@@ -643,6 +654,21 @@ attn_bwd_dq_kernel(AttnArgs a) {
       vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[buf][j], a.T - row);
     }
   };
+  if constexpr (kOps != 0) {  // the block's 4 query tiles (one per wave): landed by the loop's first wait
+    const DmaTile<D> qd(a.q_st), od(a.o_st);
+    const int g0 = qtile - wq;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = __builtin_amdgcn_readfirstlane((g0 + j) * 32);
+      if (row < a.T) {  // block-uniform
+        if constexpr ((kOps & 2) != 0)
+          qd.issue(a.q + b * a.q_sb + h * a.q_sh + static_cast<int64_t>(row) * a.q_st, qo_[0][j], a.T - row);
+        od.issue(a.dout + b * a.o_sb + h * a.o_sh + static_cast<int64_t>(row) * a.o_st, qo_[kDoSlot][j], a.T - row);
+      }
+    }
+  }
+#define DLION_DQ_QF(ks) ((kOps & 2) != 0 ? row_frag<D>(qo_[0][kOps != 0 ? wq : 0], r, ks, hf) : qf[ks])
+#define DLION_DQ_DOF(ks) ((kOps & 1) != 0 ? row_frag<D>(qo_[kDoSlot][kOps != 0 ? wq : 0], r, ks, hf) : dof[ks])
   const int ns = last / NT + 1;
   for (int j = 0; j < NB - 1 && j < ns; ++j) stage(j, j);
   for (int st = 0; st < ns; ++st) {
@@ -671,8 +697,8 @@ attn_bwd_dq_kernel(AttnArgs a) {
           dp[j] = zero16();
 #pragma unroll
           for (int ks = 0; ks < D / 16; ++ks) {
-            s[j] = mfma32(kfr[j][ks], qf[ks], s[j]);
-            dp[j] = mfma32(vfr2[j][ks], dof[ks], dp[j]);
+            s[j] = mfma32(kfr[j][ks], DLION_DQ_QF(ks), s[j]);
+            dp[j] = mfma32(vfr2[j][ks], DLION_DQ_DOF(ks), dp[j]);
           }
         }
       } else {
@@ -683,8 +709,8 @@ attn_bwd_dq_kernel(AttnArgs a) {
           dp[j] = zero16();
 #pragma unroll
           for (int ks = 0; ks < D / 16; ++ks) {
-            s[j] = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), qf[ks], s[j]);    // S^T  = K Q^T
-            dp[j] = mfma32(row_frag<D>(vs_[buf][j], r, ks, hf), dof[ks], dp[j]);  // dP^T = V dO^T
+            s[j] = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), DLION_DQ_QF(ks), s[j]);    // S^T  = K Q^T
+            dp[j] = mfma32(row_frag<D>(vs_[buf][j], r, ks, hf), DLION_DQ_DOF(ks), dp[j]);  // dP^T = V dO^T
           }
         }
         DLION_PRIO_OFF(DLION_DQ_PRIO, 1);
@@ -726,6 +752,8 @@ attn_bwd_dq_kernel(AttnArgs a) {
       DLION_PRIO_OFF(DLION_DQ_PRIO, 2);
     }
   }
+#undef DLION_DQ_QF
+#undef DLION_DQ_DOF
   if (!blk.active) return;
   // dq[t]: rows = q (registers), cols = d (lane)
   __bf16* base = a.dq + b * a.dq_sb + h * a.dq_sh;
