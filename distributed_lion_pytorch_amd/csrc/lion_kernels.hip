@@ -38,6 +38,9 @@ namespace dlion {
 #define DLION_K2_PAIR_MAJ 1  // the same for the majority vote over W <= 15 planes (all-gather exchange):
                              // W=8 GPT-2 170 -> 155 us, Llama-3-8B 9.3 -> 8.5 ms (profiles/r3/lion_pair_maj_ab.txt)
 #endif
+#ifndef DLION_K2_CPB
+#define DLION_K2_CPB 2  // chunks per block of the paired apply kernels (2 or 4)
+#endif
 #ifndef DLION_K4_UNROLL
 #define DLION_K4_UNROLL 2  // K4 sliced path: words per thread per grid-stride iteration (1 or 2);
                            // GPT-2 shard 8.1 -> 7.4 us, Llama-3-8B unchanged
@@ -602,19 +605,29 @@ __device__ __forceinline__ void apply_chunk(const SegRow& r, int64_t start, cons
   }
 }
 
-template <int DT, bool MAJ>
+template <int DT, bool MAJ, int CPB>
 __global__ void __launch_bounds__(kThreads)
 lion_apply_pair_kernel(const int64_t* __restrict__ seg, const int64_t* __restrict__ chunks, int64_t n_chunks,
                        const uint8_t* __restrict__ planes, int64_t plane_stride, const uint8_t* __restrict__ alive,
                        int world, int tie, const uint8_t* __restrict__ neg_plane, float decay, float neg_lr) {
   using E = Elem<DT>;
   using S = typename E::S;
-  const int64_t c0 = 2 * static_cast<int64_t>(blockIdx.x);
-  const bool has1 = c0 + 1 < n_chunks;
-  const int64_t s0 = chunks[2 * c0], st0 = chunks[2 * c0 + 1];
-  const int64_t s1 = has1 ? chunks[2 * c0 + 2] : s0, st1 = has1 ? chunks[2 * c0 + 3] : st0;
-  const SegRow r0 = load_seg(seg, s0);
-  const SegRow r1 = load_seg(seg, s1);
+  // CPB chunks per block (DLION_K2_CPB): every chunk's metadata chain is in
+  // flight together, and when all are full every p vector (and pre-voted
+  // plane word) is loaded before the first use
+  const int64_t c0 = CPB * static_cast<int64_t>(blockIdx.x);
+  int64_t sidx[CPB], st[CPB];
+  bool has[CPB];
+#pragma unroll
+  for (int c = 0; c < CPB; ++c) {
+    has[c] = c0 + c < n_chunks;  // chunk 0 always exists
+    const int64_t ci = has[c] ? c0 + c : c0;
+    sidx[c] = chunks[2 * ci];
+    st[c] = chunks[2 * ci + 1];
+  }
+  SegRow rs[CPB];
+#pragma unroll
+  for (int c = 0; c < CPB; ++c) rs[c] = load_seg(seg, sidx[c]);
   VoteCtx v{planes, plane_stride, neg_plane, 0u, world, 0, tie};
   if constexpr (MAJ) {
     for (int k = 0; k < world && k < kMaxSliced; ++k)
@@ -623,34 +636,37 @@ lion_apply_pair_kernel(const int64_t* __restrict__ seg, const int64_t* __restric
         ++v.n_live;
       }
   }
-  const bool full0 = r0.vec && st0 + kChunk <= r0.n, full1 = has1 && r1.vec && st1 + kChunk <= r1.n;
-  if (full0 && full1) {  // block-uniform
-    S* p0 = const_cast<S*>(static_cast<const S*>(r0.p));
-    S* p1 = const_cast<S*>(static_cast<const S*>(r1.p));
-    const int sub = threadIdx.x & 3;
-    Raw8<DT> rp[2 * kIters];
-    uint32_t pw[2 * kIters], nw[2 * kIters];
+  bool full = true;
 #pragma unroll
-    for (int q = 0; q < 2 * kIters; ++q) {
-      const int64_t e = (q < kIters ? st0 : st1) + (q % kIters) * kSpan + threadIdx.x * 8;
-      rp[q].load((q < kIters ? p0 : p1) + e);
+  for (int c = 0; c < CPB; ++c) full = full && has[c] && rs[c].vec && st[c] + kChunk <= rs[c].n;
+  if (full) {  // block-uniform
+    const int sub = threadIdx.x & 3;
+    Raw8<DT> rp[CPB * kIters];
+    uint32_t pw[CPB * kIters], nw[CPB * kIters];
+#pragma unroll
+    for (int q = 0; q < CPB * kIters; ++q) {
+      const int c = q / kIters;
+      const int64_t e = st[c] + (q % kIters) * kSpan + threadIdx.x * 8;
+      rp[q].load(static_cast<const S*>(rs[c].p) + e);
       // pre-voted: the plane words join the hoisted loads; majority: voted
       // below, one iteration's W words at a time (hoisting all of them spilled)
-      if constexpr (!MAJ) vote_word<false>(v, ((q < kIters ? r0 : r1).bit_off + e) >> 5, pw[q], nw[q]);
+      if constexpr (!MAJ) vote_word<false>(v, (rs[c].bit_off + e) >> 5, pw[q], nw[q]);
     }
 #pragma unroll
-    for (int q = 0; q < 2 * kIters; ++q) {
-      const int64_t e = (q < kIters ? st0 : st1) + (q % kIters) * kSpan + threadIdx.x * 8;
-      if constexpr (MAJ) vote_word<true>(v, ((q < kIters ? r0 : r1).bit_off + e) >> 5, pw[q], nw[q]);
+    for (int q = 0; q < CPB * kIters; ++q) {
+      const int c = q / kIters;
+      const int64_t e = st[c] + (q % kIters) * kSpan + threadIdx.x * 8;
+      if constexpr (MAJ) vote_word<true>(v, (rs[c].bit_off + e) >> 5, pw[q], nw[q]);
       float pv[8];
       rp[q].unpack(pv);
       apply8<DT>(pv, (pw[q] >> (8 * sub)) & 0xffu, (nw[q] >> (8 * sub)) & 0xffu, decay, neg_lr);
-      E::store8((q < kIters ? p0 : p1) + e, pv);
+      E::store8(const_cast<S*>(static_cast<const S*>(rs[c].p)) + e, pv);
     }
     return;
   }
-  apply_chunk<DT, MAJ>(r0, st0, v, decay, neg_lr);
-  if (has1) apply_chunk<DT, MAJ>(r1, st1, v, decay, neg_lr);
+#pragma unroll
+  for (int c = 0; c < CPB; ++c)
+    if (has[c]) apply_chunk<DT, MAJ>(rs[c], st[c], v, decay, neg_lr);
 }
 
 // ----------------------------------------------------------------------- K4
@@ -854,13 +870,13 @@ hipError_t launch_lion_vote_apply(int dt, const int64_t* seg, const int64_t* chu
                                   const uint8_t* own, unsigned long long* agree, hipStream_t st) {
   if (n_chunks == 0) return hipSuccess;
   if (DLION_K2_PAIR && mode == 2 && agree == nullptr) {
-    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_apply_pair_kernel<DT, false>), dim3((n_chunks + 1) / 2),
+    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_apply_pair_kernel<DT, false, DLION_K2_CPB>), dim3((n_chunks + DLION_K2_CPB - 1) / DLION_K2_CPB),
                                           dim3(kThreads), 0, st, seg, chunks, n_chunks, planes, plane_stride, alive,
                                           world, tie, neg, decay, neg_lr));
     return hipGetLastError();
   }
   if (DLION_K2_PAIR_MAJ && mode == 0 && world <= kMaxSliced && agree == nullptr) {
-    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_apply_pair_kernel<DT, true>), dim3((n_chunks + 1) / 2),
+    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_apply_pair_kernel<DT, true, DLION_K2_CPB>), dim3((n_chunks + DLION_K2_CPB - 1) / DLION_K2_CPB),
                                           dim3(kThreads), 0, st, seg, chunks, n_chunks, planes, plane_stride, alive,
                                           world, tie, neg, decay, neg_lr));
     return hipGetLastError();
