@@ -65,7 +65,9 @@
     }                                                                              \
   }
 // dK/dV (A/B): the wave's K-tile row fragments (S = Q K^T's B operand, the
-// same every step) held in 16 VGPRs instead of re-read from LDS each step
+// same every step) held in 16 VGPRs instead of re-read from LDS each step;
+// 2 = loaded straight from global memory, no LDS copy of K at all (16 KB of
+// LDS freed for a deeper Q / dO ring, DLION_DKV_STAGES = 3 at 3 blocks per CU)
 #ifndef DLION_DKV_KREG
 #define DLION_DKV_KREG 0
 #endif
@@ -793,7 +795,8 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   constexpr int NB = DLION_DKV_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> qs_[NB];
   __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[NB];
-  __shared__ __attribute__((aligned(16))) LdsTile<D> kvs_[2][4];  // [K | V][wave's key tile]
+  constexpr int kVs = DLION_DKV_KREG == 2 ? 0 : 1;  // V's slot (K not staged at KREG = 2)
+  __shared__ __attribute__((aligned(16))) LdsTile<D> kvs_[kVs + 1][4];  // [K | V][wave's key tile]
   __shared__ __attribute__((aligned(16))) float ls_[NB][3][32];  // [buf][lse | delta | drop row key][row]
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntiles = ntiles32(a.T), nbhk = a.B * a.Hkv;
@@ -816,8 +819,9 @@ attn_bwd_dkv_kernel(AttnArgs a) {
     for (int j = 0; j < 4; ++j) {
       const int row = __builtin_amdgcn_readfirstlane((first + j) * 32);
       if (row < a.T) {  // block-uniform
-        kd.issue(a.k + b * a.k_sb + hk * a.k_sh + static_cast<int64_t>(row) * a.k_st, kvs_[0][j], a.T - row);
-        vd.issue(a.v + b * a.v_sb + hk * a.v_sh + static_cast<int64_t>(row) * a.v_st, kvs_[1][j], a.T - row);
+        if constexpr (DLION_DKV_KREG != 2)
+          kd.issue(a.k + b * a.k_sb + hk * a.k_sh + static_cast<int64_t>(row) * a.k_st, kvs_[0][j], a.T - row);
+        vd.issue(a.v + b * a.v_sb + hk * a.v_sh + static_cast<int64_t>(row) * a.v_st, kvs_[kVs][j], a.T - row);
       }
     }
   }
@@ -870,12 +874,17 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   const int per_stage = 2 * DmaTile<D>::PPW + (w == 0 ? 1 : 0);
   int qt = first;  // query tile of step i
   bf16x8 kreg[DLION_DKV_KREG ? D / 16 : 1];
+  if constexpr (DLION_DKV_KREG == 2) {  // the lane's key row, straight from global memory (tail rows: a copy of row T-1)
+    const __bf16* kp = a.k + b * a.k_sb + hk * a.k_sh + static_cast<int64_t>(min(key, a.T - 1)) * a.k_st + 8 * hf;
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) kreg[ks] = ld8(kp + 16 * ks);
+  }
   for (int i = 0; i < total; ++i, qt = (qt + 1 == ntiles ? first : qt + 1)) {
     const int buf = i % NB;
     vm_wait_n(min(total - 1 - i, NB - 2) * per_stage);  // step i landed (later steps may be in flight)
     __syncthreads();  // for every wave; and every wave is done with the buffer restaged next
     if (i + NB - 1 < total) stage_next((i + NB - 1) % NB);
-    if constexpr (DLION_DKV_KREG != 0) {
+    if constexpr (DLION_DKV_KREG == 1) {
       if (i == 0) {  // the K / V tiles landed with step 0's wait
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) kreg[ks] = row_frag<D>(kvs_[0][w], r, ks, hf);
@@ -889,9 +898,9 @@ attn_bwd_dkv_kernel(AttnArgs a) {
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) {
           qa[ks] = row_frag<D>(qs_[buf], r, ks, hf);
-          kb_[ks] = row_frag<D>(kvs_[0][w], r, ks, hf);
+          kb_[ks] = DLION_DKV_KREG ? kreg[DLION_DKV_KREG ? ks : 0] : row_frag<D>(kvs_[0][w], r, ks, hf);
           da[ks] = row_frag<D>(ds_[buf], r, ks, hf);
-          vb[ks] = row_frag<D>(kvs_[1][w], r, ks, hf);
+          vb[ks] = row_frag<D>(kvs_[kVs][w], r, ks, hf);
         }
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) {
@@ -904,7 +913,7 @@ attn_bwd_dkv_kernel(AttnArgs a) {
         for (int ks = 0; ks < D / 16; ++ks) {
           s = mfma32(row_frag<D>(qs_[buf], r, ks, hf),
                      DLION_DKV_KREG ? kreg[DLION_DKV_KREG ? ks : 0] : row_frag<D>(kvs_[0][w], r, ks, hf), s);  // S = Q K^T
-          dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), row_frag<D>(kvs_[1][w], r, ks, hf), dp);  // dP = dO V^T
+          dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), row_frag<D>(kvs_[kVs][w], r, ks, hf), dp);  // dP = dO V^T
         }
         DLION_PRIO_OFF(DLION_DKV_PRIO, 1);
       }
