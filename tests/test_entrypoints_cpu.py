@@ -134,3 +134,29 @@ def test_sft_4bit_merge_uses_original_weights(tmp_path):
     q = quantize_model(sft_llama2.build_base(sa, 42), QuantConfig(bnb_4bit_compute_dtype=torch.float32))
     deq = q.model.layers[0].self_attn.q_proj.dequantize(torch.float32)
     assert not torch.allclose(merged[key], deq + (b @ a) * 2.0, atol=1e-4)
+
+
+def test_dpo_checkpointing_decision_sees_lora_and_frozen_reference(tmp_path, monkeypatch):
+    """dpo_llama2 decides activation checkpointing after LoRA injection with the
+    reference frozen: the memory estimate then counts a gradient + momentum only
+    for the adapters (the all-trainable count checkpointed a batch that fits)."""
+    import dpo_llama2
+    from distributed_lion_pytorch_amd.trainer import memory
+
+    seen = {}
+
+    def spy(requested, policy, config, tokens, *models, **kw):
+        seen["trainable"] = [sum(p.numel() for p in m.parameters() if p.requires_grad) for m in models]
+        seen["total"] = [sum(p.numel() for p in m.parameters()) for m in models]
+        return False
+
+    monkeypatch.setattr(memory, "should_checkpoint", spy)
+    tr = dpo_llama2.main(["--model_name_or_path", "llama-tiny", "--synthetic_samples", "60", "--max_length", "1024",
+                          "--max_prompt_length", "256", "--output_dir", str(tmp_path / "dpo"), "--max_steps", "1",
+                          "--per_device_train_batch_size", "2", "--gradient_accumulation_steps", "1", "--lion",
+                          "--async_grad", "--use_cpu", "--torch_dtype", "float32", "--eval_steps", "0",
+                          "--warmup_steps", "1", "--final_save", "false"])
+    assert tr.state.global_step == 1
+    policy, ref = seen["trainable"]
+    assert ref == 0  # the reference is frozen before the estimate
+    assert 0 < policy < seen["total"][0] // 10  # only the LoRA adapters train
