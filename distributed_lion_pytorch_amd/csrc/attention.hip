@@ -47,6 +47,23 @@
 #ifndef DLION_DQ_OPS_LDS
 #define DLION_DQ_OPS_LDS 0
 #endif
+// dQ cycle accounting (diagnostic builds only, DLION_DQ_STAMP=1;
+// tools/attn_dq_stamps.py): s_memtime deltas per wave summed over the loop --
+// [0] wait + barrier at the top of a step, [1] S / dP MFMAs until the exp
+// results exist, [2] dS VALU + dQ MFMA issue, [3] steps computed, [4] steps
+// idle (past the wave's diagonal), [5] waves -- added into g_dq_stamps with
+// vector atomics by lane 0 of every wave
+#ifndef DLION_DQ_STAMP
+#define DLION_DQ_STAMP 0
+#endif
+__device__ unsigned long long g_dq_stamps[8];
+__device__ __forceinline__ unsigned long long memtime() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
 // Start stagger (A/B): the first resident round of blocks (blockIdx < 1024, ~4 per CU)
 // sleeps ((blockIdx >> 8) & 3) * DLION_ATTN_STAGGER * 64 cycles at entry, so the waves
 // that share a SIMD (one per block) start a quarter-period apart instead of in lock
@@ -673,13 +690,23 @@ attn_bwd_dq_kernel(AttnArgs a) {
 #define DLION_DQ_DOF(ks) ((kOps & 1) != 0 ? row_frag<D>(qo_[kDoSlot][kOps != 0 ? wq : 0], r, ks, hf) : dof[ks])
   const int ns = last / NT + 1;
   for (int j = 0; j < NB - 1 && j < ns; ++j) stage(j, j);
+  unsigned long long acc_t[5] = {0, 0, 0, 0, 0}, t_mark = 0;
   for (int st = 0; st < ns; ++st) {
     const int buf = st % NB;
+    if constexpr (DLION_DQ_STAMP) t_mark = memtime();
     // super-tile st has landed once only the later ones' pieces (NT * 2 PPW each) are in flight
     vm_wait_n(min(ns - 1 - st, NB - 2) * NT * 2 * DmaTile<D>::PPW);
     __syncthreads();  // ... for every wave; and every wave is done with the buffer restaged next
+    if constexpr (DLION_DQ_STAMP) {
+      const unsigned long long t = memtime();
+      acc_t[0] += t - t_mark;
+      t_mark = t;
+    }
     if (st + NB - 1 < ns) stage(st + NB - 1, (st + NB - 1) % NB);
     const int kt0 = st * NT;
+    if constexpr (DLION_DQ_STAMP) {
+      if (!(blk.active && kt0 <= qtile)) acc_t[4] += 1;
+    }
     if (blk.active && kt0 <= qtile) {
       // NT independent S / dP chains: one tile's exp / hash VALU work can sit
       // beside the other's MFMAs
@@ -739,6 +766,15 @@ attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg)
           s[j][reg] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][reg], a.scale_log2, -lse2));  // p, carries 1/(1-p)
+      if constexpr (DLION_DQ_STAMP) {
+        float any = 0.f;  // consume the exp results so the stamp lands after them
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) any += s[0][reg];
+        asm volatile("" ::"v"(any));
+        const unsigned long long t = memtime();
+        acc_t[1] += t - t_mark;
+        t_mark = t;
+      }
       DLION_PRIO_ON(DLION_DQ_PRIO, 2);
 #pragma unroll
       for (int j = 0; j < NT; ++j)
@@ -752,6 +788,18 @@ attn_bwd_dq_kernel(AttnArgs a) {
                            dq[t]);  // dQ += dS K
         }
       DLION_PRIO_OFF(DLION_DQ_PRIO, 2);
+      if constexpr (DLION_DQ_STAMP) {
+        const unsigned long long t = memtime();
+        acc_t[2] += t - t_mark;
+        acc_t[3] += 1;
+      }
+    }
+  }
+  if constexpr (DLION_DQ_STAMP) {
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 5; ++i) atomicAdd(&g_dq_stamps[i], acc_t[i]);
+      atomicAdd(&g_dq_stamps[5], 1ull);
     }
   }
 #undef DLION_DQ_QF
@@ -1034,6 +1082,15 @@ attn_bwd_dkv_kernel(AttnArgs a) {
       }
     }
   }
+}
+
+// dQ cycle accounting readout (DLION_DQ_STAMP builds): copy out, optionally reset
+hipError_t attn_dq_stamps(unsigned long long* host8, bool reset) {
+  hipError_t e = hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_dq_stamps), sizeof(unsigned long long) * 8, 0,
+                                     hipMemcpyDeviceToHost);
+  if (e != hipSuccess || !reset) return e;
+  const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_dq_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
 }
 
 // ------------------------------------------------------------------ launchers
