@@ -51,7 +51,7 @@
 // tools/attn_dq_stamps.py): s_memtime deltas per wave summed over the loop --
 // [0] wait + barrier at the top of a step, [1] S / dP MFMAs until the exp
 // results exist, [2] dS VALU + dQ MFMA issue, [3] steps computed, [4] steps
-// idle (past the wave's diagonal), [5] waves -- added into g_dq_stamps with
+// idle (past the wave's diagonal), [5] waves, [6] the DMA wait part of [0] -- added into g_dq_stamps with
 // vector atomics by lane 0 of every wave
 #ifndef DLION_DQ_STAMP
 #define DLION_DQ_STAMP 0
@@ -690,12 +690,16 @@ attn_bwd_dq_kernel(AttnArgs a) {
 #define DLION_DQ_DOF(ks) ((kOps & 1) != 0 ? row_frag<D>(qo_[kDoSlot][kOps != 0 ? wq : 0], r, ks, hf) : dof[ks])
   const int ns = last / NT + 1;
   for (int j = 0; j < NB - 1 && j < ns; ++j) stage(j, j);
-  unsigned long long acc_t[5] = {0, 0, 0, 0, 0}, t_mark = 0;
+  unsigned long long acc_t[6] = {0, 0, 0, 0, 0, 0}, t_mark = 0;
   for (int st = 0; st < ns; ++st) {
     const int buf = st % NB;
     if constexpr (DLION_DQ_STAMP) t_mark = memtime();
     // super-tile st has landed once only the later ones' pieces (NT * 2 PPW each) are in flight
     vm_wait_n(min(ns - 1 - st, NB - 2) * NT * 2 * DmaTile<D>::PPW);
+    if constexpr (DLION_DQ_STAMP) {
+      const unsigned long long t = memtime();
+      acc_t[5] += t - t_mark;  // the DMA wait alone
+    }
     __syncthreads();  // ... for every wave; and every wave is done with the buffer restaged next
     if constexpr (DLION_DQ_STAMP) {
       const unsigned long long t = memtime();
@@ -800,6 +804,7 @@ attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
       for (int i = 0; i < 5; ++i) atomicAdd(&g_dq_stamps[i], acc_t[i]);
       atomicAdd(&g_dq_stamps[5], 1ull);
+      atomicAdd(&g_dq_stamps[6], acc_t[5]);
     }
   }
 #undef DLION_DQ_QF

@@ -32,6 +32,8 @@ def main():
     print(f"waves {st[5]}, steps computed {st[3]}, steps idle {st[4]}")
     for i, n in enumerate(names):
         print(f"  {n:28s} {st[i] / max(1, st[5]):12.0f} cycles per wave  {100.0 * st[i] / max(1, tot):5.1f} %")
+    print(f"  of which the DMA wait (vm_wait before the barrier): {st[6] / max(1, st[5]):.0f} cycles per wave "
+          f"({100.0 * st[6] / max(1, st[0]):.1f} % of the top wait)")
     print(f"  per computed step: barrier {st[0] / max(1, st[3] + st[4]):.0f} (per step incl. idle), "
           f"S/dP->exp {st[1] / max(1, st[3]):.0f}, dS+dQ {st[2] / max(1, st[3]):.0f} cycles")
 
