@@ -410,8 +410,33 @@ def _install_guarded_gathers(trainer, el) -> None:
     trainer.accelerator.wait_for_everyone = el.barrier
 
 
-class AsyncTrainer(AsyncMixin, Trainer):
+class RankShardedLoaderMixin:
+    """Training sets that shard themselves per rank (``rank_sharded``: the
+    SFT :class:`~..utils.data.PackedStream`, run_clm's ``--streaming``
+    :class:`~..utils.data.CLMStream`) get a plain DataLoader instead of
+    accelerate's: accelerate would either read the stream on rank 0 and
+    broadcast every batch (``dispatch_batches``, the reference's path for
+    iterable data) or wrap it in an ``IterableDatasetShard`` that drops
+    (W-1)/W of the already-sharded batches.  Batches are moved to the device by
+    ``_prepare_inputs``."""
+
+    def get_train_dataloader(self):
+        ds = self.train_dataset
+        if getattr(ds, "rank_sharded", False):
+            from torch.utils.data import DataLoader
+
+            return DataLoader(ds, batch_size=self._train_batch_size, collate_fn=self.data_collator,
+                              num_workers=0, pin_memory=self.args.dataloader_pin_memory)
+        return super().get_train_dataloader()
+
+
+class AsyncTrainer(AsyncMixin, RankShardedLoaderMixin, Trainer):
     """HF Trainer without gradient all-reduce (reference async_trainer.py:8-34)."""
+
+
+class LocalTrainer(RankShardedLoaderMixin, Trainer):
+    """Stock HF Trainer (DDP gradient all-reduce, the reference's path without
+    ``--async_grad``) that also takes rank-sharded streams."""
 
 
 def warn_unsynced(args) -> None:

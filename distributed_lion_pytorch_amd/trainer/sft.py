@@ -14,8 +14,8 @@ from typing import Callable, Optional
 from transformers import Trainer, default_data_collator
 
 from ..models.lora import LoraConfig, inject_lora
-from ..utils.data import ConstantLengthDataset, PackedStream, prepare_sample_text
-from .async_trainer import AsyncMixin
+from ..utils.data import ConstantLengthDataset, prepare_sample_text
+from .async_trainer import AsyncMixin, RankShardedLoaderMixin
 
 
 def _is_packed(ds) -> bool:
@@ -28,7 +28,7 @@ def _is_packed(ds) -> bool:
     return isinstance(item, dict) and "input_ids" in item
 
 
-class SFTTrainer(Trainer):
+class SFTTrainer(RankShardedLoaderMixin, Trainer):
     def __init__(self, model=None, args=None, train_dataset=None, eval_dataset=None, tokenizer=None,
                  processing_class=None, peft_config: Optional[LoraConfig] = None, packing: bool = True,
                  max_seq_length: int = 1024, formatting_func: Optional[Callable] = None, data_collator=None,
@@ -43,20 +43,6 @@ class SFTTrainer(Trainer):
             eval_dataset = ConstantLengthDataset(tok, eval_dataset, fmt, seq_length=max_seq_length)
         super().__init__(model=model, args=args, train_dataset=train_dataset, eval_dataset=eval_dataset,
                          processing_class=tok, data_collator=data_collator or default_data_collator, **kwargs)
-
-    def get_train_dataloader(self):
-        """A :class:`PackedStream` shards its rows per rank itself, so its
-        loader is NOT handed to accelerate: accelerate would either read the
-        stream on rank 0 and broadcast every batch (``dispatch_batches``, the
-        reference's path for iterable data) or wrap it in an
-        ``IterableDatasetShard`` that drops (W-1)/W of the already-sharded
-        batches.  Batches are moved to the device by ``_prepare_inputs``."""
-        if isinstance(self.train_dataset, PackedStream):
-            from torch.utils.data import DataLoader
-
-            return DataLoader(self.train_dataset, batch_size=self._train_batch_size, collate_fn=self.data_collator,
-                              num_workers=0, pin_memory=self.args.dataloader_pin_memory)
-        return super().get_train_dataloader()
 
 
 class AsyncSFTTrainer(AsyncMixin, SFTTrainer):

@@ -195,6 +195,180 @@ def clm_blocks(texts: Sequence[str], tokenizer, block_size: int, num_workers: Op
     return TokenBlocks(torch.from_numpy(arr))
 
 
+# ------------------------------------------------- run_clm local files
+# The reference loads --train_file / --validation_file by extension through
+# ``datasets.load_dataset(extension, data_files=...)`` ("txt" -> the "text"
+# builder with ``keep_linebreaks``; csv; json) and, without a validation file,
+# carves ``train[:p%]`` / ``train[p%:]`` out of the train file
+# (/root/reference/run_clm.py:343-381).  The text column is "text" if present,
+# else the first column (:455-458).  Same here, offline: ``datasets`` reads
+# local files without the hub; without ``datasets`` a small reader of the same
+# three formats stands in (blank lines stay rows, as in the text builder).
+def file_builder(path: str) -> str:
+    """The ``datasets`` builder name for a data file (reference: its extension,
+    ``txt`` -> ``text``; ``jsonl`` is read by the json builder too)."""
+    ext = path.rsplit(".", 1)[-1].lower()
+    return {"txt": "text", "jsonl": "json"}.get(ext, ext)
+
+
+def text_column(columns: Sequence[str]) -> str:
+    cols = list(columns)
+    if not cols:
+        raise ValueError("the data file has no columns")
+    return "text" if "text" in cols else cols[0]
+
+
+def _fallback_rows(builder: str, path: str, keep_linebreaks: bool) -> List[Dict]:
+    """The three builders' row semantics without ``datasets``."""
+    import csv
+
+    if builder == "text":
+        with open(path, encoding="utf-8") as f:
+            return [{"text": ln if keep_linebreaks else ln.rstrip("\n")} for ln in f]
+    if builder == "json":
+        with open(path, encoding="utf-8") as f:
+            head = f.read(1)
+            while head and head.isspace():
+                head = f.read(1)
+            f.seek(0)
+            if head == "[":
+                return list(json.load(f))
+            return [json.loads(ln) for ln in f if ln.strip()]
+    if builder == "csv":
+        with open(path, encoding="utf-8", newline="") as f:
+            return list(csv.DictReader(f))
+    raise ValueError(f"unsupported data file type {builder!r} (csv, json, jsonl, txt)")
+
+
+def _percent_split(n: int, pct: float):
+    """HF percent slicing boundary (``train[:p%]``: rounded to the closest row)."""
+    return int(round(n * pct / 100.0))
+
+
+def load_local_splits(train_file: Optional[str], validation_file: Optional[str], keep_linebreaks: bool = True,
+                      validation_split_percentage: float = 5, streaming: bool = False,
+                      cache_dir: Optional[str] = None):
+    """(train_rows, validation_rows, text_column) for run_clm's local files.
+
+    Without streaming the rows are ``datasets`` Datasets (or lists of dicts);
+    with streaming they are lazy re-iterable row sources (``datasets``
+    IterableDataset ``take`` / ``skip``): nothing of the corpus is held in
+    memory.  The validation rows without a validation file are the first
+    ``validation_split_percentage`` percent of the train file, exactly the
+    reference's ``train[:p%]`` / ``train[p%:]`` (a streaming run counts the
+    rows in one lazy pass to place that boundary)."""
+    src = train_file if train_file is not None else validation_file
+    if src is None:
+        raise ValueError("no data file given")
+    builder = file_builder(src)
+    kw = {"keep_linebreaks": keep_linebreaks} if builder == "text" else {}
+    files = {}
+    if train_file is not None:
+        files["train"] = train_file
+    if validation_file is not None:
+        files["validation"] = validation_file
+    try:
+        import datasets
+    except ImportError:  # pragma: no cover - datasets is installed in this image
+        datasets = None
+    if datasets is None:
+        raw = {k: _fallback_rows(builder, v, keep_linebreaks) for k, v in files.items()}
+        tr, va = raw.get("train"), raw.get("validation")
+        if va is None and tr is not None:
+            n_val = _percent_split(len(tr), validation_split_percentage)
+            tr, va = tr[n_val:], tr[:n_val]
+        cols = list((tr or va)[0].keys()) if (tr or va) else ["text"]
+        return tr, va, text_column(cols)
+    if streaming:
+        raw = datasets.load_dataset(builder, data_files=files, streaming=True, **kw)
+        tr, va = raw.get("train"), raw.get("validation")
+        if va is None and tr is not None:
+            n_val = _percent_split(sum(1 for _ in tr), validation_split_percentage)
+            tr, va = tr.skip(n_val), tr.take(n_val)
+        probe = tr if tr is not None else va
+        cols = probe.column_names
+        if cols is None:  # features resolved from the first row
+            first = next(iter(probe), None)
+            cols = list(first.keys()) if first is not None else ["text"]
+        return tr, va, text_column(cols)
+    raw = datasets.load_dataset(builder, data_files=files, cache_dir=cache_dir, **kw)
+    tr, va = raw.get("train"), raw.get("validation")
+    if va is None and tr is not None:
+        p = validation_split_percentage
+        va = datasets.load_dataset(builder, data_files=files, split=f"train[:{p}%]", cache_dir=cache_dir, **kw)
+        tr = datasets.load_dataset(builder, data_files=files, split=f"train[{p}%:]", cache_dir=cache_dir, **kw)
+    return tr, va, text_column((tr if tr is not None else va).column_names)
+
+
+def column_texts(rows, col: str) -> List[str]:
+    """A column of a Dataset / list of row dicts as a list of strings."""
+    if rows is None:
+        return []
+    if hasattr(rows, "column_names") and not isinstance(rows, list):
+        return list(rows[col])
+    return [r[col] for r in rows]
+
+
+class CLMStream(torch.utils.data.IterableDataset):
+    """run_clm's ``--streaming`` pipeline on a lazy row source: the
+    reference's two batched maps (tokenize, then group_texts over 1000-text
+    batches with each batch's remainder dropped, run_clm.py:463-544) applied
+    one batch at a time, so at most ``map_batch`` texts and their tokens are
+    held (``peak_buffer_rows`` / ``peak_buffer_tokens`` record it) -- a corpus
+    larger than memory streams through.
+
+    With ``shard`` (training) every rank runs the same deterministic block
+    stream and keeps blocks ``i % W == rank`` from each complete group of W,
+    so all ranks yield the same number of blocks (equal step counts, no rank
+    ends its epoch early) without rank 0 reading and broadcasting every batch
+    (``rank_sharded``: the trainer hands it to a plain DataLoader).
+    ``max_blocks`` caps the global block count (``max_train_samples``)."""
+
+    rank_sharded = True
+
+    def __init__(self, rows, column: str, tokenizer, block_size: int, shard: bool = True,
+                 max_blocks: Optional[int] = None, map_batch: int = MAP_BATCH):
+        self.rows, self.col, self.tok, self.block = rows, column, tokenizer, int(block_size)
+        self.shard, self.max_blocks, self.map_batch = shard, max_blocks, int(map_batch)
+        self.rank_sharded = bool(shard)
+        self.peak_buffer_rows = 0
+        self.peak_buffer_tokens = 0
+
+    def _batches(self):
+        buf: List[str] = []
+        for row in self.rows:
+            buf.append(row[self.col])
+            if len(buf) == self.map_batch:
+                yield buf
+                buf = []
+        if buf:
+            yield buf
+
+    def blocks(self):
+        """The global (unsharded) block stream."""
+        n = 0
+        for texts in self._batches():
+            self.peak_buffer_rows = max(self.peak_buffer_rows, len(texts))
+            ids = self.tok(texts)["input_ids"]
+            self.peak_buffer_tokens = max(self.peak_buffer_tokens, sum(len(x) for x in ids))
+            for blk in _group_batch(ids, self.block):
+                if self.max_blocks is not None and n >= self.max_blocks:
+                    return
+                n += 1
+                yield blk
+
+    def __iter__(self):
+        rank, world = _dist_shard() if self.shard else (0, 1)
+        group: List[List[int]] = []
+        for blk in self.blocks():
+            group.append(blk)
+            if len(group) < world:
+                continue
+            x = torch.tensor(group[rank], dtype=torch.long)
+            group = []
+            yield {"input_ids": x, "labels": x.clone()}
+
+
 # ---------------------------------------------------------------- SFT data
 def _sentence(rng: random.Random, n: int) -> str:
     return " ".join(rng.choice(_WORDS) for _ in range(n))
@@ -214,7 +388,8 @@ def prepare_sample_text(example: Dict[str, str]) -> str:
 
 class ConstantLengthDataset(Dataset):
     """Packed fixed-length training chunks (trl ConstantLengthDataset semantics,
-    sft_llama2.py:122-129): samples are formatted, tokenized, joined with EOS
+    sft_llama2.py:122-129): samples are formatted, tokenized (with the
+    tokenizer's special tokens, trl's default), joined with EOS
     and cut into ``seq_length`` blocks.  Map-style (pre-packed once), so every
     rank reads its own shard instead of rank 0 broadcasting each batch."""
 
@@ -223,7 +398,7 @@ class ConstantLengthDataset(Dataset):
         eos = tokenizer.eos_token_id if eos_token_id is None else eos_token_id
         toks: List[int] = []
         for ex in dataset:
-            toks.extend(tokenizer(formatting_func(ex), add_special_tokens=False)["input_ids"])
+            toks.extend(tokenizer(formatting_func(ex), add_special_tokens=True)["input_ids"])
             toks.append(eos)
         n = max(1, len(toks) // seq_length)
         if len(toks) < seq_length:
@@ -348,7 +523,13 @@ class PackedStream(torch.utils.data.IterableDataset):
     rank reads every row but keeps rows i % W == rank (``shard``), so ranks
     train on disjoint data with no broadcast.  ``peak_buffer_chars`` records
     the largest character buffer held (memory is bounded by it, not by the
-    corpus)."""
+    corpus).  Samples are tokenized with the tokenizer's default special
+    tokens (trl's ``add_special_tokens=True``: a BOS per sample for Llama),
+    then joined with EOS.  An infinite stream whose rank shard holds no rows
+    (fewer rows than ranks) raises instead of ending: that rank would stop
+    training while the others block in the vote collectives."""
+
+    rank_sharded = True
 
     def __init__(self, tokenizer, rows, formatting_func=prepare_sample_text, seq_length: int = 1024,
                  infinite: bool = False, chars_per_token: float = 3.6, num_of_sequences: int = 1024,
@@ -380,7 +561,11 @@ class PackedStream(torch.utils.data.IterableDataset):
                     text = self.fmt(next(it))
                     seen += 1
                 except StopIteration:
-                    if not self.infinite or seen == 0:  # finite, or a source with no rows for this rank
+                    if self.infinite and seen == 0:
+                        raise ValueError(f"rank {rank} of {world}: no rows in this rank's shard of the "
+                                         "training stream (fewer rows than ranks); an infinite stream "
+                                         "cannot end on one rank only") from None
+                    if not self.infinite:
                         more = False
                         break
                     epoch, seen = epoch + 1, 0
@@ -392,7 +577,7 @@ class PackedStream(torch.utils.data.IterableDataset):
             if not buf:
                 break
             ids: List[int] = []
-            for t in self.tok(buf, add_special_tokens=False)["input_ids"]:
+            for t in self.tok(buf, add_special_tokens=True)["input_ids"]:
                 ids.extend(t)
                 ids.append(self.eos)
             for i in range(0, len(ids) - self.seq_length + 1, self.seq_length):

@@ -8,8 +8,11 @@ TrainingArguments + ``--lion`` / ``--async_grad``), MI355X-native underneath:
 * ``--lion`` builds the distributed Lion (1-bit vote exchange over RCCL);
   ``--async_grad`` trains with per-rank gradients (``AsyncTrainer``);
 * runs offline: ``--synthetic_data`` (or no dataset) trains on random token
-  blocks; ``--train_file`` reads a local text file; configs come from the
-  built-in size registry (``--config_name gpt2``) or a local directory;
+  blocks; ``--train_file`` / ``--validation_file`` are read by extension
+  (txt / csv / json / jsonl, the "text" column or the first one) like the
+  reference, and ``--streaming`` tokenizes and groups them lazily (a corpus
+  larger than host memory streams through); configs come from the built-in
+  size registry (``--config_name gpt2``) or a local directory;
 * no wandb login, no hub telemetry; AdamW fallback keeps the
   reference's hard-coded weight_decay=0.1 (D17) and warns about it.
 
@@ -28,15 +31,17 @@ from typing import Optional
 
 import torch
 import transformers
-from transformers import HfArgumentParser, Trainer, set_seed
+from transformers import HfArgumentParser, set_seed
 from transformers.trainer_utils import get_last_checkpoint
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from distributed_lion_pytorch_amd.models.registry import build_model, load_config  # noqa: E402
 from distributed_lion_pytorch_amd.trainer.async_trainer import (  # noqa: E402
-    AsyncTrainer, AsyncTrainingArguments, build_lion, warn_unsynced)
-from distributed_lion_pytorch_amd.utils.data import SyntheticCLMDataset, clm_blocks, default_cache_dir, load_tokenizer  # noqa: E402
+    AsyncTrainer, AsyncTrainingArguments, LocalTrainer, build_lion, warn_unsynced)
+from distributed_lion_pytorch_amd.utils.data import (CLMStream, SyntheticCLMDataset, clm_blocks,  # noqa: E402
+                                                     column_texts, default_cache_dir, load_local_splits,
+                                                     load_tokenizer)
 from distributed_lion_pytorch_amd.utils.metrics import JsonlMetricsCallback  # noqa: E402
 
 logger = logging.getLogger(__name__)
@@ -62,7 +67,7 @@ class ModelArguments:
 class DataTrainingArguments:
     dataset_name: Optional[str] = field(default=None)
     dataset_config_name: Optional[str] = field(default=None)
-    train_file: Optional[str] = field(default=None, metadata={"help": "local text file"})
+    train_file: Optional[str] = field(default=None, metadata={"help": "local csv / json / jsonl / txt file"})
     validation_file: Optional[str] = field(default=None)
     max_train_samples: Optional[int] = field(default=None)
     max_eval_samples: Optional[int] = field(default=None)
@@ -73,12 +78,6 @@ class DataTrainingArguments:
     preprocessing_num_workers: Optional[int] = field(default=None)
     keep_linebreaks: bool = field(default=True)
     synthetic_samples: int = field(default=100_000, metadata={"help": "size of the synthetic train set"})
-
-
-def _read_text(path: str, keep_linebreaks: bool):
-    with open(path, encoding="utf-8") as f:
-        lines = f.read().splitlines(keepends=keep_linebreaks)
-    return [ln for ln in lines if ln.strip()]
 
 
 def split_train_validation(texts, pct: int):
@@ -113,7 +112,7 @@ def _cap(ds, n: Optional[int]):
     return torch.utils.data.Subset(ds, range(n))
 
 
-def build_datasets(data_args, train_args, tokenizer, vocab_size, block_size):
+def build_datasets(data_args, train_args, tokenizer, vocab_size, block_size, cache_dir=None):
     pct = data_args.validation_split_percentage if data_args.validation_split_percentage is not None else 5
     if data_args.dataset_name and not train_args.synthetic_data:
         try:
@@ -133,19 +132,34 @@ def build_datasets(data_args, train_args, tokenizer, vocab_size, block_size):
         except Exception as e:  # offline: no hub datasets
             logger.warning("dataset %s unavailable offline (%s); falling back to synthetic data",
                            data_args.dataset_name, e)
-    if data_args.train_file and not train_args.synthetic_data:
-        tr = _read_text(data_args.train_file, data_args.keep_linebreaks)
-        if data_args.validation_file:
-            va = _read_text(data_args.validation_file, data_args.keep_linebreaks)
-        else:
-            tr, va = split_train_validation(tr, pct)
-        return (_cap(_blocks(tr, tokenizer, block_size, data_args, train_args), data_args.max_train_samples),
-                _cap(_blocks(va, tokenizer, block_size, data_args, train_args), data_args.max_eval_samples))
+    if (data_args.train_file or data_args.validation_file) and not train_args.synthetic_data:
+        # by extension through datasets.load_dataset (reference run_clm.py:343-381)
+        tr, va, col = load_local_splits(data_args.train_file, data_args.validation_file, data_args.keep_linebreaks,
+                                        pct, streaming=data_args.streaming, cache_dir=cache_dir)
+        if data_args.streaming:
+            # lazy tokenize + group_texts; no main_process_first: nothing is cached
+            # (the reference's streaming maps run without num_proc / cache files, :484-489, :540-544)
+            return (CLMStream(tr, col, tokenizer, block_size, shard=True, max_blocks=data_args.max_train_samples)
+                    if tr is not None else None,
+                    CLMStream(va, col, tokenizer, block_size, shard=False, max_blocks=data_args.max_eval_samples)
+                    if va is not None else None)
+        return (_cap(_blocks(column_texts(tr, col), tokenizer, block_size, data_args, train_args),
+                     data_args.max_train_samples),
+                _cap(_blocks(column_texts(va, col), tokenizer, block_size, data_args, train_args),
+                     data_args.max_eval_samples))
     n_train = data_args.max_train_samples or data_args.synthetic_samples
     n_eval = data_args.max_eval_samples or max(8, n_train // 20)
     # disjoint by construction: the eval set is drawn from a different seed
     return (SyntheticCLMDataset(n_train, block_size, vocab_size, seed=train_args.seed),
             SyntheticCLMDataset(n_eval, block_size, vocab_size, seed=train_args.seed + 1))
+
+
+def _n_samples(ds, cap):
+    """len() of a map-style set; for a stream the cap (or -1: unknown)."""
+    try:
+        return len(ds)
+    except TypeError:
+        return cap if cap is not None else -1
 
 
 def resize_embeddings_for(model, tokenizer) -> bool:
@@ -165,11 +179,13 @@ def main(argv=None):
     else:
         model_args, data_args, training_args = parser.parse_args_into_dataclasses(args=argv)
 
-    if data_args.streaming:
-        # the reference streams hub datasets (run_clm.py:323); there is no hub here and the
-        # local paths are map-style -- refuse instead of silently loading everything
-        raise ValueError("--streaming is not supported: datasets are read from local files / synthetic data "
-                         "(no network); drop the flag")
+    if data_args.streaming and not (data_args.train_file or data_args.validation_file):
+        # the reference streams hub datasets (run_clm.py:323); there is no hub here: streaming
+        # covers local files (--train_file / --validation_file), refuse it for anything else
+        raise ValueError("--streaming needs --train_file / --validation_file (local files; there is no hub "
+                         "offline): synthetic data and saved datasets are map-style")
+    if data_args.streaming and training_args.do_train and not (training_args.max_steps and training_args.max_steps > 0):
+        raise ValueError("--streaming needs --max_steps (a stream has no length; reference run_clm.py:204)")
 
     logging.basicConfig(format="%(asctime)s - %(levelname)s - %(name)s - %(message)s", datefmt="%m/%d/%Y %H:%M:%S",
                         handlers=[logging.StreamHandler(sys.stdout)])
@@ -199,7 +215,8 @@ def main(argv=None):
 
     max_pos = getattr(config, "n_positions", None) or getattr(config, "max_position_embeddings", 1024)
     block_size = min(data_args.block_size or 1024, max_pos)
-    train_ds, eval_ds = build_datasets(data_args, training_args, tokenizer, model.config.vocab_size, block_size)
+    train_ds, eval_ds = build_datasets(data_args, training_args, tokenizer, model.config.vocab_size, block_size,
+                                       cache_dir=model_args.cache_dir)
 
     def preprocess_logits_for_metrics(logits, labels):
         if isinstance(logits, tuple):
@@ -226,7 +243,7 @@ def main(argv=None):
     else:  # D18: a cosine schedule over max_steps=-1 is broken; let HF derive the length
         optimizers = (optimizer, None)
 
-    trainer_class = AsyncTrainer if training_args.async_grad else Trainer
+    trainer_class = AsyncTrainer if training_args.async_grad else LocalTrainer
     trainer = trainer_class(
         model=model,
         args=training_args,
@@ -248,14 +265,14 @@ def main(argv=None):
         if hasattr(tokenizer, "save_pretrained") and trainer.is_world_process_zero():
             tokenizer.save_pretrained(training_args.output_dir)
         metrics = train_result.metrics
-        metrics["train_samples"] = len(train_ds)
+        metrics["train_samples"] = _n_samples(train_ds, data_args.max_train_samples)
         trainer.log_metrics("train", metrics)
         trainer.save_metrics("train", metrics)
         trainer.save_state()
 
     if training_args.do_eval:
         metrics = trainer.evaluate()
-        metrics["eval_samples"] = len(eval_ds)
+        metrics["eval_samples"] = _n_samples(eval_ds, data_args.max_eval_samples)
         try:
             metrics["perplexity"] = math.exp(metrics["eval_loss"])
         except OverflowError:
