@@ -34,25 +34,48 @@ logger = logging.getLogger(__name__)
 
 
 @dataclass
-class AsyncTrainingArguments(TrainingArguments):
-    """HF TrainingArguments + the reference's flags (run_clm.py:73-86) + Lion knobs."""
+class LionArguments:
+    """The Lion knobs every entrypoint exposes: run_clm through
+    :class:`AsyncTrainingArguments`, ``sft_llama2.py`` / ``dpo_llama2.py`` as
+    their own argument group (:func:`apply_lion_args` copies them onto the
+    TrainingArguments the trainer reads).  ``lion_bucket_mb`` None sizes the
+    vote buckets automatically (>= 4 per step at W > 1 on RCCL, so encode of
+    bucket i+1 overlaps the exchange of bucket i; optim/lion.py)."""
 
-    lion: bool = field(default=False, metadata={"help": "use the (distributed) Lion optimizer"})
-    async_grad: bool = field(default=False, metadata={
-        "help": "compute gradients per worker and never combine them (sync only via Lion's vote)"})
     lion_beta1: float = field(default=0.9, metadata={"help": "Lion beta1"})
     lion_beta2: float = field(default=0.99, metadata={"help": "Lion beta2"})
     lion_vote: str = field(default="majority", metadata={"help": "majority | average"})
     lion_tie_break: str = field(default="negative", metadata={"help": "negative (reference) | zero | positive"})
     lion_wire: str = field(default="a2a", metadata={"help": "allgather | a2a | ref_int64"})
-    lion_bucket_mb: float = field(default=32.0, metadata={"help": "packed-bit bucket size (MB)"})
+    lion_bucket_mb: Optional[float] = field(default=None, metadata={
+        "help": "packed-bit bucket size (MB); default: automatic (>= 4 pipelined buckets at W > 1)"})
     lion_stochastic_max_norm: Optional[float] = field(default=None, metadata={
         "help": "enable stochastic binarization with this max_grad_norm (reference max_grad_norm)"})
     lion_backend: str = field(default="auto", metadata={"help": "auto | hip | torch"})
     lion_dropout_schedule: Optional[str] = field(default=None, metadata={
         "help": "fault injection, e.g. '100:3' drops rank 3 from optimizer step 100 on"})
     lion_elastic_timeout: Optional[float] = field(default=None, metadata={
-        "help": "real worker dropout: heartbeat timeout (s) before each vote; survivors regroup and continue"})
+        "help": "real worker dropout: collective deadline (s); survivors regroup and continue "
+                "(launch with python -m distributed_lion_pytorch_amd.launch for death notices)"})
+
+
+def apply_lion_args(training_args, lion_args: LionArguments):
+    """Copy the Lion knobs onto ``training_args`` (what build_lion and the
+    AsyncMixin read)."""
+    import dataclasses
+
+    for f in dataclasses.fields(LionArguments):
+        setattr(training_args, f.name, getattr(lion_args, f.name))
+    return training_args
+
+
+@dataclass
+class AsyncTrainingArguments(TrainingArguments, LionArguments):
+    """HF TrainingArguments + the reference's flags (run_clm.py:73-86) + Lion knobs."""
+
+    lion: bool = field(default=False, metadata={"help": "use the (distributed) Lion optimizer"})
+    async_grad: bool = field(default=False, metadata={
+        "help": "compute gradients per worker and never combine them (sync only via Lion's vote)"})
     synthetic_data: bool = field(default=False, metadata={"help": "train on synthetic token ids (offline)"})
 
 
@@ -78,7 +101,7 @@ def build_lion(model: torch.nn.Module, args, lr: Optional[float] = None, weight_
         vote=getattr(args, "lion_vote", "majority"),
         tie_break=getattr(args, "lion_tie_break", "negative"),
         exchange=getattr(args, "lion_wire", "a2a"),
-        bucket_mb=getattr(args, "lion_bucket_mb", 32.0),
+        bucket_mb=getattr(args, "lion_bucket_mb", None),
         backend=getattr(args, "lion_backend", "auto"),
         seed=getattr(args, "seed", 0),
         elastic_timeout=getattr(args, "lion_elastic_timeout", None),
@@ -200,7 +223,9 @@ class AsyncMixin:
             self.args.ddp_broadcast_buffers = False
             self._elastic()
         out = super().train(*a, **kw)
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        elastic = getattr(self, "_dlion_elastic", None)
+        # also when a regroup left a single survivor: world_end records the shrink
+        if dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or elastic is not None):
             same = replicas_identical(self.model, self._elastic())
             self.log({"replicas_identical": float(same), "world_end": float(dist.get_world_size())})
         return out

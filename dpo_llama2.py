@@ -15,7 +15,9 @@ Same ScriptArguments (beta, lr, schedule, LoRA, lengths, steps, ``--lion``,
 * LoRA targets use Llama module names (q_proj, k_proj, v_proj -- the modules
   that actually matched in the reference's GPT-J-style list, D11);
 * the optimizer sees the adapter parameters and ``--weight_decay`` (0.05 by
-  default) is actually forwarded to it (D10, D12).
+  default) is actually forwarded to it (D10, D12);
+* every Lion knob of run_clm (``--lion_*``, incl. ``--lion_elastic_timeout``
+  for real worker dropout and ``--ddp_backend`` for the process group).
 Offline: prompt/chosen/rejected triples are synthetic unless
 ``--dataset_name`` is a local json/jsonl file with those fields.
 """
@@ -36,7 +38,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from distributed_lion_pytorch_amd.models.lora import LoraConfig, print_trainable_parameters  # noqa: E402
 from distributed_lion_pytorch_amd.models.registry import build_model, load_config  # noqa: E402
-from distributed_lion_pytorch_amd.trainer.async_trainer import build_lion, warn_unsynced  # noqa: E402
+from distributed_lion_pytorch_amd.trainer.async_trainer import (LionArguments, apply_lion_args,  # noqa: E402
+                                                                build_lion, warn_unsynced)
 from distributed_lion_pytorch_amd.trainer.dpo import AsyncDPOTrainer, DPOTrainer  # noqa: E402
 from distributed_lion_pytorch_amd.utils.data import load_tokenizer, synthetic_paired  # noqa: E402
 from distributed_lion_pytorch_amd.utils.metrics import JsonlMetricsCallback  # noqa: E402
@@ -78,7 +81,6 @@ class ScriptArguments:
     ignore_bias_buffers: Optional[bool] = field(default=False)
     lion: Optional[bool] = field(default=False, metadata={"help": "whether to use lion optimizer"})
     async_grad: Optional[bool] = field(default=False, metadata={"help": "do not sync gradients between workers"})
-    lion_wire: Optional[str] = field(default="a2a")
     dataset_name: Optional[str] = field(default=None, metadata={"help": "local json/jsonl of prompt/chosen/rejected"})
     synthetic_samples: Optional[int] = field(default=10000)
     synthetic_chars: Optional[int] = field(default=None, metadata={
@@ -92,6 +94,7 @@ class ScriptArguments:
     bf16: Optional[bool] = field(default=True)
     seed: Optional[int] = field(default=0)
     use_cpu: Optional[bool] = field(default=False)
+    ddp_backend: Optional[str] = field(default=None, metadata={"help": "nccl (RCCL) | gloo; default: HF's choice"})
 
 
 def load_pairs(args):
@@ -108,8 +111,8 @@ def load_pairs(args):
 
 
 def main(argv=None):
-    parser = HfArgumentParser(ScriptArguments)
-    (script_args,) = parser.parse_args_into_dataclasses(args=argv)
+    parser = HfArgumentParser((ScriptArguments, LionArguments))
+    script_args, lion_args = parser.parse_args_into_dataclasses(args=argv)
     logging.basicConfig(level=logging.INFO, handlers=[logging.StreamHandler(sys.stdout)])
     transformers.set_seed(script_args.seed)
 
@@ -153,8 +156,9 @@ def main(argv=None):
         run_name="dpo_llama2",
         seed=script_args.seed,
         use_cpu=script_args.use_cpu,
+        ddp_backend=script_args.ddp_backend,
     )
-    training_args.lion_wire = script_args.lion_wire
+    apply_lion_args(training_args, lion_args)  # --lion_* knobs, incl. --lion_elastic_timeout (worker dropout)
 
     peft_config = None
     if script_args.use_lora:

@@ -17,6 +17,10 @@
   an infinite packed training stream read lazily and sharded per rank);
   offline: the stack-exchange-paired data is replaced by a synthetic corpus of
   the same format unless ``--dataset_name`` points at a local json/jsonl file;
+* every Lion knob of run_clm (``--lion_beta1/2``, ``--lion_vote``,
+  ``--lion_tie_break``, ``--lion_wire``, ``--lion_bucket_mb``,
+  ``--lion_stochastic_max_norm``, ``--lion_dropout_schedule`` and
+  ``--lion_elastic_timeout`` for real worker dropout);
 * saves the adapter (final_checkpoint/) and the merged model
   (final_merged_checkpoint/, safetensors) like sft_llama2.py:183-199.
 """
@@ -38,7 +42,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from distributed_lion_pytorch_amd.models.lora import (LoraConfig, load_adapter, merge_and_unload,  # noqa: E402
                                                       print_trainable_parameters, save_adapter)
 from distributed_lion_pytorch_amd.models.registry import build_model, load_config  # noqa: E402
-from distributed_lion_pytorch_amd.trainer.async_trainer import build_lion, warn_unsynced  # noqa: E402
+from distributed_lion_pytorch_amd.trainer.async_trainer import (LionArguments, apply_lion_args,  # noqa: E402
+                                                                build_lion, warn_unsynced)
 from distributed_lion_pytorch_amd.trainer.sft import AsyncSFTTrainer, SFTTrainer  # noqa: E402
 from distributed_lion_pytorch_amd.utils.data import (ConstantLengthDataset, PackedStream, RowSlice,  # noqa: E402
                                                      Rows, ShuffledRows, chars_token_ratio, load_tokenizer,
@@ -67,7 +72,6 @@ class ScriptArguments:
     use_lora: Optional[bool] = field(default=True, metadata={"help": "False: full fine-tune"})
     lion: Optional[bool] = field(default=False, metadata={"help": "whether to use lion optimizer"})
     async_grad: Optional[bool] = field(default=False, metadata={"help": "do not sync gradients between workers"})
-    lion_wire: Optional[str] = field(default="a2a")
     synthetic_samples: Optional[int] = field(default=20000)
     model_overrides: Optional[str] = field(default=None, metadata={"help": "config overrides, e.g. num_hidden_layers=4"})
     torch_dtype: Optional[str] = field(default="bfloat16")
@@ -128,8 +132,8 @@ def create_datasets(tokenizer, script_args, seed):
 
 
 def main(argv=None):
-    parser = HfArgumentParser((ScriptArguments, TrainingArguments))
-    script_args, training_args = parser.parse_args_into_dataclasses(args=argv)
+    parser = HfArgumentParser((ScriptArguments, LionArguments, TrainingArguments))
+    script_args, lion_args, training_args = parser.parse_args_into_dataclasses(args=argv)
     logging.basicConfig(level=logging.INFO, handlers=[logging.StreamHandler(sys.stdout)])
     if getattr(training_args, "group_by_length", False) and script_args.packing:
         raise ValueError("Cannot use both packing and group by length")
@@ -137,7 +141,7 @@ def main(argv=None):
     # checkpointing because of a peft/trl issue, sft_llama2.py:58-59)
     training_args.lion = script_args.lion
     training_args.async_grad = script_args.async_grad
-    training_args.lion_wire = script_args.lion_wire
+    apply_lion_args(training_args, lion_args)  # --lion_* knobs, incl. --lion_elastic_timeout (worker dropout)
     transformers.set_seed(training_args.seed)
 
     tokenizer = load_tokenizer(script_args.model_name)

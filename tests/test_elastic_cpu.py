@@ -181,3 +181,42 @@ def test_no_dropout_elastic_equals_plain(exchange):
         assert r["same_as_plain"], "guarded vote must give the plain vote's result bit for bit"
         assert r["events"] == [] and r["world"] == 3 and r["commits"] >= 4
     assert res[0]["sum"] == 3.0
+
+
+def _sft_corpus(tmp_path, n):
+    rows = [{"question": f"q{i:04d} " + "what is this " * 3, "response_j": "an answer " * 8,
+             "response_k": "other " * 8} for i in range(n)]
+    path = tmp_path / "sft.jsonl"
+    path.write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    return str(path)
+
+
+@pytest.mark.parametrize("script", ["sft", "dpo"])
+def test_sft_and_dpo_survive_a_dropout(tmp_path, script):
+    """the SFT / DPO entrypoints take the full --lion_*
+    flag set, --lion_elastic_timeout included; a 2-rank gloo run under the
+    launcher loses rank 1 inside backward and the survivor finishes, saves and
+    logs world_end = 1."""
+    out = str(tmp_path / script)
+    common = ["--lion", "--async_grad", "--lion_elastic_timeout", "20", "--lion_beta1", "0.95",
+              "--lion_tie_break", "negative", "--lion_wire", "a2a", "--output_dir", out, "--max_steps", "4",
+              "--logging_steps", "1", "--per_device_train_batch_size", "2", "--report_to", "none", "--use_cpu",
+              "--ddp_backend", "gloo"]
+    if script == "sft":
+        args = ["sft_llama2.py", "--model_name", "llama-tiny", "--dataset_name", _sft_corpus(tmp_path, 200),
+                "--seq_length", "64", "--size_valid_set", "10", "--shuffle_buffer", "50",
+                "--save_strategy", "no", "--gradient_accumulation_steps", "1"] + common
+    else:
+        args = ["dpo_llama2.py", "--model_name_or_path", "llama-tiny", "--synthetic_samples", "64",
+                "--max_length", "400", "--max_prompt_length", "200", "--gradient_accumulation_steps", "1",
+                "--eval_steps", "0", "--save_steps", "100", "--warmup_steps", "1",
+                "--checkpointing_policy", "reference", "--gradient_checkpointing", "false"] + common
+    r = _launch(2, args, env_extra={"DLION_FAULT": "1:2:backward"})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-4000:]
+    recs = [json.loads(x) for x in open(os.path.join(out, "metrics.jsonl"))]
+    last = [x for x in recs if "world_end" in x]
+    assert last and last[-1]["world_end"] == 1.0, recs[-3:]
+    lion = [x["lion"] for x in recs if "lion" in x]
+    assert lion[-1]["world"] == 1 and lion[-1]["dropout_events"][0]["dropped"] == [1]
+    assert max(x["step"] for x in recs if "loss" in x) == 4
+    assert os.path.isdir(os.path.join(out, "final_checkpoint"))

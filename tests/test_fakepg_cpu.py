@@ -180,3 +180,60 @@ def test_auto_buckets_pipeline_gpt2_at_w_gt_1():
     # host-side collectives (gloo): the fewest buckets; an explicit size still wins
     assert opt._bucket_bytes(entries, 8, backend="gloo") == 32 << 20
     assert Lion(ps, bucket_mb=2.0)._bucket_bytes(entries, 8, backend="gloo") == 2 << 20
+
+
+def _clm_buckets(q, world):
+    """run_clm's own argument parsing + build_lion on a 2-rank fake group:
+    the default (automatic) bucket size at GPT-2 small."""
+    try:
+        import os
+        import sys
+
+        import torch.distributed as dist
+        from torch.testing._internal.distributed.fake_pg import FakeStore
+
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import run_clm
+        from distributed_lion_pytorch_amd.models.gpt2 import GPT2LMHeadModel, gpt2_config
+        from transformers import HfArgumentParser
+
+        torch.set_num_threads(2)
+        dist.init_process_group("fake", store=FakeStore(), rank=1, world_size=world)
+        parser = HfArgumentParser((run_clm.ModelArguments, run_clm.DataTrainingArguments,
+                                   run_clm.AsyncTrainingArguments))
+        _, _, targs = parser.parse_args_into_dataclasses(
+            args=["--output_dir", "/tmp/unused", "--use_cpu", "--lion", "--async_grad", "--report_to", "none"])
+        model = GPT2LMHeadModel(gpt2_config("gpt2")).to(torch.bfloat16)
+        opt = run_clm.build_lion(model, targs)
+        opt.backend = "torch"
+        opt.verify_consistency = False
+        for p in model.parameters():
+            p.grad = torch.zeros_like(p)
+        opt.step()
+        plan = opt.plan
+        q.put(("ok", {"default_bucket_mb": targs.lion_bucket_mb, "buckets": [b.nbytes for b in plan.buckets],
+                      "backend": dist.get_backend()}))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - reported to the parent
+        q.put(("err", traceback.format_exc()))
+
+
+def test_run_clm_default_buckets_pipeline_at_w2():
+    """the HF entrypoints used to pin 32 MB buckets (GPT-2
+    went out as ONE bucket and never pipelined at W > 1).  With the default
+    (automatic) size, run_clm's Lion splits GPT-2 small into >= 4 buckets on a
+    non-gloo backend."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_clm_buckets, args=(q, 2))
+    p.start()
+    try:
+        status, out = q.get(timeout=300)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert status == "ok", out
+    assert out["default_bucket_mb"] is None and out["backend"] != "gloo"
+    assert len(out["buckets"]) >= 4, out["buckets"]
+    assert max(out["buckets"]) <= 32 << 20
