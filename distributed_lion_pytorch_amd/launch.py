@@ -40,6 +40,8 @@ from typing import List, Optional, Sequence
 
 DEATH_KEY = "dlion/dead"  # parallel/elastic.py reads these (kept in sync by test_elastic_cpu)
 DEATH_COUNT_KEY = "dlion/dead_count"
+# seconds the ranks get to exit on their own after a forwarded SIGTERM / SIGINT
+SIGNAL_GRACE_S = float(os.environ.get("DLION_LAUNCH_GRACE_S", "10"))
 
 
 def _free_port(host: str) -> int:
@@ -73,14 +75,25 @@ def run(cmd: Sequence[str], nproc: int, max_failures: int = 0, host: str = "127.
     # must not orphan rank processes holding GPUs: forward the signal, then
     # terminate / kill whatever is left (finally block)
     prev = {}
+    signalled = []
+
+    def _foreground_sigint() -> bool:
+        # Ctrl-C at a terminal already reached every process of the foreground
+        # group, the ranks included (they inherit the launcher's group)
+        try:
+            return os.tcgetpgrp(sys.stdin.fileno()) == os.getpgrp()
+        except (OSError, ValueError, AttributeError):
+            return False
 
     def _forward(signum, _frame):
-        for q in procs:
-            if q.poll() is None:
-                try:
-                    q.send_signal(signum)
-                except OSError:
-                    pass
+        signalled.append(signum)
+        if not (signum == signal.SIGINT and _foreground_sigint()):
+            for q in procs:
+                if q.poll() is None:
+                    try:
+                        q.send_signal(signum)
+                    except OSError:
+                        pass
         raise KeyboardInterrupt if signum == signal.SIGINT else SystemExit(128 + signum)
 
     for sig in (signal.SIGTERM, signal.SIGINT):
@@ -117,6 +130,13 @@ def run(cmd: Sequence[str], nproc: int, max_failures: int = 0, host: str = "127.
         for sig, h in prev.items():
             signal.signal(sig, h)
         live = [q for q in procs if q.poll() is None]
+        if signalled:
+            # the ranks got the signal: let them shut down on their own first
+            # (flush a checkpoint, abort their process groups) before SIGTERM
+            grace = time.monotonic() + SIGNAL_GRACE_S
+            while live and time.monotonic() < grace:
+                time.sleep(0.05)
+                live = [q for q in live if q.poll() is None]
         for q in live:
             q.terminate()
         deadline = time.monotonic() + 10.0

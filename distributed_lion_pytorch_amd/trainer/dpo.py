@@ -96,7 +96,9 @@ class DPOTrainer(Trainer):
         super().__init__(model=model, args=args, train_dataset=train_dataset, eval_dataset=eval_dataset,
                          processing_class=tok, data_collator=DPOCollator(tok, max_length, max_prompt_length),
                          **kwargs)
-        self._reward_acc = None  # device [chosen, rejected, accuracy, margin, micro-batches] since the last log
+        # device [chosen, rejected, accuracy, margin, micro-batches] since the last log, kept apart for
+        # training and evaluation batches (trl reports them as rewards/* and eval_rewards/*)
+        self._reward_acc = {"train": None, "eval": None}
         self.tokens_seen = 0  # training tokens through the policy (chosen + rejected, padded), host-side count
 
     _REWARD_KEYS = ("rewards/chosen", "rewards/rejected", "rewards/accuracies", "rewards/margins")
@@ -119,22 +121,30 @@ class DPOTrainer(Trainer):
         # log() reads the window's means with one transfer
         stats = torch.stack([r_c.float().mean(), r_r.float().mean(), (r_c > r_r).float().mean(),
                              (r_c - r_r).float().mean(), torch.ones((), device=r_c.device)])
-        self._reward_acc = stats if self._reward_acc is None else self._reward_acc + stats
+        split = "train" if model.training else "eval"
+        acc = self._reward_acc[split]
+        self._reward_acc[split] = stats if acc is None else acc + stats
         return (loss, {"loss": loss}) if return_outputs else loss
 
-    def reward_stats(self, reset: bool = True) -> Dict[str, float]:
-        """Means of the reward statistics over the micro-batches since the last
-        call (one device-to-host copy)."""
-        if self._reward_acc is None:
+    def reward_stats(self, reset: bool = True, split: str = "train") -> Dict[str, float]:
+        """Means of the reward statistics of ``split`` ("train" / "eval") over
+        the micro-batches since the last call (one device-to-host copy); eval
+        keys carry trl's ``eval_`` prefix."""
+        acc = self._reward_acc.get(split)
+        if acc is None:
             return {}
-        v = self._reward_acc.tolist()
+        v = acc.tolist()
         if reset:
-            self._reward_acc = None
+            self._reward_acc[split] = None
         n = max(v[4], 1.0)
-        return {k: x / n for k, x in zip(self._REWARD_KEYS, v[:4])}
+        prefix = "eval_" if split == "eval" else ""
+        return {prefix + k: x / n for k, x in zip(self._REWARD_KEYS, v[:4])}
 
     def log(self, logs, *args, **kwargs):
-        logs.update(self.reward_stats())
+        # an evaluation log (eval_* keys) gets the evaluation batches' statistics,
+        # a training log the training batches' -- never a mix of the two
+        is_eval = any(k.startswith("eval_") for k in logs)
+        logs.update(self.reward_stats(split="eval" if is_eval else "train"))
         return super().log(logs, *args, **kwargs)
 
 

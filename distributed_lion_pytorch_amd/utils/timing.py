@@ -63,12 +63,18 @@ class PhaseTimer:
             self._fold()
 
     def _fold(self) -> None:
-        """Move the recorded event pairs into the millisecond sums (one device
-        synchronisation every ~MAX_PENDING phases)."""
-        torch.cuda.synchronize(self.device)
+        """Move the event pairs whose end event has completed into the
+        millisecond sums -- no device synchronisation on the training path
+        (``query()`` only asks); pairs still in flight stay pending.  Events
+        complete in stream order, so the completed pairs are a prefix of each
+        list."""
         for k, v in self._events.items():
-            self._wall[k] += sum(s.elapsed_time(e) for s, e in v)
-        self._events.clear()
+            done = 0
+            while done < len(v) and v[done][1].query():
+                done += 1
+            if done:
+                self._wall[k] += sum(s.elapsed_time(e) for s, e in v[:done])
+                del v[:done]
 
     def totals_ms(self) -> Dict[str, float]:
         """Summed milliseconds per phase (synchronises the device)."""

@@ -160,3 +160,21 @@ def test_dpo_checkpointing_decision_sees_lora_and_frozen_reference(tmp_path, mon
     policy, ref = seen["trainable"]
     assert ref == 0  # the reference is frozen before the estimate
     assert 0 < policy < seen["total"][0] // 10  # only the LoRA adapters train
+
+
+def test_dpo_reward_stats_keep_train_and_eval_apart(tmp_path):
+    """evaluation batches must not be averaged into the training
+    log's rewards/* (trl logs them separately as eval_rewards/*)."""
+    import dpo_llama2
+
+    tr = dpo_llama2.main(["--model_name_or_path", "llama-tiny", "--synthetic_samples", "60", "--max_length", "512",
+                          "--max_prompt_length", "256", "--output_dir", str(tmp_path / "dpo"), "--max_steps", "2",
+                          "--per_device_train_batch_size", "2", "--gradient_accumulation_steps", "1", "--lion",
+                          "--async_grad", "--use_cpu", "--torch_dtype", "float32", "--eval_steps", "1",
+                          "--warmup_steps", "1", "--logging_steps", "1", "--final_save", "false"])
+    hist = tr.state.log_history
+    evals = [h for h in hist if "eval_loss" in h]
+    trains = [h for h in hist if "loss" in h and "eval_loss" not in h]
+    assert evals and trains
+    assert all("eval_rewards/accuracies" in h and "rewards/accuracies" not in h for h in evals), evals
+    assert all("rewards/accuracies" in h and "eval_rewards/accuracies" not in h for h in trains), trains

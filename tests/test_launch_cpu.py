@@ -42,3 +42,33 @@ def test_sigterm_to_launcher_stops_every_rank(tmp_path):
     assert rc != 0
     time.sleep(0.2)
     assert not any(_alive(x) for x in pids), pids
+
+
+def test_ranks_get_one_signal_and_a_grace_period(tmp_path):
+    """after forwarding SIGTERM the launcher gives the ranks time
+    to shut down on their own (here: a 1 s "checkpoint flush" in the
+    handler) instead of SIGTERMing them again at once."""
+    script = tmp_path / "flusher.py"
+    script.write_text(
+        "import os, signal, time\n"
+        f"d = {str(tmp_path)!r}\n"
+        "n = [0]\n"
+        "def h(signum, frame):\n"
+        "    n[0] += 1\n"
+        "    if n[0] == 1:\n"
+        "        time.sleep(1.0)\n"
+        "        open(os.path.join(d, 'flushed' + os.environ['RANK']), 'w').write(str(n[0]))\n"
+        "        os._exit(0)\n"
+        "signal.signal(signal.SIGTERM, h)\n"
+        "open(os.path.join(d, 'pid' + os.environ['RANK']), 'w').write(str(os.getpid()))\n"
+        "time.sleep(120)\n")
+    p = subprocess.Popen([sys.executable, "-m", "distributed_lion_pytorch_amd.launch", "--nproc", "2", str(script)],
+                         cwd=ROOT)
+    deadline = time.monotonic() + 60
+    while time.monotonic() < deadline and not all((tmp_path / f"pid{r}").exists() for r in range(2)):
+        time.sleep(0.1)
+    time.sleep(0.3)
+    p.send_signal(signal.SIGTERM)
+    p.wait(timeout=30)
+    # each rank saw exactly one SIGTERM (n == 1 when it flushed) and finished its flush
+    assert [(tmp_path / f"flushed{r}").read_text() for r in range(2)] == ["1", "1"]
