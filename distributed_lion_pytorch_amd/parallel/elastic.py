@@ -63,6 +63,7 @@ import torch.distributed as dist
 log = logging.getLogger(__name__)
 
 DEFAULT_GRACE_S = 5.0
+DECISION_WAIT_S = 0.25  # slice of the blocking decision read between death-notice checks
 GLOO_DRAIN_S = 2.0  # after a failure signal: time gloo works get to fail on their own before being abandoned
 DEATH_KEY = "dlion/dead"  # + "/<rank>", in the root rendezvous store (written by ..launch)
 DEATH_COUNT_KEY = "dlion/dead_count"
@@ -168,6 +169,7 @@ class ElasticGroup:
         self._root = root
         self._dead: set = set()
         self._dead_count = 0
+        self._trash: List[str] = []  # commit keys every member has read: deleted while the host idles
 
     @classmethod
     def get(cls, timeout_s: float = 60.0, **kw) -> "ElasticGroup":
@@ -259,7 +261,10 @@ class ElasticGroup:
                             if self.backend != "gloo":
                                 return False
                             drain_until = now + GLOO_DRAIN_S
-                    time.sleep(self._poll)
+                    if self._trash:  # store housekeeping while the host would sleep anyway
+                        self._delete_keys(self._trash.pop())
+                    else:
+                        time.sleep(self._poll)
                 if drain_until is not None:  # completed after a death: do not use it
                     try:
                         w.wait()
@@ -279,7 +284,16 @@ class ElasticGroup:
     def commit(self, ok: bool) -> bool:
         """Store-arbitrated outcome of the current guarded collective: True
         when every member completed it (the result may be used), False when
-        the survivors must regroup.  Identical on every surviving rank."""
+        the survivors must regroup.  Identical on every surviving rank.
+
+        Steady state costs two store round trips on every rank and no polling
+        sleep: each member ``add``s itself to the commit's ok counter; the
+        member that completes the count writes the decision (``compare_set``:
+        the first decision written is final, so a concurrent "fail" wins or
+        loses atomically), and the others block in one ``get`` of the decision
+        key, which the store answers the moment it is written.  (Round 4 polled
+        the key every 5 ms and had the deciding rank delete old keys inline:
+        3-5 round trips plus up to 5 ms of sleep per commit.)"""
         key = f"{self.gen}/{self.seq}"
         self.seq += 1
         self.commits += 1
@@ -291,24 +305,44 @@ class ElasticGroup:
         if ok:
             if self.store.add(key + "/ok", 1) == self.world:
                 val = self.store.compare_set(dec, "", "all")
-                if val == b"all" and self.seq > 2:  # everybody is past seq-2: drop its keys
-                    old = f"{self.gen}/{self.seq - 3}"
-                    for k in ("/ok", "/decision"):
-                        try:
-                            self.store.delete_key(old + k)
-                        except Exception:  # noqa: BLE001 - best effort
-                            pass
+                if val == b"all" and self.seq > 2:  # every member is past seq-2: its keys can go
+                    self._trash.append(f"{self.gen}/{self.seq - 3}")
                 return val == b"all"
         else:
             self.store.compare_set(dec, "", "fail")
+        return self._await_decision(dec) == b"all"
+
+    def _await_decision(self, dec: str) -> bytes:
+        """Block until the decision of ``dec`` is written (one ``get``), in
+        slices of DECISION_WAIT_S so that a member that died before adding
+        itself -- it never will -- is noticed through the death notices or
+        the deadline; then decide "fail" (first write wins)."""
         deadline = time.monotonic() + self.timeout + self.grace
-        while not self.store.check([dec]):
-            # a member that died before adding itself never will: decide now
-            if time.monotonic() > deadline or self.dead_members():
-                break
-            time.sleep(0.005)
-        val = self.store.compare_set(dec, "", "fail")
-        return val == b"all"
+        first = True
+        old = self.store.timeout
+        try:
+            while True:
+                left = deadline - time.monotonic()
+                if left <= 0 or (not first and self.dead_members()):
+                    break
+                first = False
+                # the timeout is the client's (shared with the process group's
+                # store ops): set for this get only, restored below
+                self.store.set_timeout(datetime.timedelta(seconds=min(left, DECISION_WAIT_S)))
+                try:
+                    return self.store.get(dec)
+                except RuntimeError:  # DistStoreError: not decided yet
+                    continue
+        finally:
+            self.store.set_timeout(old)
+        return self.store.compare_set(dec, "", "fail")
+
+    def _delete_keys(self, key: str) -> None:
+        for k in ("/ok", "/decision"):
+            try:
+                self.store.delete_key(key + k)
+            except Exception:  # noqa: BLE001 - best effort
+                pass
 
     # --------------------------------------------------------------- regroup
     def regroup(self, tag: Optional[dict] = None) -> None:
