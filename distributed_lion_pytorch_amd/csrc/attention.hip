@@ -182,6 +182,18 @@ __device__ __forceinline__ uint32_t mix1(uint32_t x) {
   x = __umul24(x, 0x9E3779u);
   return x ^ (x >> 16);
 }
+// drop hash v3: the pair hash of tile kt starts from a per-(row, tile) base,
+// each tile reading a different 24-bit view (rotation by 8 (kt mod 4)) of the
+// 32-bit row key: v2's base arow + 16 kt kKeyMul was linear in the tile, so
+// every row's mask was a window of one fixed sequence (rows a small multiple
+// of kKeyMul apart had shifted copies of each other's masks) and rows sharing
+// arow's low 24 bits had identical masks (CPU statistics in
+// tests/test_attention_gpu.py).  4 VALU per tile and lane.
+constexpr uint32_t kTileMul = 0x27D4EB2Fu;
+__device__ __forceinline__ uint32_t tile_base(uint32_t arow, int kt) {
+  return mix1(__builtin_amdgcn_alignbit(arow, arow, 8u * static_cast<uint32_t>(kt & 3)) ^
+              (static_cast<uint32_t>(kt) * kTileMul));
+}
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 // tm1 = (thresh16 - 32769) mod 2^16 in both halves (thresh16 >= 1)
@@ -478,8 +490,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 
   const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
   const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
-  // dropout: the row's pair base, advanced by 16 pairs per key tile
-  const uint32_t prow = drop_row(a.seed, bh, q) + static_cast<uint32_t>(2 * hf) * kKeyMul;
+  // dropout: the row key; per key tile the pair base tile_base(arow, kt) + 2hf kKeyMul
+  const uint32_t arow = drop_row(a.seed, bh, q), hoff = static_cast<uint32_t>(2 * hf) * kKeyMul;
   const uint32_t tm1 = drop_tm1(a.thresh16);
   const DmaTile<D> kd(a.k_st), vd(a.v_st);
   // tiles past `last` re-read tile `last` (valid memory); the causal mask
@@ -574,14 +586,16 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
       // applied once to O at the end)
       DLION_PRIO_ON(DLION_FWD_PRIO, 2);
 #pragma unroll
-      for (int j = 0; j < NT; ++j)
+      for (int j = 0; j < NT; ++j) {
+        const uint32_t pb = DROP ? tile_base(arow, kt + j) + hoff : 0u;
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 pf = p_frag<DROP>(s[j], s2, prow + static_cast<uint32_t>((kt + j) * 16) * kKeyMul, tm1);
+          const bf16x8 pf = p_frag<DROP>(s[j], s2, pb, tm1);
 #pragma unroll
           for (int t = 0; t < D / 32; ++t)
             oacc[t] = mfma32((DLION_ATTN_PF & 1) ? vfr[j][s2][t] : tr_frag<D>(vs_[buf][j], s2, t, lane), pf, oacc[t]);
         }
+      }
       DLION_PRIO_OFF(DLION_FWD_PRIO, 2);
     }
     vm_wait0();  // this wave's pieces of the next tiles have landed
@@ -656,7 +670,7 @@ attn_bwd_dq_kernel(AttnArgs a) {
     if (a.thresh16) dlt /= a.inv_keep;  // delta * (1-p), see the forward's lse note
     if (hf == 0 && q < a.T) const_cast<float*>(a.delta)[static_cast<int64_t>(bh) * a.T + q] = dlt;
   }
-  const uint32_t prow = drop_row(a.seed, bh, q) + static_cast<uint32_t>(2 * hf) * kKeyMul;
+  const uint32_t arow = drop_row(a.seed, bh, q), hoff = static_cast<uint32_t>(2 * hf) * kKeyMul;
   const uint32_t tm1 = drop_tm1(a.thresh16);
   f32x16 dq[D / 32];
 #pragma unroll
@@ -782,16 +796,17 @@ attn_bwd_dq_kernel(AttnArgs a) {
       }
       DLION_PRIO_ON(DLION_DQ_PRIO, 2);
 #pragma unroll
-      for (int j = 0; j < NT; ++j)
+      for (int j = 0; j < NT; ++j) {
+        const uint32_t pb = DROP ? tile_base(arow, kt0 + j) + hoff : 0u;
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 dsf = ds_frag<DROP>(s[j], dp[j], dlt, s2,
-                                           prow + static_cast<uint32_t>((kt0 + j) * 16) * kKeyMul, tm1);  // dS^T
+          const bf16x8 dsf = ds_frag<DROP>(s[j], dp[j], dlt, s2, pb, tm1);  // dS^T
 #pragma unroll
           for (int t = 0; t < D / 32; ++t)
             dq[t] = mfma32(dsf, (DLION_ATTN_PF & 1) ? kt_fr[j][s2][t] : tr_frag<D>(ks_[buf][j], s2, t, lane),
                            dq[t]);  // dQ += dS K
         }
+      }
       DLION_PRIO_OFF(DLION_DQ_PRIO, 2);
       if constexpr (DLION_DQ_STAMP) {
         const unsigned long long t = memtime();
@@ -874,7 +889,7 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_pp_kernel(AttnArgs a) {
   const int q = qtile * 32 + r, qc = min(q, a.T - 1);  // tail rows: a copy of row T-1, never stored
   const int ns = (last + 2) >> 1;                        // steps per half: key tile 2s + half
 
-  const uint32_t prow = drop_row(a.seed, bh, q) + static_cast<uint32_t>(2 * hf) * kKeyMul;
+  const uint32_t arow = drop_row(a.seed, bh, q), hoff = static_cast<uint32_t>(2 * hf) * kKeyMul;
   const uint32_t tm1 = drop_tm1(a.thresh16);
   const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
   const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
@@ -958,7 +973,7 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_pp_kernel(AttnArgs a) {
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg)
       sacc[reg] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[reg], a.scale_log2, -lse2));  // p, carries 1/(1-p)
-    const uint32_t pbase = prow + static_cast<uint32_t>(kt * 16) * kKeyMul;
+    const uint32_t pbase = DROP ? tile_base(arow, kt) + hoff : 0u;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) dsf[s2] = ds_frag<DROP>(sacc, dpacc, dlt, s2, pbase, tm1);  // dS^T
     // refill the slot step s - 1 used (last read by X(s)) with step s + NB - 1
@@ -1027,7 +1042,7 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[NB];
   constexpr int kVs = DLION_DKV_KREG == 2 ? 0 : 1;  // V's slot (K not staged at KREG = 2)
   __shared__ __attribute__((aligned(16))) LdsTile<D> kvs_[kVs + 1][4];  // [K | V][wave's key tile]
-  __shared__ __attribute__((aligned(16))) float ls_[NB][3][32];  // [buf][lse | delta | drop row key][row]
+  __shared__ __attribute__((aligned(16))) float ls_[NB][6][32];  // [buf][lse | delta | hash base of key tile 0..3][row]
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntiles = ntiles32(a.T), nbhk = a.B * a.Hkv;
   const int bhk = static_cast<int>(blockIdx.x % nbhk);
@@ -1070,7 +1085,7 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   // odd lane [other.hi, own.hi]; the row keys sit in LDS parity-interleaved.
   const uint32_t tm1 = drop_tm1(a.thresh16), sel = (key & 1) ? 0x03020706u : 0x05040100u;
   const int par2 = 2 * (key & 1);
-  const uint32_t kmix = (static_cast<uint32_t>(key) >> 1) * kKeyMul;
+  const uint32_t kmix = (static_cast<uint32_t>(key & 31) >> 1) * kKeyMul;  // pair within the key tile
   const DmaTile<D> qd(a.q_st), dd(a.o_st);
   const int nq = ntiles - first;   // query tiles per head
   const int total = group * nq;    // (head, query tile) steps, head-major
@@ -1089,10 +1104,18 @@ attn_bwd_dkv_kernel(AttnArgs a) {
       const float* src = (lane < 32 ? a.lse : a.delta) + static_cast<int64_t>(bh) * a.T +
                          min(qrow + (lane & 31), a.T - 1);
       glds4(src, &ls_[buf][0][0]);
-    } else if (DROP && w == 1 && lane < 32) {
-      // rows 4i..4i+3 stored as [4i, 4i+2, 4i+1, 4i+3]: an even lane reads the
-      // pair heads, an odd lane the pair tails, as one 8-byte read
-      ls_[buf][2][(lane & ~3) | ((lane & 1) << 1) | ((lane >> 1) & 1)] = __uint_as_float(drop_row(a.seed, bh, qrow + lane));
+    } else if (DROP && w == 1) {
+      // the hash bases of the 32 rows for the block's 4 key tiles (lane: row
+      // lane & 31, tiles 2 (lane >> 5) + {0, 1}); rows 4i..4i+3 stored as
+      // [4i, 4i+2, 4i+1, 4i+3]: an even lane reads the pair heads, an odd lane
+      // the pair tails, as one 8-byte read
+      const int row = lane & 31, slot = (row & ~3) | ((row & 1) << 1) | ((row >> 1) & 1);
+      const uint32_t ar = drop_row(a.seed, bh, qrow + row);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int tt = 2 * (lane >> 5) + u;
+        ls_[buf][2 + tt][slot] = __uint_as_float(tile_base(ar, first + tt));
+      }
     }
     if (++sq == ntiles) {
       sq = first;
@@ -1183,7 +1206,7 @@ attn_bwd_dkv_kernel(AttnArgs a) {
           const float4 lv = *reinterpret_cast<const float4*>(&ls_[buf][0][8 * g + 4 * hf]);
           const float4 dv4 = *reinterpret_cast<const float4*>(&ls_[buf][1][8 * g + 4 * hf]);
           uint2 av = make_uint2(0, 0);
-          if constexpr (DROP) av = *reinterpret_cast<const uint2*>(&ls_[buf][2][8 * g + 4 * hf + par2]);
+          if constexpr (DROP) av = *reinterpret_cast<const uint2*>(&ls_[buf][2 + w][8 * g + 4 * hf + par2]);
           const float lse_g[4] = {lv.x, lv.y, lv.z, lv.w};
           const float dl_g[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
           // this lane's hash word of row pair pi, and the neighbour's (both
@@ -1286,13 +1309,13 @@ __global__ void __launch_bounds__(512) attn_bwd_dkv_pp_kernel(AttnArgs a) {
   constexpr int kTile = 32 * D * 2;                  // bytes of one 32 x D bf16 tile
   constexpr int kKV = 2 * 4 * kTile;                 // [K | V][key tile]
   constexpr int kRing = 2 * 2 * NB * kTile;          // [Q | dO][half][slot]
-  constexpr int kLs = 2 * NB * 3 * 32 * 4;           // [half][slot][lse | delta | hash key][row]
+  constexpr int kLs = 2 * NB * 6 * 32 * 4;           // [half][slot][lse | delta | hash base of tile 0..3][row]
   constexpr int kRed = 4 * 2 * (D / 32) * 16 * 64 * 4;  // half 1's dk | dv partials
   constexpr int kAll = kKV + kRing + kLs;
   __shared__ __attribute__((aligned(16))) char smem[kAll > kRed ? kAll : kRed];
   typedef LdsTile<D> KV[2][4];
   typedef LdsTile<D> Ring[2][NB];
-  typedef float Ls[2][NB][3][32];
+  typedef float Ls[2][NB][6][32];
   KV& kv_ = *reinterpret_cast<KV*>(smem);
   Ring& qs_ = *reinterpret_cast<Ring*>(smem + kKV);
   Ring& os_ = *reinterpret_cast<Ring*>(smem + kKV + kRing / 2);
@@ -1340,10 +1363,14 @@ __global__ void __launch_bounds__(512) attn_bwd_dkv_pp_kernel(AttnArgs a) {
     if (wk == 0) {
       const float* src = (lane < 32 ? a.lse : a.delta) + static_cast<int64_t>(bh) * a.T + min(qrow + (lane & 31), a.T - 1);
       glds4(src, &ls_[half][slot][0][0]);
-    } else if (DROP && wk == 1 && lane < 32) {
-      // rows 4i..4i+3 stored as [4i, 4i+2, 4i+1, 4i+3] (see the 4-wave kernel)
-      ls_[half][slot][2][(lane & ~3) | ((lane & 1) << 1) | ((lane >> 1) & 1)] =
-          __uint_as_float(drop_row(a.seed, bh, qrow + lane));
+    } else if (DROP && wk == 1) {  // hash bases per (row, key tile), as in the 4-wave kernel
+      const int row = lane & 31, ps = (row & ~3) | ((row & 1) << 1) | ((row >> 1) & 1);
+      const uint32_t ar = drop_row(a.seed, bh, qrow + row);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int tt = 2 * (lane >> 5) + u;
+        ls_[half][slot][2 + tt][ps] = __uint_as_float(tile_base(ar, first + tt));
+      }
     }
     // next step of this half: two steps on
     sq += 2;
@@ -1356,7 +1383,7 @@ __global__ void __launch_bounds__(512) attn_bwd_dkv_pp_kernel(AttnArgs a) {
 
   const uint32_t tm1 = drop_tm1(a.thresh16), sel = (key & 1) ? 0x03020706u : 0x05040100u;
   const int par2 = 2 * (key & 1);
-  const uint32_t kmix = (static_cast<uint32_t>(key) >> 1) * kKeyMul;
+  const uint32_t kmix = (static_cast<uint32_t>(key & 31) >> 1) * kKeyMul;  // pair within the key tile
   f32x16 dk[D / 32], dv[D / 32];
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) dk[t] = dv[t] = zero16();
@@ -1407,7 +1434,7 @@ __global__ void __launch_bounds__(512) attn_bwd_dkv_pp_kernel(AttnArgs a) {
         const float4 lv = *reinterpret_cast<const float4*>(&ls_[half][slot][0][8 * g + 4 * hf]);
         const float4 dv4 = *reinterpret_cast<const float4*>(&ls_[half][slot][1][8 * g + 4 * hf]);
         uint2 av = make_uint2(0, 0);
-        if constexpr (DROP) av = *reinterpret_cast<const uint2*>(&ls_[half][slot][2][8 * g + 4 * hf + par2]);
+        if constexpr (DROP) av = *reinterpret_cast<const uint2*>(&ls_[half][slot][2 + wk][8 * g + 4 * hf + par2]);
         const float lse_g[4] = {lv.x, lv.y, lv.z, lv.w};
         const float dl_g[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
         uint32_t own[2], other[2];

@@ -990,17 +990,33 @@ def _lowbias32(x: torch.Tensor) -> torch.Tensor:
 
 def attention_dropout_keep(B: int, H: int, T: int, p: float, seed: int, device=None) -> torch.Tensor:
     """bool keep-mask [B, H, T(q), T(key)] exactly as the HIP kernels draw it
-    (csrc/attention.hip, drop hash v2): one 32-bit hash per (row, key pair),
+    (csrc/attention.hip, drop hash v3): one 32-bit hash per (row, key pair),
     the low half for the even key; a key is kept iff its half, read as a
-    signed 16-bit value, is >= thresh16 - 32768."""
+    signed 16-bit value, is >= thresh16 - 32768.  The hash of pair jj (0..15)
+    of 32-key tile kt in row (bh, q) is mix1(base + jj * kKeyMul) with a
+    per-(row, tile) base mix1(rotr(arow, 8 (kt mod 4)) ^ kt * kTileMul).  v2's
+    base was linear in the tile (arow + 16 kt kKeyMul): the rows' masks were
+    windows of ONE fixed sequence, rows whose arow differed by a small multiple
+    of kKeyMul held shifted copies of each other's masks, and since
+    mix1 reads 24 bits, rows agreeing in arow's low 24 bits (a 2^-24 birthday
+    rate: ~4 pairs among a GPT-2 layer's 12k rows per batch row) had identical
+    masks.  The rotation gives each tile a different 24-bit view of the
+    32-bit row key, so two rows coincide in every tile only if their full
+    keys do."""
     th = min(65535, int(round(p * 65536)))
     bh = torch.arange(B * H, device=device, dtype=torch.int64).view(B * H, 1, 1)
     q = torch.arange(T, device=device, dtype=torch.int64).view(1, T, 1)
     key = torch.arange(T, device=device, dtype=torch.int64).view(1, 1, T)
-    # per-(head, query) row key: full hash; per key pair: one multiply round
+
+    def mix1(x):  # v_mul_u32_u24 + xor-shift
+        x = ((x & 0xFFFFFF) * 0x9E3779) & _M32
+        return x ^ (x >> 16)
+
     arow = _lowbias32(((bh * 0x9E3779B9) & _M32) ^ ((q * 0x85EBCA6B) & _M32) ^ (seed & _M32))
-    x = ((arow + (((key >> 1) * 0xC2B2AE35) & _M32)) & 0xFFFFFF) * 0x9E3779  # v_mul_u32_u24
-    x = (x & _M32) ^ ((x & _M32) >> 16)
+    rot = ((key >> 5) & 3) * 8
+    arot = ((arow >> rot) | (arow << ((32 - rot) & 31))) & _M32
+    base = mix1(arot ^ (((key >> 5) * 0x27D4EB2F) & _M32))
+    x = mix1((base + (((key >> 1) & 15) * 0xC2B2AE35)) & _M32)
     u16 = (x >> ((key & 1) * 16)) & 0xFFFF
     s16 = u16 - ((u16 >> 15) << 16)
     return (s16 >= th - 32768).view(B, H, T, T)

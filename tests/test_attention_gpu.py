@@ -20,6 +20,26 @@ def test_dropout_mask_statistics_cpu():
         assert abs(both - 0.01) < 0.003, both
 
 
+def test_dropout_masks_of_different_rows_are_not_shifted_copies_cpu():
+    """with v2's tile-linear pair hash, every row's mask was a
+    window of one fixed 2^24-periodic sequence, so ~15 other rows per row held
+    shifted copies of it.  No 256-key window (at any even offset) may repeat
+    across the rows of a GPT-2-sized head set (random masks: P ~ 1e-22)."""
+    import torch
+
+    B, H, T = 1, 12, 1024
+    keep = fused.attention_dropout_keep(B, H, T, 0.1, seed=11).view(B * H * T, T).double()
+    g = torch.Generator().manual_seed(0)
+    v = torch.randn(1, 1, 256, generator=g, dtype=torch.float64)
+    # signature of every 256-key window at an even offset: a random projection
+    sig = torch.nn.functional.conv1d(keep.unsqueeze(1), v, stride=2).reshape(-1)
+    rows = torch.arange(B * H * T).repeat_interleave((T - 256) // 2 + 1)
+    _, inv, counts = torch.unique(sig, return_inverse=True, return_counts=True)
+    dup = counts[inv] > 1
+    # the only repeats allowed are rows too short to be random (none here)
+    assert int(dup.sum()) == 0, f"{int(dup.sum())} repeated windows, e.g. rows {rows[dup][:6].tolist()}"
+
+
 def _close(a, b, tol, floor=0.0):
     err = (a.float() - b.float()).abs().max().item()
     scale = max(b.float().abs().max().item(), floor) + 1e-6
