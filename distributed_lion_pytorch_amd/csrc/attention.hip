@@ -852,24 +852,28 @@ attn_bwd_dq_kernel(AttnArgs a) {
 }
 
 // ------------------------------------------------- backward dQ, ping-pong form
-// 8 waves = 4 query tiles x 2 halves.  Waves w and w + 4 share a SIMD and the
-// query tile 4g + w; half 0 takes the even key tiles, half 1 the odd ones, and
-// their dQ partials are summed through LDS at the end.  Each wave alternates
-// two phases, one per block barrier interval:
-//   X(s): MFMA only -- dQ += dS(s-1) K(s-1), then S(s) = K Q^T, dP(s) = V dO^T
-//   Y(s): VALU only -- p = exp2(S scale - lse), dS(s) with the dropout mask,
-//         and the LDS-DMA of step s + NB - 1's K / V tiles
+// 8 waves = 4 query tiles x 2 halves, one block per CU.  Waves w and w + 4
+// share a SIMD and the query tile 4g + w; half 0 takes the even key tiles,
+// half 1 the odd ones, and their dQ partials are summed through LDS at the
+// end.  Each wave alternates two phases, one per block barrier interval:
+//   X(s): MFMA only, every operand already in registers --
+//         dQ += dS(s-1) K(s-1), S(s) = K Q^T, dP(s) = V dO^T
+//   Y(s): the LDS reads of X(s+1)'s operands (K(s)^T fragments, K / V(s+1)
+//         row fragments) issued first, their latency under the VALU work:
+//         p = exp2(S scale - lse), dS(s) with the dropout mask; then the
+//         LDS-DMA of step s + NB - 1's K / V tiles
 // and half 1 runs one interval behind half 0, so on every SIMD one wave is in
 // its matrix phase while its partner is in its vector phase (the guide's
-// 8-wave ping-pong).  The 4-wave kernel above runs the same work as one
-// dependency chain per wave (MFMA -> exp -> MFMA) and three such waves per
-// SIMD drifted into the same phase: ~25 % of the matrix pipe and of VALU issue
-// busy (profiles/r3/pmc_attn_sq_summary.txt).  K / V stream through a
-// NB-slot ring per half; slot s % NB is refilled in Y(s) for step s + NB - 1
-// (its previous tile, step s - 1, was last read by X(s)).
+// 8-wave ping-pong).  The first ping-pong version read each MFMA's operand
+// from LDS right before it inside X (lgkmcnt(0) per MFMA): the matrix phase
+// was a chain of LDS latencies, ~2800 cycles per interval, and the kernel ran
+// 106 us against the 4-wave kernel's 85 us.  K / V stream through a NB-slot
+// ring per half: step s's slot is last read in Y(s) (K^T fragments), so Y(s+1)
+// refills it with step s + NB; the wait at the end of X(s) retires step s + 1,
+// whose row fragments Y(s) reads.
 template <int D, bool DROP>
-__global__ void __launch_bounds__(512) attn_bwd_dq_pp_kernel(AttnArgs a) {
-  constexpr int NB = 3;
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_bwd_dq_pp_kernel(AttnArgs a) {
+  constexpr int NB = 4;
   constexpr int PPW = DmaTile<D>::PPW;
   constexpr int kRing = 2 * 2 * NB * 32 * D * 2;             // bytes: [K | V][half][slot] tiles
   constexpr int kRed = 4 * (D / 32) * 16 * 64 * 4;            // bytes: half 1's dq partials
@@ -902,8 +906,6 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_pp_kernel(AttnArgs a) {
     vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[half][slot], a.T - row);
   };
   for (int s = 0; s < NB - 1 && s < ns; ++s) stage(s, s);  // first: their latency runs under the loads below
-  // step s's tiles have landed once at most the later steps' pieces are in flight
-  auto wait_step = [&](int s) { vm_wait_n(min(ns - 1 - s, NB - 2) * 2 * PPW); };
 
   bf16x8 qf[D / 16], dof[D / 16];
   float lse2 = 0.f, dlt = 0.f;
@@ -931,40 +933,65 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_pp_kernel(AttnArgs a) {
     if (a.thresh16) dlt /= a.inv_keep;  // delta * (1-p), see the forward's lse note
     if (half == 0 && hf == 0 && q < a.T) const_cast<float*>(a.delta)[static_cast<int64_t>(bh) * a.T + q] = dlt;
   }
-  // the waitcnt pass cannot see the asm DMAs: without this it defers the
-  // waits for the register loads above to their first use INSIDE the loop
-  // (vmcnt(0) at every Y phase), draining the K / V prefetch each step
+  // vmcnt(0) through the builtin: the prologue's steps have landed, and the
+  // waitcnt pass (which cannot see the asm DMAs) knows the register loads
+  // above are complete -- otherwise it defers their waits to their first use
+  // inside the loop, where a vmcnt also drains the K / V prefetch
   vm_wait0();
   f32x16 dq[D / 32];
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) dq[t] = zero16();
   f32x16 sacc, dpacc;
   bf16x8 dsf[2] = {acc_frag(zero16(), 0), acc_frag(zero16(), 0)};
+  bf16x8 ktf[2][D / 32], kr[D / 16], vr[D / 16];  // X's operands, read in the previous Y
   // The loop body is straight-line (both phases unconditional: a step past
   // the wave's diagonal is all -inf after the causal mask, so its p and dS are
   // exact zeros) -- conditional MFMA updates made hipcc copy every
   // accumulator at each branch merge (~64 v_mov_b64 per step).  Half 1 starts
   // one interval late, half 0 ends one late: equal barrier counts.
   if (half == 1) __syncthreads();
-  wait_step(0);
   __syncthreads();
-  int slot = 0, pslot = 0;  // slots of step s and s - 1 (s = 0: any landed tile, dsf is 0)
+  // X(0)'s operands: step 0's rows, and any landed K^T (dsf = 0 for "step -1")
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) {
+    kr[ks] = row_frag<D>(ks_[half][0], r, ks, hf);
+    vr[ks] = row_frag<D>(vs_[half][0], r, ks, hf);
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int t2 = 0; t2 < D / 32; ++t2) ktf[s2][t2] = tr_frag<D>(ks_[half][0], s2, t2, lane);
+  int slot = 0;  // slot of step s
   for (int s = 0; s < ns; ++s) {
     const int kt = 2 * s + half;
-    // ---- X(s): matrix phase
+    // ---- X(s): matrix phase, operands in registers
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int t2 = 0; t2 < D / 32; ++t2) dq[t2] = mfma32(dsf[s2], tr_frag<D>(ks_[half][pslot], s2, t2, lane), dq[t2]);
+      for (int t2 = 0; t2 < D / 32; ++t2) dq[t2] = mfma32(dsf[s2], ktf[s2][t2], dq[t2]);  // dQ += dS K
     sacc = zero16();
     dpacc = zero16();
 #pragma unroll
     for (int ks = 0; ks < D / 16; ++ks) {
-      sacc = mfma32(row_frag<D>(ks_[half][slot], r, ks, hf), qf[ks], sacc);     // S^T  = K Q^T
-      dpacc = mfma32(row_frag<D>(vs_[half][slot], r, ks, hf), dof[ks], dpacc);  // dP^T = V dO^T
+      sacc = mfma32(kr[ks], qf[ks], sacc);     // S^T  = K Q^T
+      dpacc = mfma32(vr[ks], dof[ks], dpacc);  // dP^T = V dO^T
     }
+    // retire step s + 1 before Y(s) reads its rows (issued in Y(s - 2): three
+    // intervals ago); only step s + 2 may still be in flight
+    if (s + 1 < ns) vm_wait_n((s + 2 < ns ? 1 : 0) * 2 * PPW);
     __syncthreads();
-    // ---- Y(s): vector phase
+    // ---- Y(s): X(s+1)'s operand reads first (step s's K^T, step s+1's rows)
+    const int nxt = slot + 1 == NB ? 0 : slot + 1;
+    const int rs = s + 1 < ns ? nxt : slot;  // past the last step: any landed tile
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int t2 = 0; t2 < D / 32; ++t2) ktf[s2][t2] = tr_frag<D>(ks_[half][slot], s2, t2, lane);
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      kr[ks] = row_frag<D>(ks_[half][rs], r, ks, hf);
+      vr[ks] = row_frag<D>(vs_[half][rs], r, ks, hf);
+    }
     if (kt >= qtile) {  // the diagonal tile, or past it: exp2(-inf) = 0
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg)
@@ -976,19 +1003,17 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_pp_kernel(AttnArgs a) {
     const uint32_t pbase = DROP ? tile_base(arow, kt) + hoff : 0u;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) dsf[s2] = ds_frag<DROP>(sacc, dpacc, dlt, s2, pbase, tm1);  // dS^T
-    // refill the slot step s - 1 used (last read by X(s)) with step s + NB - 1
-    const int nslot = slot == 0 ? NB - 1 : slot - 1;
-    if (s + NB - 1 < ns) stage(s + NB - 1, nslot);
-    pslot = slot;
-    slot = slot + 1 == NB ? 0 : slot + 1;
-    if (s + 1 < ns) wait_step(s + 1);
+    // step s - 1's slot (last read in Y(s - 1); at s = 0 the unused slot NB - 1) takes step s + NB - 1
+    const int fslot = slot == 0 ? NB - 1 : slot - 1;
+    if (s + NB - 1 < ns) stage(s + NB - 1, fslot);
+    slot = nxt;
     __syncthreads();
   }
   // X(ns): the last step's dQ
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-    for (int t2 = 0; t2 < D / 32; ++t2) dq[t2] = mfma32(dsf[s2], tr_frag<D>(ks_[half][pslot], s2, t2, lane), dq[t2]);
+    for (int t2 = 0; t2 < D / 32; ++t2) dq[t2] = mfma32(dsf[s2], ktf[s2][t2], dq[t2]);
   if (half == 0) __syncthreads();
   __syncthreads();
   // half 1's partials -> LDS -> half 0 adds, stores, and emits the bias partials
@@ -1295,16 +1320,19 @@ attn_bwd_dkv_kernel(AttnArgs a) {
 // alternately: half 0 takes the even steps, half 1 the odd ones; each wave
 // keeps partial dK / dV and half 1's are added into half 0's through LDS at
 // the end.  Phases as in attn_bwd_dq_pp_kernel:
-//   X(s): MFMA only -- dV += Pd^T dO, dK += dS^T Q of step s-1, then
-//         S = Q K^T, dP = dO V^T of step s
-//   Y(s): VALU only -- p, Pd and dS of step s (the dropout pair hash as in the
-//         4-wave kernel), the LDS-DMA of step s + NB - 1
-// with half 1 one interval behind.  The block's K / V tiles sit in LDS for the
-// whole kernel; Q / dO tiles and the 32 lse / delta / hash-key row values of
-// each step stream through a NB-slot ring per half.
+//   X(s): MFMA only, operands in registers -- dV += Pd^T dO, dK += dS^T Q of
+//         step s-1, then S = Q K^T, dP = dO V^T of step s
+//   Y(s): the LDS reads of X(s+1)'s operands (step s's Q^T / dO^T fragments,
+//         step s+1's Q / dO rows) first, then p, Pd and dS of step s (the
+//         dropout pair hash as in the 4-wave kernel) and the LDS-DMA of step
+//         s + NB - 1
+// with half 1 one interval behind.  The wave's K / V row fragments (the B
+// operands of S and dP, the same every step) stay in registers; Q / dO tiles
+// and the 32 lse / delta / hash-base row values of each step stream through a
+// NB-slot ring per half (slot schedule as in attn_bwd_dq_pp_kernel).
 template <int D, bool DROP>
-__global__ void __launch_bounds__(512) attn_bwd_dkv_pp_kernel(AttnArgs a) {
-  constexpr int NB = 3;
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_bwd_dkv_pp_kernel(AttnArgs a) {
+  constexpr int NB = 4;
   constexpr int PPW = DmaTile<D>::PPW;
   constexpr int kTile = 32 * D * 2;                  // bytes of one 32 x D bf16 tile
   constexpr int kKV = 2 * 4 * kTile;                 // [K | V][key tile]
@@ -1378,8 +1406,6 @@ __global__ void __launch_bounds__(512) attn_bwd_dkv_pp_kernel(AttnArgs a) {
   };
   for (int s = 0; s < NB - 1 && s < ns; ++s) stage(s, s);
   const int pps = 2 * PPW + (wk == 0 ? 1 : 0);  // LDS-DMA pieces per stage of this wave
-  // step s's tiles have landed once at most the later steps' pieces are in flight
-  auto wait_step = [&](int s) { vm_wait_n(min(ns - 1 - s, NB - 2) * pps); };
 
   const uint32_t tm1 = drop_tm1(a.thresh16), sel = (key & 1) ? 0x03020706u : 0x05040100u;
   const int par2 = 2 * (key & 1);
@@ -1394,28 +1420,62 @@ __global__ void __launch_bounds__(512) attn_bwd_dkv_pp_kernel(AttnArgs a) {
   // query tile of this half's step s (for the masks), advanced with the steps
   int qt = first + half, qg = 0;
   while (qt >= ntiles) { qt -= nq; ++qg; }
+  // the K / V loads and the prologue's steps have landed; the builtin also
+  // tells the waitcnt pass the register work above is complete (see dQ)
+  vm_wait0();
   if (half == 1) __syncthreads();
-  wait_step(0);
   __syncthreads();
-  int slot = 0, pslot = 0;
+  bf16x8 kreg[D / 16], vreg[D / 16];                    // this wave's key tile: S / dP B operands
+  bf16x8 qtf[2][D / 32], otf[2][D / 32], qr[D / 16], dr[D / 16];  // X's operands, read in the previous Y
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) {
+    kreg[ks] = row_frag<D>(kv_[0][wk], r, ks, hf);
+    vreg[ks] = row_frag<D>(kv_[1][wk], r, ks, hf);
+    qr[ks] = row_frag<D>(qs_[half][0], r, ks, hf);
+    dr[ks] = row_frag<D>(os_[half][0], r, ks, hf);
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t) {  // any landed tile: pf = dsf = 0 for "step -1"
+      qtf[s2][t] = tr_frag<D>(qs_[half][0], s2, t, lane);
+      otf[s2][t] = tr_frag<D>(os_[half][0], s2, t, lane);
+    }
+  int slot = 0;
   for (int s = 0; s < ns; ++s) {
-    // ---- X(s): matrix phase
+    // ---- X(s): matrix phase, operands in registers
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
       for (int t = 0; t < D / 32; ++t) {
-        dv[t] = mfma32(pf[s2], tr_frag<D>(os_[half][pslot], s2, t, lane), dv[t]);   // dV += Pd^T dO
-        dk[t] = mfma32(dsf[s2], tr_frag<D>(qs_[half][pslot], s2, t, lane), dk[t]);  // dK += dS^T Q
+        dv[t] = mfma32(pf[s2], otf[s2][t], dv[t]);   // dV += Pd^T dO
+        dk[t] = mfma32(dsf[s2], qtf[s2][t], dk[t]);  // dK += dS^T Q
       }
     sacc = zero16();
     dpacc = zero16();
 #pragma unroll
     for (int ks = 0; ks < D / 16; ++ks) {
-      sacc = mfma32(row_frag<D>(qs_[half][slot], r, ks, hf), row_frag<D>(kv_[0][wk], r, ks, hf), sacc);   // S = Q K^T
-      dpacc = mfma32(row_frag<D>(os_[half][slot], r, ks, hf), row_frag<D>(kv_[1][wk], r, ks, hf), dpacc);  // dP = dO V^T
+      sacc = mfma32(qr[ks], kreg[ks], sacc);   // S = Q K^T
+      dpacc = mfma32(dr[ks], vreg[ks], dpacc);  // dP = dO V^T
     }
+    // retire step s + 1 before Y(s) reads its rows; only step s + 2 may stay in flight
+    if (s + 1 < ns) vm_wait_n((s + 2 < ns ? 1 : 0) * pps);
     __syncthreads();
-    // ---- Y(s): vector phase
+    // ---- Y(s): X(s+1)'s operand reads first (step s's Q^T / dO^T, step s+1's rows)
+    const int nxt = slot + 1 == NB ? 0 : slot + 1;
+    const int rs = s + 1 < ns ? nxt : slot;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int t = 0; t < D / 32; ++t) {
+        qtf[s2][t] = tr_frag<D>(qs_[half][slot], s2, t, lane);
+        otf[s2][t] = tr_frag<D>(os_[half][slot], s2, t, lane);
+      }
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      qr[ks] = row_frag<D>(qs_[half][rs], r, ks, hf);
+      dr[ks] = row_frag<D>(os_[half][rs], r, ks, hf);
+    }
     const int qb = qt * 32;
     const bool live = 2 * s + half < total;
     if (!live || qt <= ktile || qb + 32 > a.T) {  // diagonal / before it (all masked), tail rows, no step
@@ -1468,14 +1528,12 @@ __global__ void __launch_bounds__(512) attn_bwd_dkv_pp_kernel(AttnArgs a) {
       pf[s2] = __builtin_bit_cast(bf16x8, pw);
       dsf[s2] = __builtin_bit_cast(bf16x8, dw);
     }
-    // refill the slot step s - 1 used (last read by X(s)) with step s + NB - 1
-    const int nslot = slot == 0 ? NB - 1 : slot - 1;
-    if (s + NB - 1 < ns) stage(s + NB - 1, nslot);
-    pslot = slot;
-    slot = slot + 1 == NB ? 0 : slot + 1;
+    // step s - 1's slot (last read in Y(s - 1); at s = 0 the unused slot NB - 1) takes step s + NB - 1
+    const int fslot = slot == 0 ? NB - 1 : slot - 1;
+    if (s + NB - 1 < ns) stage(s + NB - 1, fslot);
+    slot = nxt;
     qt += 2;
     while (qt >= ntiles) { qt -= nq; ++qg; }
-    if (s + 1 < ns) wait_step(s + 1);
     __syncthreads();
   }
   // X(ns): the last step's dV / dK
@@ -1483,8 +1541,8 @@ __global__ void __launch_bounds__(512) attn_bwd_dkv_pp_kernel(AttnArgs a) {
   for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
     for (int t = 0; t < D / 32; ++t) {
-      dv[t] = mfma32(pf[s2], tr_frag<D>(os_[half][pslot], s2, t, lane), dv[t]);
-      dk[t] = mfma32(dsf[s2], tr_frag<D>(qs_[half][pslot], s2, t, lane), dk[t]);
+      dv[t] = mfma32(pf[s2], otf[s2][t], dv[t]);
+      dk[t] = mfma32(dsf[s2], qtf[s2][t], dk[t]);
     }
   if (half == 0) __syncthreads();
   __syncthreads();
@@ -1599,14 +1657,12 @@ hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
       else hipLaunchKernelGGL((attn_bwd_dkv_kernel<64, false>), bkv, dim3(256), 0, st, a);
     }
   } else if (D == 128) {
-    // (the ping-pong dK/dV ring does not fit LDS at D = 128)
+    // (the ping-pong kernels' register-resident operands / LDS rings do not fit at D = 128)
     if (drop) {
-      if (pp_dq) hipLaunchKernelGGL((attn_bwd_dq_pp_kernel<128, true>), bq, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((attn_bwd_dq_kernel<128, true, 1>), bq, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<128, true, 1>), bq, dim3(256), 0, st, a);
       hipLaunchKernelGGL((attn_bwd_dkv_kernel<128, true>), bkv, dim3(256), 0, st, a);
     } else {
-      if (pp_dq) hipLaunchKernelGGL((attn_bwd_dq_pp_kernel<128, false>), bq, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((attn_bwd_dq_kernel<128, false, 1>), bq, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<128, false, 1>), bq, dim3(256), 0, st, a);
       hipLaunchKernelGGL((attn_bwd_dkv_kernel<128, false>), bkv, dim3(256), 0, st, a);
     }
   } else {
