@@ -40,61 +40,6 @@
 #ifndef DLION_DQ_WAVES64
 #define DLION_DQ_WAVES64 1
 #endif
-// dQ (A/B): the wave's dO rows (1) and also its Q rows (2) read from LDS per
-// tile instead of held in 16 VGPRs each for the whole kernel, leaving the
-// registers to the fragment loads (the S / dP phase otherwise waits on each
-// LDS read right before its MFMA: the fragments share one register quad)
-#ifndef DLION_DQ_OPS_LDS
-#define DLION_DQ_OPS_LDS 0
-#endif
-// dQ cycle accounting (diagnostic builds only, DLION_DQ_STAMP=1;
-// tools/attn_dq_stamps.py): s_memtime deltas per wave summed over the loop --
-// [0] wait + barrier at the top of a step, [1] S / dP MFMAs until the exp
-// results exist, [2] dS VALU + dQ MFMA issue, [3] steps computed, [4] steps
-// idle (past the wave's diagonal), [5] waves, [6] the DMA wait part of [0] -- added into g_dq_stamps with
-// vector atomics by lane 0 of every wave
-#ifndef DLION_DQ_STAMP
-#define DLION_DQ_STAMP 0
-#endif
-__device__ unsigned long long g_dq_stamps[8];
-__device__ __forceinline__ unsigned long long memtime() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-// Start stagger (A/B): the first resident round of blocks (blockIdx < 1024, ~4 per CU)
-// sleeps ((blockIdx >> 8) & 3) * DLION_ATTN_STAGGER * 64 cycles at entry, so the waves
-// that share a SIMD (one per block) start a quarter-period apart instead of in lock
-// step (all in their MFMA phase together, then all in their VALU phase); kernel
-// mask: 1 = fwd, 2 = dQ, 4 = dK/dV
-#ifndef DLION_ATTN_STAGGER
-#define DLION_ATTN_STAGGER 0
-#endif
-#ifndef DLION_STAGGER_MASK
-#define DLION_STAGGER_MASK 7
-#endif
-#define DLION_STAGGER(bit)                                                         \
-  if constexpr (DLION_ATTN_STAGGER > 0 && (DLION_STAGGER_MASK & (bit)) != 0) {     \
-    if (blockIdx.x < 1024u) {                                                      \
-      for (unsigned i_ = (blockIdx.x >> 8) & 3u; i_ > 0; --i_) __builtin_amdgcn_s_sleep(DLION_ATTN_STAGGER); \
-    }                                                                              \
-  }
-// dK/dV (A/B): the wave's K-tile row fragments (S = Q K^T's B operand, the
-// same every step) held in 16 VGPRs instead of re-read from LDS each step;
-// 2 = loaded straight from global memory, no LDS copy of K at all (16 KB of
-// LDS freed for a deeper Q / dO ring, DLION_DKV_STAGES = 3 at 3 blocks per CU)
-#ifndef DLION_DKV_KREG
-#define DLION_DKV_KREG 0
-#endif
-#ifndef DLION_DQ_NT64
-#define DLION_DQ_NT64 1
-#endif
-// DLION_ATTN_NT: O / dQ / dK / dV leave with non-temporal hints (A/B switch)
-#ifndef DLION_ATTN_NT
-#define DLION_ATTN_NT 0
-#endif
 // key tiles per barrier in the D = 64 forward
 #ifndef DLION_FWD_NT64
 #define DLION_FWD_NT64 2
@@ -102,42 +47,26 @@ __device__ __forceinline__ unsigned long long memtime() {
 #ifndef DLION_DKV_WAVES128
 #define DLION_DKV_WAVES128 1
 #endif
-// LDS ring depth of the backward kernels' streamed tiles: tile i+NB-1 is
-// staged while tile i is consumed (NB = 2: classic double buffering).  NB = 3
-// spills 34 dwords in dK/dV under the 3-wave floor (168 VGPRs) and lifts dQ
-// from 133 to 162 VGPRs: GPT-2 bench 977k (NB 3) vs 1007k (NB 2) same box
-// (profiles/r3/attn_stages_ab.txt)
+// LDS ring depth of the 4-wave backward kernels' streamed tiles: tile i+NB-1
+// is staged while tile i is consumed (NB = 2: classic double buffering).
+// NB = 3 spills 34 dwords in dK/dV under the 3-wave floor (168 VGPRs) and
+// lifts dQ from 133 to 162 VGPRs: GPT-2 bench 977k (NB 3) vs 1007k (NB 2)
+// same box (profiles/r3/attn_stages_ab.txt)
 #ifndef DLION_ATTN_STAGES
 #define DLION_ATTN_STAGES 2
 #endif
-// per-kernel overrides (A/B): the dQ kernel's K/V ring, the dK/dV kernel's Q/dO ring
-#ifndef DLION_DQ_STAGES
-#define DLION_DQ_STAGES DLION_ATTN_STAGES
-#endif
-#ifndef DLION_DKV_STAGES
-#define DLION_DKV_STAGES DLION_ATTN_STAGES
-#endif
-// LDS fragment prefetch (bit mask, A/B switch): 1 = the second MFMA phase's
-// operands (V^T for PV, K for dQ, dO / Q for dV / dK) are read into registers
-// before the softmax / dS VALU section instead of right before each MFMA;
-// 2 = the first phase's row fragments (K for QK^T, K / V for S / dP, Q / dO)
-// are all read before its MFMA chain
-#ifndef DLION_ATTN_PF
-#define DLION_ATTN_PF 0
-#endif
+// Variants measured neutral or slower and removed in round 5 (numbers in
+// docs/DESIGN.md and profiles/r4/): dQ's Q / dO rows read from LDS per tile,
+// a start stagger between co-resident blocks, dK/dV's K fragments held in
+// registers or loaded straight from global memory, two key tiles per barrier
+// in dQ, non-temporal O / dQ / dK / dV stores, per-kernel ring depths, LDS
+// fragment prefetch before the VALU section, and the dQ cycle-stamp build.
+//
 // s_setprio 1 around the first (1) / second (2) MFMA phase of each tile, per
 // kernel.  At the GPT-2 shape (interleaved, 2 rounds) the second phase at
 // priority 1 took fwd 69.3-69.9 -> 67.9-68.2 us and dK/dV 117-119 -> 115 us,
 // but dQ 85-86 -> 92 us (its dS VALU then waits behind the other waves' MFMAs)
-#ifndef DLION_FWD_PRIO
-#define DLION_FWD_PRIO 2
-#endif
-#ifndef DLION_DQ_PRIO
-#define DLION_DQ_PRIO 0
-#endif
-#ifndef DLION_DKV_PRIO
-#define DLION_DKV_PRIO 2
-#endif
+constexpr int kFwdPrio = 2, kDqPrio = 0, kDkvPrio = 2;
 #define DLION_PRIO_ON(mask, bit) if constexpr (((mask) & (bit)) != 0) __builtin_amdgcn_s_setprio(1)
 #define DLION_PRIO_OFF(mask, bit) if constexpr (((mask) & (bit)) != 0) __builtin_amdgcn_s_setprio(0)
 
@@ -239,10 +168,7 @@ __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ bf16x8 ld8(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
-__device__ __forceinline__ void st_bf16(__bf16* p, float v) {
-  if constexpr (DLION_ATTN_NT != 0) __builtin_nontemporal_store(static_cast<__bf16>(v), p);
-  else *p = static_cast<__bf16>(v);
-}
+__device__ __forceinline__ void st_bf16(__bf16* p, float v) { *p = static_cast<__bf16>(v); }
 // accumulator registers 8s..8s+7 as a bf16 operand fragment (k-step s).  The
 // k order this gives -- rows {0..3, 8..11} + 4hf (+16s) -- is the "permuted k"
 // every partner operand below is read in.
@@ -465,7 +391,6 @@ struct QBlock {
 // softmax -- measured neutral to -1 % in round 3 and were removed.)
 template <int D, bool DROP, int NT>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
-  DLION_STAGGER(1)
   __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[2][NT];
   __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[2][NT];
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
@@ -512,38 +437,14 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     if (kt + NT <= last) stage(kt + NT, buf ^ 1);  // the other buffer was last read before the previous barrier
     if (blk.active && kt <= qtile) {  // wave-uniform
       f32x16 s[NT];
-      if constexpr ((DLION_ATTN_PF & 2) != 0) {
-        bf16x8 kfr[NT][D / 16];
+      DLION_PRIO_ON(kFwdPrio, 1);
 #pragma unroll
-        for (int j = 0; j < NT; ++j)
+      for (int j = 0; j < NT; ++j) {
+        s[j] = zero16();
 #pragma unroll
-          for (int ks = 0; ks < D / 16; ++ks) kfr[j][ks] = row_frag<D>(ks_[buf][j], r, ks, hf);
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          s[j] = zero16();
-#pragma unroll
-          for (int ks = 0; ks < D / 16; ++ks) s[j] = mfma32(kfr[j][ks], qf[ks], s[j]);
-        }
-      } else {
-        DLION_PRIO_ON(DLION_FWD_PRIO, 1);
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          s[j] = zero16();
-#pragma unroll
-          for (int ks = 0; ks < D / 16; ++ks) s[j] = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), qf[ks], s[j]);
-        }
-        DLION_PRIO_OFF(DLION_FWD_PRIO, 1);
+        for (int ks = 0; ks < D / 16; ++ks) s[j] = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), qf[ks], s[j]);
       }
-      // V^T operands of this group's PV, in flight during the softmax (PF & 1)
-      bf16x8 vfr[NT][2][D / 32];
-      if constexpr ((DLION_ATTN_PF & 1) != 0) {
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-            for (int t = 0; t < D / 32; ++t) vfr[j][s2][t] = tr_frag<D>(vs_[buf][j], s2, t, lane);
-      }
+      DLION_PRIO_OFF(kFwdPrio, 1);
       if (kt + NT - 1 >= qtile) {  // the diagonal (or tiles past it) in this group: causal mask
 #pragma unroll
         for (int j = 0; j < NT; ++j)
@@ -584,7 +485,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
       l = l * alpha + xsum32(rs);
       // PV with the dropout mask on the packed bf16 P pairs (1/(1-p) is
       // applied once to O at the end)
-      DLION_PRIO_ON(DLION_FWD_PRIO, 2);
+      DLION_PRIO_ON(kFwdPrio, 2);
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const uint32_t pb = DROP ? tile_base(arow, kt + j) + hoff : 0u;
@@ -593,10 +494,10 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
           const bf16x8 pf = p_frag<DROP>(s[j], s2, pb, tm1);
 #pragma unroll
           for (int t = 0; t < D / 32; ++t)
-            oacc[t] = mfma32((DLION_ATTN_PF & 1) ? vfr[j][s2][t] : tr_frag<D>(vs_[buf][j], s2, t, lane), pf, oacc[t]);
+            oacc[t] = mfma32(tr_frag<D>(vs_[buf][j], s2, t, lane), pf, oacc[t]);
         }
       }
-      DLION_PRIO_OFF(DLION_FWD_PRIO, 2);
+      DLION_PRIO_OFF(kFwdPrio, 2);
     }
     vm_wait0();  // this wave's pieces of the next tiles have landed
     __syncthreads();
@@ -611,8 +512,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
       bf16x4 wv;
 #pragma unroll
       for (int i = 0; i < 4; ++i) wv[i] = static_cast<__bf16>(oacc[t][4 * g + i] * inv_l);
-      if constexpr (DLION_ATTN_NT != 0) __builtin_nontemporal_store(wv, reinterpret_cast<bf16x4*>(op + 32 * t + 8 * g + 4 * hf));
-      else *reinterpret_cast<bf16x4*>(op + 32 * t + 8 * g + 4 * hf) = wv;
+      *reinterpret_cast<bf16x4*>(op + 32 * t + 8 * g + 4 * hf) = wv;
     }
   // under dropout the stored row constant is lse + log2(1-p): the backward's
   // exp2(s*scale - lse') is then P/(1-p) directly, and with delta' = delta*(1-p)
@@ -622,20 +522,17 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 }
 
 // --------------------------------------------------------------- backward dQ
-// NT key tiles per barrier (see the forward).  (Round 3's software-pipelined
+// One 32-query tile per wave, key tiles streamed through a DLION_ATTN_STAGES
+// ring; NT key tiles per barrier (see the forward; dQ runs NT = 1: NT = 2 was
+// 4 % slower, profiles/r4/attn_dq_nt2_ab.txt).  (Round 3's software-pipelined
 // and sequential-NT variants measured neutral and were removed.)
 template <int D, bool DROP, int NT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? DLION_DQ_WAVES64 : 1)))
 attn_bwd_dq_kernel(AttnArgs a) {
-  DLION_STAGGER(2)
-  constexpr int NB = DLION_DQ_STAGES;
+  constexpr int NB = DLION_ATTN_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> ks_[NB][NT];
   __shared__ __attribute__((aligned(16))) LdsTile<D> vs_[NB][NT];
-  constexpr int kOps = DLION_DQ_OPS_LDS;
-  constexpr int kDoSlot = (kOps & 2) != 0 ? 1 : 0;  // dO's slot: after Q when Q is staged too
-  __shared__ __attribute__((aligned(16))) LdsTile<D> qo_[kDoSlot + 1][kOps != 0 ? 4 : 1];  // [Q | dO][wave]
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
-  const int wq = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nt = ntiles32(a.T);
   const QBlock blk(a.B * a.H, nt);
   const int bh = blk.bh, qtile = blk.qtile, last = blk.last;
@@ -650,7 +547,7 @@ attn_bwd_dq_kernel(AttnArgs a) {
     const __bf16* dop = a.dout + b * a.o_sb + static_cast<int64_t>(qc) * a.o_st + h * a.o_sh + 8 * hf;
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
-      if constexpr ((kOps & 2) == 0) qf[s] = ld8(qp + 16 * s);
+      qf[s] = ld8(qp + 16 * s);
       dof[s] = ld8(dop + 16 * s);
     }
     lse2 = a.lse[static_cast<int64_t>(bh) * a.T + qc];
@@ -688,91 +585,31 @@ attn_bwd_dq_kernel(AttnArgs a) {
       vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[buf][j], a.T - row);
     }
   };
-  if constexpr (kOps != 0) {  // the block's 4 query tiles (one per wave): landed by the loop's first wait
-    const DmaTile<D> qd(a.q_st), od(a.o_st);
-    const int g0 = qtile - wq;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = __builtin_amdgcn_readfirstlane((g0 + j) * 32);
-      if (row < a.T) {  // block-uniform
-        if constexpr ((kOps & 2) != 0)
-          qd.issue(a.q + b * a.q_sb + h * a.q_sh + static_cast<int64_t>(row) * a.q_st, qo_[0][j], a.T - row);
-        od.issue(a.dout + b * a.o_sb + h * a.o_sh + static_cast<int64_t>(row) * a.o_st, qo_[kDoSlot][j], a.T - row);
-      }
-    }
-  }
-#define DLION_DQ_QF(ks) ((kOps & 2) != 0 ? row_frag<D>(qo_[0][kOps != 0 ? wq : 0], r, ks, hf) : qf[ks])
-#define DLION_DQ_DOF(ks) ((kOps & 1) != 0 ? row_frag<D>(qo_[kDoSlot][kOps != 0 ? wq : 0], r, ks, hf) : dof[ks])
   const int ns = last / NT + 1;
   for (int j = 0; j < NB - 1 && j < ns; ++j) stage(j, j);
-  unsigned long long acc_t[6] = {0, 0, 0, 0, 0, 0}, t_mark = 0;
   for (int st = 0; st < ns; ++st) {
     const int buf = st % NB;
-    if constexpr (DLION_DQ_STAMP) t_mark = memtime();
     // super-tile st has landed once only the later ones' pieces (NT * 2 PPW each) are in flight
     vm_wait_n(min(ns - 1 - st, NB - 2) * NT * 2 * DmaTile<D>::PPW);
-    if constexpr (DLION_DQ_STAMP) {
-      const unsigned long long t = memtime();
-      acc_t[5] += t - t_mark;  // the DMA wait alone
-    }
     __syncthreads();  // ... for every wave; and every wave is done with the buffer restaged next
-    if constexpr (DLION_DQ_STAMP) {
-      const unsigned long long t = memtime();
-      acc_t[0] += t - t_mark;
-      t_mark = t;
-    }
     if (st + NB - 1 < ns) stage(st + NB - 1, (st + NB - 1) % NB);
     const int kt0 = st * NT;
-    if constexpr (DLION_DQ_STAMP) {
-      if (!(blk.active && kt0 <= qtile)) acc_t[4] += 1;
-    }
     if (blk.active && kt0 <= qtile) {
       // NT independent S / dP chains: one tile's exp / hash VALU work can sit
       // beside the other's MFMAs
       f32x16 s[NT], dp[NT];
-      if constexpr ((DLION_ATTN_PF & 2) != 0) {
-        bf16x8 kfr[NT][D / 16], vfr2[NT][D / 16];
+      DLION_PRIO_ON(kDqPrio, 1);
 #pragma unroll
-        for (int j = 0; j < NT; ++j)
+      for (int j = 0; j < NT; ++j) {
+        s[j] = zero16();
+        dp[j] = zero16();
 #pragma unroll
-          for (int ks = 0; ks < D / 16; ++ks) {
-            kfr[j][ks] = row_frag<D>(ks_[buf][j], r, ks, hf);
-            vfr2[j][ks] = row_frag<D>(vs_[buf][j], r, ks, hf);
-          }
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          s[j] = zero16();
-          dp[j] = zero16();
-#pragma unroll
-          for (int ks = 0; ks < D / 16; ++ks) {
-            s[j] = mfma32(kfr[j][ks], DLION_DQ_QF(ks), s[j]);
-            dp[j] = mfma32(vfr2[j][ks], DLION_DQ_DOF(ks), dp[j]);
-          }
+        for (int ks = 0; ks < D / 16; ++ks) {
+          s[j] = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), qf[ks], s[j]);    // S^T  = K Q^T
+          dp[j] = mfma32(row_frag<D>(vs_[buf][j], r, ks, hf), dof[ks], dp[j]);  // dP^T = V dO^T
         }
-      } else {
-        DLION_PRIO_ON(DLION_DQ_PRIO, 1);
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          s[j] = zero16();
-          dp[j] = zero16();
-#pragma unroll
-          for (int ks = 0; ks < D / 16; ++ks) {
-            s[j] = mfma32(row_frag<D>(ks_[buf][j], r, ks, hf), DLION_DQ_QF(ks), s[j]);    // S^T  = K Q^T
-            dp[j] = mfma32(row_frag<D>(vs_[buf][j], r, ks, hf), DLION_DQ_DOF(ks), dp[j]);  // dP^T = V dO^T
-          }
-        }
-        DLION_PRIO_OFF(DLION_DQ_PRIO, 1);
       }
-      // K operands of this group's dQ MFMAs, in flight during the dS VALU work (PF & 1)
-      bf16x8 kt_fr[NT][2][D / 32];
-      if constexpr ((DLION_ATTN_PF & 1) != 0) {
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-            for (int t = 0; t < D / 32; ++t) kt_fr[j][s2][t] = tr_frag<D>(ks_[buf][j], s2, t, lane);
-      }
+      DLION_PRIO_OFF(kDqPrio, 1);
       if (kt0 + NT - 1 >= qtile) {  // the diagonal (or tiles past it) in this group: exp2(-inf) = 0
 #pragma unroll
         for (int j = 0; j < NT; ++j)
@@ -785,16 +622,7 @@ attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg)
           s[j][reg] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][reg], a.scale_log2, -lse2));  // p, carries 1/(1-p)
-      if constexpr (DLION_DQ_STAMP) {
-        float any = 0.f;  // consume the exp results so the stamp lands after them
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) any += s[0][reg];
-        asm volatile("" ::"v"(any));
-        const unsigned long long t = memtime();
-        acc_t[1] += t - t_mark;
-        t_mark = t;
-      }
-      DLION_PRIO_ON(DLION_DQ_PRIO, 2);
+      DLION_PRIO_ON(kDqPrio, 2);
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const uint32_t pb = DROP ? tile_base(arow, kt0 + j) + hoff : 0u;
@@ -802,29 +630,12 @@ attn_bwd_dq_kernel(AttnArgs a) {
         for (int s2 = 0; s2 < 2; ++s2) {
           const bf16x8 dsf = ds_frag<DROP>(s[j], dp[j], dlt, s2, pb, tm1);  // dS^T
 #pragma unroll
-          for (int t = 0; t < D / 32; ++t)
-            dq[t] = mfma32(dsf, (DLION_ATTN_PF & 1) ? kt_fr[j][s2][t] : tr_frag<D>(ks_[buf][j], s2, t, lane),
-                           dq[t]);  // dQ += dS K
+          for (int t = 0; t < D / 32; ++t) dq[t] = mfma32(dsf, tr_frag<D>(ks_[buf][j], s2, t, lane), dq[t]);  // dQ += dS K
         }
       }
-      DLION_PRIO_OFF(DLION_DQ_PRIO, 2);
-      if constexpr (DLION_DQ_STAMP) {
-        const unsigned long long t = memtime();
-        acc_t[2] += t - t_mark;
-        acc_t[3] += 1;
-      }
+      DLION_PRIO_OFF(kDqPrio, 2);
     }
   }
-  if constexpr (DLION_DQ_STAMP) {
-    if (lane == 0) {
-#pragma unroll
-      for (int i = 0; i < 5; ++i) atomicAdd(&g_dq_stamps[i], acc_t[i]);
-      atomicAdd(&g_dq_stamps[5], 1ull);
-      atomicAdd(&g_dq_stamps[6], acc_t[5]);
-    }
-  }
-#undef DLION_DQ_QF
-#undef DLION_DQ_DOF
   if (!blk.active) return;
   // dq[t]: rows = q (registers), cols = d (lane)
   __bf16* base = a.dq + b * a.dq_sb + h * a.dq_sh;
@@ -1061,12 +872,10 @@ template <int D, bool DROP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     D == 64 ? DLION_DKV_WAVES64 : DLION_DKV_WAVES128)))
 attn_bwd_dkv_kernel(AttnArgs a) {
-  DLION_STAGGER(4)
-  constexpr int NB = DLION_DKV_STAGES;
+  constexpr int NB = DLION_ATTN_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> qs_[NB];
   __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[NB];
-  constexpr int kVs = DLION_DKV_KREG == 2 ? 0 : 1;  // V's slot (K not staged at KREG = 2)
-  __shared__ __attribute__((aligned(16))) LdsTile<D> kvs_[kVs + 1][4];  // [K | V][wave's key tile]
+  __shared__ __attribute__((aligned(16))) LdsTile<D> kvs_[2][4];  // [K | V][wave's key tile]
   __shared__ __attribute__((aligned(16))) float ls_[NB][6][32];  // [buf][lse | delta | hash base of key tile 0..3][row]
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntiles = ntiles32(a.T), nbhk = a.B * a.Hkv;
@@ -1089,9 +898,8 @@ attn_bwd_dkv_kernel(AttnArgs a) {
     for (int j = 0; j < 4; ++j) {
       const int row = __builtin_amdgcn_readfirstlane((first + j) * 32);
       if (row < a.T) {  // block-uniform
-        if constexpr (DLION_DKV_KREG != 2)
-          kd.issue(a.k + b * a.k_sb + hk * a.k_sh + static_cast<int64_t>(row) * a.k_st, kvs_[0][j], a.T - row);
-        vd.issue(a.v + b * a.v_sb + hk * a.v_sh + static_cast<int64_t>(row) * a.v_st, kvs_[kVs][j], a.T - row);
+        kd.issue(a.k + b * a.k_sb + hk * a.k_sh + static_cast<int64_t>(row) * a.k_st, kvs_[0][j], a.T - row);
+        vd.issue(a.v + b * a.v_sb + hk * a.v_sh + static_cast<int64_t>(row) * a.v_st, kvs_[1][j], a.T - row);
       }
     }
   }
@@ -1151,61 +959,21 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   // LDS-DMA pieces per stage: Q + dO tiles, and wave 0's lse / delta row values
   const int per_stage = 2 * DmaTile<D>::PPW + (w == 0 ? 1 : 0);
   int qt = first;  // query tile of step i
-  bf16x8 kreg[DLION_DKV_KREG ? D / 16 : 1];
-  if constexpr (DLION_DKV_KREG == 2) {  // the lane's key row, straight from global memory (tail rows: a copy of row T-1)
-    const __bf16* kp = a.k + b * a.k_sb + hk * a.k_sh + static_cast<int64_t>(min(key, a.T - 1)) * a.k_st + 8 * hf;
-#pragma unroll
-    for (int ks = 0; ks < D / 16; ++ks) kreg[ks] = ld8(kp + 16 * ks);
-  }
   for (int i = 0; i < total; ++i, qt = (qt + 1 == ntiles ? first : qt + 1)) {
     const int buf = i % NB;
     vm_wait_n(min(total - 1 - i, NB - 2) * per_stage);  // step i landed (later steps may be in flight)
     __syncthreads();  // for every wave; and every wave is done with the buffer restaged next
     if (i + NB - 1 < total) stage_next((i + NB - 1) % NB);
-    if constexpr (DLION_DKV_KREG == 1) {
-      if (i == 0) {  // the K / V tiles landed with step 0's wait
-#pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) kreg[ks] = row_frag<D>(kvs_[0][w], r, ks, hf);
-      }
-    }
     if (active && qt >= ktile) {  // wave-uniform
       const int qb = qt * 32;
       f32x16 s = zero16(), dp = zero16();
-      if constexpr ((DLION_ATTN_PF & 2) != 0) {
-        bf16x8 qa[D / 16], kb_[D / 16], da[D / 16], vb[D / 16];
+      DLION_PRIO_ON(kDkvPrio, 1);
 #pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          qa[ks] = row_frag<D>(qs_[buf], r, ks, hf);
-          kb_[ks] = DLION_DKV_KREG ? kreg[DLION_DKV_KREG ? ks : 0] : row_frag<D>(kvs_[0][w], r, ks, hf);
-          da[ks] = row_frag<D>(ds_[buf], r, ks, hf);
-          vb[ks] = row_frag<D>(kvs_[kVs][w], r, ks, hf);
-        }
-#pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          s = mfma32(qa[ks], kb_[ks], s);
-          dp = mfma32(da[ks], vb[ks], dp);
-        }
-      } else {
-        DLION_PRIO_ON(DLION_DKV_PRIO, 1);
-#pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          s = mfma32(row_frag<D>(qs_[buf], r, ks, hf),
-                     DLION_DKV_KREG ? kreg[DLION_DKV_KREG ? ks : 0] : row_frag<D>(kvs_[0][w], r, ks, hf), s);  // S = Q K^T
-          dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), row_frag<D>(kvs_[kVs][w], r, ks, hf), dp);  // dP = dO V^T
-        }
-        DLION_PRIO_OFF(DLION_DKV_PRIO, 1);
+      for (int ks = 0; ks < D / 16; ++ks) {
+        s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), row_frag<D>(kvs_[0][w], r, ks, hf), s);   // S = Q K^T
+        dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), row_frag<D>(kvs_[1][w], r, ks, hf), dp);  // dP = dO V^T
       }
-      // dO^T / Q^T operands of dV / dK, in flight during the dS VALU work (PF & 1)
-      bf16x8 dtr[2][D / 32], qtr[2][D / 32];
-      if constexpr ((DLION_ATTN_PF & 1) != 0) {
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int t = 0; t < D / 32; ++t) {
-            dtr[s2][t] = tr_frag<D>(ds_[buf], s2, t, lane);
-            qtr[s2][t] = tr_frag<D>(qs_[buf], s2, t, lane);
-          }
-      }
+      DLION_PRIO_OFF(kDkvPrio, 1);
       if (qt == ktile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg)
@@ -1267,16 +1035,16 @@ attn_bwd_dkv_kernel(AttnArgs a) {
         }
         const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);
         const bf16x8 dsf = __builtin_bit_cast(bf16x8, dw);
-        DLION_PRIO_ON(DLION_DKV_PRIO, 2);
+        DLION_PRIO_ON(kDkvPrio, 2);
 #pragma unroll
         for (int t = 0; t < D / 32; ++t) {
-          dv[t] = mfma32(pf, (DLION_ATTN_PF & 1) ? dtr[s2][t] : tr_frag<D>(ds_[buf], s2, t, lane), dv[t]);   // dV += Pd^T dO
-          dk[t] = mfma32(dsf, (DLION_ATTN_PF & 1) ? qtr[s2][t] : tr_frag<D>(qs_[buf], s2, t, lane), dk[t]);  // dK += dS^T Q
+          dv[t] = mfma32(pf, tr_frag<D>(ds_[buf], s2, t, lane), dv[t]);   // dV += Pd^T dO
+          dk[t] = mfma32(dsf, tr_frag<D>(qs_[buf], s2, t, lane), dk[t]);  // dK += dS^T Q
         }
-        DLION_PRIO_OFF(DLION_DKV_PRIO, 2);
+        DLION_PRIO_OFF(kDkvPrio, 2);
         // keep the second fragment's LDS reads from being hoisted above this
         // point (their registers pushed the kernel past 168 VGPRs: spills)
-        if constexpr ((DLION_ATTN_PF & 1) == 0) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
@@ -1598,15 +1366,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   }
 }
 
-// dQ cycle accounting readout (DLION_DQ_STAMP builds): copy out, optionally reset
-hipError_t attn_dq_stamps(unsigned long long* host8, bool reset) {
-  hipError_t e = hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_dq_stamps), sizeof(unsigned long long) * 8, 0,
-                                     hipMemcpyDeviceToHost);
-  if (e != hipSuccess || !reset) return e;
-  const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_dq_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
-}
-
 // ------------------------------------------------------------------ launchers
 // ceil(tiles / 4) blocks of 4 waves per head
 static inline int64_t tile_blocks(int64_t nbh, int T) { return nbh * ((((T + 31) >> 5) + 3) >> 2); }
@@ -1647,12 +1406,12 @@ hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
   if (D == 64) {
     if (drop) {
       if (pp_dq) hipLaunchKernelGGL((attn_bwd_dq_pp_kernel<64, true>), bq, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, true, DLION_DQ_NT64>), bq, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, true, 1>), bq, dim3(256), 0, st, a);
       if (pp_dkv) hipLaunchKernelGGL((attn_bwd_dkv_pp_kernel<64, true>), bkv, dim3(512), 0, st, a);
       else hipLaunchKernelGGL((attn_bwd_dkv_kernel<64, true>), bkv, dim3(256), 0, st, a);
     } else {
       if (pp_dq) hipLaunchKernelGGL((attn_bwd_dq_pp_kernel<64, false>), bq, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, false, DLION_DQ_NT64>), bq, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, false, 1>), bq, dim3(256), 0, st, a);
       if (pp_dkv) hipLaunchKernelGGL((attn_bwd_dkv_pp_kernel<64, false>), bkv, dim3(512), 0, st, a);
       else hipLaunchKernelGGL((attn_bwd_dkv_kernel<64, false>), bkv, dim3(256), 0, st, a);
     }

@@ -1093,11 +1093,6 @@ TORCH_LIBRARY(dlion, m) {
   m.def("vote_reduce(Tensor recv, int nbytes, Tensor alive, int tie, Tensor(a!) out, Tensor(b!)? neg_out,"
         " Tensor(c!)? ties=None) -> ()");
   // persistent NT GEMM switch (A/B); returns the previous setting
-  m.def("attn_dq_stamps(bool reset) -> int[]", [](bool reset) -> std::vector<int64_t> {
-    unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    check_hip(dlion::attn_dq_stamps(h, reset), "attn_dq_stamps");
-    return std::vector<int64_t>(h, h + 8);
-  });
   m.def("set_gemm_persist(int on) -> int", [](int64_t on) -> int64_t {
     const int prev = dlion::gemm_persist_enabled();
     dlion::set_gemm_persist(static_cast<int>(on));

@@ -75,8 +75,6 @@ hipError_t launch_sum_partials_split(const float* const* ptrs, const int64_t* ro
 // and the part column sums of 4 (no bias).
 // Needs K % 128 == 0, N % 8 == 0, leading dims % 8 == 0.
 void set_gemm_persist(int on);
-// dQ cycle accounting of DLION_DQ_STAMP builds (zeros otherwise): 8 counters, optional reset
-hipError_t attn_dq_stamps(unsigned long long* host8, bool reset);
 int gemm_persist_enabled();
 hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
                           void* aux, int ldaux, int M, int N, int K, int epi, float* part, hipStream_t st);
