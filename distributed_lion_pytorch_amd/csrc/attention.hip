@@ -334,9 +334,8 @@ struct DmaTile {
   int off0, off1, lds;  // source element offsets (tile-relative) of the lane's chunks; wave's LDS byte offset
   uint32_t boff0, boff1;  // the same as byte offsets (scalar-base DMA)
   int r0, r1, c0, c1, st;  // the lane's tile rows / swizzled chunk offsets, for partial (tail) tiles
-  // `wave` = the issuing wave's index among the 4 that share the tile (default: its block index)
-  __device__ __forceinline__ DmaTile(int64_t stride, int wave = -1) {
-    const int w = wave >= 0 ? wave : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  __device__ __forceinline__ DmaTile(int64_t stride) {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int p0 = 64 * PPW * w + lane, p1 = p0 + 64;
     r0 = p0 / CPR;
     r1 = p1 / CPR;
@@ -662,207 +661,6 @@ attn_bwd_dq_kernel(AttnArgs a) {
   }
 }
 
-// ------------------------------------------------- backward dQ, ping-pong form
-// 8 waves = 4 query tiles x 2 halves, one block per CU.  Waves w and w + 4
-// share a SIMD and the query tile 4g + w; half 0 takes the even key tiles,
-// half 1 the odd ones, and their dQ partials are summed through LDS at the
-// end.  Each wave alternates two phases, one per block barrier interval:
-//   X(s): MFMA only, every operand already in registers --
-//         dQ += dS(s-1) K(s-1), S(s) = K Q^T, dP(s) = V dO^T
-//   Y(s): the LDS reads of X(s+1)'s operands (K(s)^T fragments, K / V(s+1)
-//         row fragments) issued first, their latency under the VALU work:
-//         p = exp2(S scale - lse), dS(s) with the dropout mask; then the
-//         LDS-DMA of step s + NB - 1's K / V tiles
-// and half 1 runs one interval behind half 0, so on every SIMD one wave is in
-// its matrix phase while its partner is in its vector phase (the guide's
-// 8-wave ping-pong).  The first ping-pong version read each MFMA's operand
-// from LDS right before it inside X (lgkmcnt(0) per MFMA): the matrix phase
-// was a chain of LDS latencies, ~2800 cycles per interval, and the kernel ran
-// 106 us against the 4-wave kernel's 85 us.  K / V stream through a NB-slot
-// ring per half: step s's slot is last read in Y(s) (K^T fragments), so Y(s+1)
-// refills it with step s + NB; the wait at the end of X(s) retires step s + 1,
-// whose row fragments Y(s) reads.
-template <int D, bool DROP>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_bwd_dq_pp_kernel(AttnArgs a) {
-  constexpr int NB = 4;
-  constexpr int PPW = DmaTile<D>::PPW;
-  constexpr int kRing = 2 * 2 * NB * 32 * D * 2;             // bytes: [K | V][half][slot] tiles
-  constexpr int kRed = 4 * (D / 32) * 16 * 64 * 4;            // bytes: half 1's dq partials
-  __shared__ __attribute__((aligned(16))) char smem[kRing > kRed ? kRing : kRed];
-  typedef LdsTile<D> Ring[2][NB];
-  Ring& ks_ = *reinterpret_cast<Ring*>(smem);
-  Ring& vs_ = *reinterpret_cast<Ring*>(smem + kRing / 2);
-  const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int half = wv >> 2, wq = wv & 3;
-  const int nt = ntiles32(a.T), nbh = a.B * a.H;
-  const int bh = static_cast<int>(blockIdx.x % nbh);
-  const int grp = ((nt + 3) >> 2) - 1 - static_cast<int>(blockIdx.x / nbh);  // heavy (late) query groups first
-  const int qtile = grp * 4 + wq, last = min(grp * 4 + 3, nt - 1);
-  const bool active = qtile < nt;
-  const int b = bh / a.H, h = bh % a.H, hk = h / (a.H / a.Hkv);
-  const int q = qtile * 32 + r, qc = min(q, a.T - 1);  // tail rows: a copy of row T-1, never stored
-  const int ns = (last + 2) >> 1;                        // steps per half: key tile 2s + half
-
-  const uint32_t arow = drop_row(a.seed, bh, q), hoff = static_cast<uint32_t>(2 * hf) * kKeyMul;
-  const uint32_t tm1 = drop_tm1(a.thresh16);
-  const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
-  const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
-  const DmaTile<D> kd(a.k_st, wq), vd(a.v_st, wq);
-  // step s of this half = key tile 2s + half; past `last` it re-reads tile
-  // `last` (valid memory), and the causal mask zeroes its contribution
-  auto stage = [&](int s, int slot) {
-    const int row = __builtin_amdgcn_readfirstlane(min(2 * s + half, last) * 32);
-    kd.issue(kg + static_cast<int64_t>(row) * a.k_st, ks_[half][slot], a.T - row);
-    vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[half][slot], a.T - row);
-  };
-  for (int s = 0; s < NB - 1 && s < ns; ++s) stage(s, s);  // first: their latency runs under the loads below
-
-  bf16x8 qf[D / 16], dof[D / 16];
-  float lse2 = 0.f, dlt = 0.f;
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) qf[s] = dof[s] = acc_frag(zero16(), 0);  // inactive waves: finite zeros
-  if (active) {
-    const __bf16* qp = a.q + b * a.q_sb + static_cast<int64_t>(qc) * a.q_st + h * a.q_sh + 8 * hf;
-    const __bf16* dop = a.dout + b * a.o_sb + static_cast<int64_t>(qc) * a.o_st + h * a.o_sh + 8 * hf;
-    const __bf16* op = a.o + b * a.o_sb + static_cast<int64_t>(qc) * a.o_st + h * a.o_sh + 8 * hf;
-    bf16x8 of[D / 16];
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s) {
-      qf[s] = ld8(qp + 16 * s);
-      dof[s] = ld8(dop + 16 * s);
-      of[s] = ld8(op + 16 * s);
-    }
-    lse2 = a.lse[static_cast<int64_t>(bh) * a.T + qc];
-    // delta = rowsum(dO * O), published for the dKV kernel by half 0
-    float part = 0.f;
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) part += static_cast<float>(of[s][j]) * static_cast<float>(dof[s][j]);
-    dlt = xsum32(part);
-    if (a.thresh16) dlt /= a.inv_keep;  // delta * (1-p), see the forward's lse note
-    if (half == 0 && hf == 0 && q < a.T) const_cast<float*>(a.delta)[static_cast<int64_t>(bh) * a.T + q] = dlt;
-  }
-  // vmcnt(0) through the builtin: the prologue's steps have landed, and the
-  // waitcnt pass (which cannot see the asm DMAs) knows the register loads
-  // above are complete -- otherwise it defers their waits to their first use
-  // inside the loop, where a vmcnt also drains the K / V prefetch
-  vm_wait0();
-  f32x16 dq[D / 32];
-#pragma unroll
-  for (int t = 0; t < D / 32; ++t) dq[t] = zero16();
-  f32x16 sacc, dpacc;
-  bf16x8 dsf[2] = {acc_frag(zero16(), 0), acc_frag(zero16(), 0)};
-  bf16x8 ktf[2][D / 32], kr[D / 16], vr[D / 16];  // X's operands, read in the previous Y
-  // The loop body is straight-line (both phases unconditional: a step past
-  // the wave's diagonal is all -inf after the causal mask, so its p and dS are
-  // exact zeros) -- conditional MFMA updates made hipcc copy every
-  // accumulator at each branch merge (~64 v_mov_b64 per step).  Half 1 starts
-  // one interval late, half 0 ends one late: equal barrier counts.
-  if (half == 1) __syncthreads();
-  __syncthreads();
-  // X(0)'s operands: step 0's rows, and any landed K^T (dsf = 0 for "step -1")
-#pragma unroll
-  for (int ks = 0; ks < D / 16; ++ks) {
-    kr[ks] = row_frag<D>(ks_[half][0], r, ks, hf);
-    vr[ks] = row_frag<D>(vs_[half][0], r, ks, hf);
-  }
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-    for (int t2 = 0; t2 < D / 32; ++t2) ktf[s2][t2] = tr_frag<D>(ks_[half][0], s2, t2, lane);
-  int slot = 0;  // slot of step s
-  for (int s = 0; s < ns; ++s) {
-    const int kt = 2 * s + half;
-    // ---- X(s): matrix phase, operands in registers
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int t2 = 0; t2 < D / 32; ++t2) dq[t2] = mfma32(dsf[s2], ktf[s2][t2], dq[t2]);  // dQ += dS K
-    sacc = zero16();
-    dpacc = zero16();
-#pragma unroll
-    for (int ks = 0; ks < D / 16; ++ks) {
-      sacc = mfma32(kr[ks], qf[ks], sacc);     // S^T  = K Q^T
-      dpacc = mfma32(vr[ks], dof[ks], dpacc);  // dP^T = V dO^T
-    }
-    // retire step s + 1 before Y(s) reads its rows (issued in Y(s - 2): three
-    // intervals ago); only step s + 2 may still be in flight
-    if (s + 1 < ns) vm_wait_n((s + 2 < ns ? 1 : 0) * 2 * PPW);
-    __syncthreads();
-    // ---- Y(s): X(s+1)'s operand reads first (step s's K^T, step s+1's rows)
-    const int nxt = slot + 1 == NB ? 0 : slot + 1;
-    const int rs = s + 1 < ns ? nxt : slot;  // past the last step: any landed tile
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int t2 = 0; t2 < D / 32; ++t2) ktf[s2][t2] = tr_frag<D>(ks_[half][slot], s2, t2, lane);
-#pragma unroll
-    for (int ks = 0; ks < D / 16; ++ks) {
-      kr[ks] = row_frag<D>(ks_[half][rs], r, ks, hf);
-      vr[ks] = row_frag<D>(vs_[half][rs], r, ks, hf);
-    }
-    if (kt >= qtile) {  // the diagonal tile, or past it: exp2(-inf) = 0
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg)
-        if (kt * 32 + acc_row(reg, hf) > q) sacc[reg] = -INFINITY;
-    }
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg)
-      sacc[reg] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[reg], a.scale_log2, -lse2));  // p, carries 1/(1-p)
-    const uint32_t pbase = DROP ? tile_base(arow, kt) + hoff : 0u;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) dsf[s2] = ds_frag<DROP>(sacc, dpacc, dlt, s2, pbase, tm1);  // dS^T
-    // step s - 1's slot (last read in Y(s - 1); at s = 0 the unused slot NB - 1) takes step s + NB - 1
-    const int fslot = slot == 0 ? NB - 1 : slot - 1;
-    if (s + NB - 1 < ns) stage(s + NB - 1, fslot);
-    slot = nxt;
-    __syncthreads();
-  }
-  // X(ns): the last step's dQ
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-    for (int t2 = 0; t2 < D / 32; ++t2) dq[t2] = mfma32(dsf[s2], ktf[s2][t2], dq[t2]);
-  if (half == 0) __syncthreads();
-  __syncthreads();
-  // half 1's partials -> LDS -> half 0 adds, stores, and emits the bias partials
-  float* red = reinterpret_cast<float*>(smem) + wq * ((D / 32) * 16 * 64);
-  if (half == 1) {
-#pragma unroll
-    for (int t2 = 0; t2 < D / 32; ++t2)
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) red[(t2 * 16 + reg) * 64 + lane] = dq[t2][reg];
-  }
-  __syncthreads();
-  if (half == 1 || !active) return;
-#pragma unroll
-  for (int t2 = 0; t2 < D / 32; ++t2)
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) dq[t2][reg] += red[(t2 * 16 + reg) * 64 + lane];
-  __bf16* base = a.dq + b * a.dq_sb + h * a.dq_sh;
-#pragma unroll
-  for (int t2 = 0; t2 < D / 32; ++t2)
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int qq = qtile * 32 + acc_row(reg, hf);
-      if (qq < a.T) st_bf16(base + static_cast<int64_t>(qq) * a.dq_st + 32 * t2 + r, dq[t2][reg] * a.scale);
-    }
-  if (a.colsum != nullptr) {  // c_attn bias-gradient partials (see attn_bwd_dq_kernel)
-    float* cs = a.colsum + static_cast<int64_t>(b * nt + qtile) * (3 * a.H * D) + h * D;
-#pragma unroll
-    for (int t2 = 0; t2 < D / 32; ++t2) {
-      float sum = 0.f;
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg)
-        if (qtile * 32 + acc_row(reg, hf) < a.T) sum += static_cast<float>(static_cast<__bf16>(dq[t2][reg] * a.scale));
-      sum = xsum32(sum);
-      if (hf == 0) cs[32 * t2 + r] = sum;
-    }
-  }
-}
-
 // -------------------------------------------------------------- backward dKV
 // 4 waves = 4 consecutive key tiles of one (b, kv-head); every query tile of
 // every head in the GQA group is staged once per block (Q, dO and the 32
@@ -1082,290 +880,6 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   }
 }
 
-// ------------------------------------------------ backward dKV, ping-pong form
-// 8 waves = 4 key tiles x 2 halves (waves w and w + 4 share a SIMD and the key
-// tile 4g + w).  The block's (head in group, query tile) steps are dealt
-// alternately: half 0 takes the even steps, half 1 the odd ones; each wave
-// keeps partial dK / dV and half 1's are added into half 0's through LDS at
-// the end.  Phases as in attn_bwd_dq_pp_kernel:
-//   X(s): MFMA only, operands in registers -- dV += Pd^T dO, dK += dS^T Q of
-//         step s-1, then S = Q K^T, dP = dO V^T of step s
-//   Y(s): the LDS reads of X(s+1)'s operands (step s's Q^T / dO^T fragments,
-//         step s+1's Q / dO rows) first, then p, Pd and dS of step s (the
-//         dropout pair hash as in the 4-wave kernel) and the LDS-DMA of step
-//         s + NB - 1
-// with half 1 one interval behind.  The wave's K / V row fragments (the B
-// operands of S and dP, the same every step) stay in registers; Q / dO tiles
-// and the 32 lse / delta / hash-base row values of each step stream through a
-// NB-slot ring per half (slot schedule as in attn_bwd_dq_pp_kernel).
-template <int D, bool DROP>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_bwd_dkv_pp_kernel(AttnArgs a) {
-  constexpr int NB = 4;
-  constexpr int PPW = DmaTile<D>::PPW;
-  constexpr int kTile = 32 * D * 2;                  // bytes of one 32 x D bf16 tile
-  constexpr int kKV = 2 * 4 * kTile;                 // [K | V][key tile]
-  constexpr int kRing = 2 * 2 * NB * kTile;          // [Q | dO][half][slot]
-  constexpr int kLs = 2 * NB * 6 * 32 * 4;           // [half][slot][lse | delta | hash base of tile 0..3][row]
-  constexpr int kRed = 4 * 2 * (D / 32) * 16 * 64 * 4;  // half 1's dk | dv partials
-  constexpr int kAll = kKV + kRing + kLs;
-  __shared__ __attribute__((aligned(16))) char smem[kAll > kRed ? kAll : kRed];
-  typedef LdsTile<D> KV[2][4];
-  typedef LdsTile<D> Ring[2][NB];
-  typedef float Ls[2][NB][6][32];
-  KV& kv_ = *reinterpret_cast<KV*>(smem);
-  Ring& qs_ = *reinterpret_cast<Ring*>(smem + kKV);
-  Ring& os_ = *reinterpret_cast<Ring*>(smem + kKV + kRing / 2);
-  Ls& ls_ = *reinterpret_cast<Ls*>(smem + kKV + kRing);
-  const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int half = wv >> 2, wk = wv & 3;
-  const int ntiles = ntiles32(a.T), nbhk = a.B * a.Hkv;
-  const int bhk = static_cast<int>(blockIdx.x % nbhk);
-  const int grp = static_cast<int>(blockIdx.x / nbhk);  // low key groups (most query tiles) first
-  const int ktile = grp * 4 + wk, first = grp * 4;
-  const bool active = ktile < ntiles;
-  const int b = bhk / a.Hkv, hk = bhk % a.Hkv, group = a.H / a.Hkv;
-  const int kb = ktile * 32, key = kb + r;
-  const int nq = ntiles - first, total = group * nq;  // (head in group, query tile) steps, head-major
-  const int ns = (total + 1) >> 1;                     // steps per half: step 2s + half
-
-  // the block's 4 key tiles of K and V (the first step's wait covers them)
-  {
-    const DmaTile<D> kd(a.k_st, wk), vd(a.v_st, wk);
-    const int row = __builtin_amdgcn_readfirstlane((first + half * 2) * 32);
-    // half h stages key tiles first + 2h and first + 2h + 1 (both K and V)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int rj = row + 32 * j;
-      if (rj < a.T) {  // block-uniform
-        kd.issue(a.k + b * a.k_sb + hk * a.k_sh + static_cast<int64_t>(rj) * a.k_st, kv_[0][2 * half + j], a.T - rj);
-        vd.issue(a.v + b * a.v_sb + hk * a.v_sh + static_cast<int64_t>(rj) * a.v_st, kv_[1][2 * half + j], a.T - rj);
-      }
-    }
-  }
-  const DmaTile<D> qd(a.q_st, wk), dd(a.o_st, wk);
-  // step i = 2s + half -> (head sg, query tile sq), advanced by counters (no
-  // runtime division per step); steps past `total` (half 1's last, odd total)
-  // re-stage step total - 1 and are masked out
-  int sg = 0, sq = first + half;
-  while (sq >= ntiles) { sq -= nq; ++sg; }
-  auto stage = [&](int s, int slot) {
-    const bool ok = 2 * s + half < total;
-    const int g2 = ok ? sg : (total - 1) / nq, q2 = ok ? sq : first + (total - 1) % nq;
-    const int h = hk * group + g2, bh = b * a.H + h;
-    const int qrow = __builtin_amdgcn_readfirstlane(q2 * 32);
-    qd.issue(a.q + b * a.q_sb + h * a.q_sh + static_cast<int64_t>(qrow) * a.q_st, qs_[half][slot], a.T - qrow);
-    dd.issue(a.dout + b * a.o_sb + h * a.o_sh + static_cast<int64_t>(qrow) * a.o_st, os_[half][slot], a.T - qrow);
-    if (wk == 0) {
-      const float* src = (lane < 32 ? a.lse : a.delta) + static_cast<int64_t>(bh) * a.T + min(qrow + (lane & 31), a.T - 1);
-      glds4(src, &ls_[half][slot][0][0]);
-    } else if (DROP && wk == 1) {  // hash bases per (row, key tile), as in the 4-wave kernel
-      const int row = lane & 31, ps = (row & ~3) | ((row & 1) << 1) | ((row >> 1) & 1);
-      const uint32_t ar = drop_row(a.seed, bh, qrow + row);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int tt = 2 * (lane >> 5) + u;
-        ls_[half][slot][2 + tt][ps] = __uint_as_float(tile_base(ar, first + tt));
-      }
-    }
-    // next step of this half: two steps on
-    sq += 2;
-    while (sq >= ntiles) { sq -= nq; ++sg; }
-  };
-  for (int s = 0; s < NB - 1 && s < ns; ++s) stage(s, s);
-  const int pps = 2 * PPW + (wk == 0 ? 1 : 0);  // LDS-DMA pieces per stage of this wave
-
-  const uint32_t tm1 = drop_tm1(a.thresh16), sel = (key & 1) ? 0x03020706u : 0x05040100u;
-  const int par2 = 2 * (key & 1);
-  const uint32_t kmix = (static_cast<uint32_t>(key & 31) >> 1) * kKeyMul;  // pair within the key tile
-  f32x16 dk[D / 32], dv[D / 32];
-#pragma unroll
-  for (int t = 0; t < D / 32; ++t) dk[t] = dv[t] = zero16();
-  f32x16 sacc, dpacc;
-  bf16x8 pf[2], dsf[2];
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) pf[s2] = dsf[s2] = acc_frag(zero16(), 0);
-  // query tile of this half's step s (for the masks), advanced with the steps
-  int qt = first + half, qg = 0;
-  while (qt >= ntiles) { qt -= nq; ++qg; }
-  // the K / V loads and the prologue's steps have landed; the builtin also
-  // tells the waitcnt pass the register work above is complete (see dQ)
-  vm_wait0();
-  if (half == 1) __syncthreads();
-  __syncthreads();
-  bf16x8 kreg[D / 16], vreg[D / 16];                    // this wave's key tile: S / dP B operands
-  bf16x8 qtf[2][D / 32], otf[2][D / 32], qr[D / 16], dr[D / 16];  // X's operands, read in the previous Y
-#pragma unroll
-  for (int ks = 0; ks < D / 16; ++ks) {
-    kreg[ks] = row_frag<D>(kv_[0][wk], r, ks, hf);
-    vreg[ks] = row_frag<D>(kv_[1][wk], r, ks, hf);
-    qr[ks] = row_frag<D>(qs_[half][0], r, ks, hf);
-    dr[ks] = row_frag<D>(os_[half][0], r, ks, hf);
-  }
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-    for (int t = 0; t < D / 32; ++t) {  // any landed tile: pf = dsf = 0 for "step -1"
-      qtf[s2][t] = tr_frag<D>(qs_[half][0], s2, t, lane);
-      otf[s2][t] = tr_frag<D>(os_[half][0], s2, t, lane);
-    }
-  int slot = 0;
-  for (int s = 0; s < ns; ++s) {
-    // ---- X(s): matrix phase, operands in registers
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int t = 0; t < D / 32; ++t) {
-        dv[t] = mfma32(pf[s2], otf[s2][t], dv[t]);   // dV += Pd^T dO
-        dk[t] = mfma32(dsf[s2], qtf[s2][t], dk[t]);  // dK += dS^T Q
-      }
-    sacc = zero16();
-    dpacc = zero16();
-#pragma unroll
-    for (int ks = 0; ks < D / 16; ++ks) {
-      sacc = mfma32(qr[ks], kreg[ks], sacc);   // S = Q K^T
-      dpacc = mfma32(dr[ks], vreg[ks], dpacc);  // dP = dO V^T
-    }
-    // retire step s + 1 before Y(s) reads its rows; only step s + 2 may stay in flight
-    if (s + 1 < ns) vm_wait_n((s + 2 < ns ? 1 : 0) * pps);
-    __syncthreads();
-    // ---- Y(s): X(s+1)'s operand reads first (step s's Q^T / dO^T, step s+1's rows)
-    const int nxt = slot + 1 == NB ? 0 : slot + 1;
-    const int rs = s + 1 < ns ? nxt : slot;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int t = 0; t < D / 32; ++t) {
-        qtf[s2][t] = tr_frag<D>(qs_[half][slot], s2, t, lane);
-        otf[s2][t] = tr_frag<D>(os_[half][slot], s2, t, lane);
-      }
-#pragma unroll
-    for (int ks = 0; ks < D / 16; ++ks) {
-      qr[ks] = row_frag<D>(qs_[half][rs], r, ks, hf);
-      dr[ks] = row_frag<D>(os_[half][rs], r, ks, hf);
-    }
-    const int qb = qt * 32;
-    const bool live = 2 * s + half < total;
-    if (!live || qt <= ktile || qb + 32 > a.T) {  // diagonal / before it (all masked), tail rows, no step
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int qr = qb + acc_row(reg, hf);
-        if (!live || key > qr || qr >= a.T) sacc[reg] = -INFINITY;
-      }
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      i32x4 pw, dw;
-#pragma unroll
-      for (int gg = 0; gg < 2; ++gg) {
-        const int g = 2 * s2 + gg;
-        const float4 lv = *reinterpret_cast<const float4*>(&ls_[half][slot][0][8 * g + 4 * hf]);
-        const float4 dv4 = *reinterpret_cast<const float4*>(&ls_[half][slot][1][8 * g + 4 * hf]);
-        uint2 av = make_uint2(0, 0);
-        if constexpr (DROP) av = *reinterpret_cast<const uint2*>(&ls_[half][slot][2 + wk][8 * g + 4 * hf + par2]);
-        const float lse_g[4] = {lv.x, lv.y, lv.z, lv.w};
-        const float dl_g[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
-        uint32_t own[2], other[2];
-        if constexpr (DROP) {
-          own[0] = mix1(av.x + kmix);
-          own[1] = mix1(av.y + kmix);
-#pragma unroll
-          for (int pi = 0; pi < 2; ++pi)  // lanes 0<->1, 2<->3
-            other[pi] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(own[pi]), 0xB1, 0xF, 0xF, false));
-        }
-#pragma unroll
-        for (int pi = 0; pi < 2; ++pi) {
-          const int e0 = 2 * pi, r0 = 4 * g + e0;
-          const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r0], a.scale_log2, -lse_g[e0]));
-          const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r0 + 1], a.scale_log2, -lse_g[e0 + 1]));
-          uint32_t pv, dsv;
-          if constexpr (DROP) {
-            const uint32_t mk = keep_mask2(__builtin_amdgcn_perm(other[pi], own[pi], sel), tm1);
-            pv = pk2(p0, p1) & mk;  // Pd
-            const float a0 = p0 * dl_g[e0], a1 = p1 * dl_g[e0 + 1];
-            dsv = bfi(mk, pk2(__builtin_fmaf(p0, dpacc[r0], -a0), __builtin_fmaf(p1, dpacc[r0 + 1], -a1)),
-                      pk2(-a0, -a1));
-          } else {
-            pv = pk2(p0, p1);
-            dsv = pk2(p0 * (dpacc[r0] - dl_g[e0]), p1 * (dpacc[r0 + 1] - dl_g[e0 + 1]));
-          }
-          pw[2 * gg + pi] = static_cast<int>(pv);
-          dw[2 * gg + pi] = static_cast<int>(dsv);
-        }
-      }
-      pf[s2] = __builtin_bit_cast(bf16x8, pw);
-      dsf[s2] = __builtin_bit_cast(bf16x8, dw);
-    }
-    // step s - 1's slot (last read in Y(s - 1); at s = 0 the unused slot NB - 1) takes step s + NB - 1
-    const int fslot = slot == 0 ? NB - 1 : slot - 1;
-    if (s + NB - 1 < ns) stage(s + NB - 1, fslot);
-    slot = nxt;
-    qt += 2;
-    while (qt >= ntiles) { qt -= nq; ++qg; }
-    __syncthreads();
-  }
-  // X(ns): the last step's dV / dK
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-    for (int t = 0; t < D / 32; ++t) {
-      dv[t] = mfma32(pf[s2], otf[s2][t], dv[t]);
-      dk[t] = mfma32(dsf[s2], qtf[s2][t], dk[t]);
-    }
-  if (half == 0) __syncthreads();
-  __syncthreads();
-  // half 1's partials -> LDS -> half 0 adds and stores
-  float* red = reinterpret_cast<float*>(smem) + wk * (2 * (D / 32) * 16 * 64);
-  if (half == 1) {
-#pragma unroll
-    for (int t = 0; t < D / 32; ++t)
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        red[(t * 16 + reg) * 64 + lane] = dk[t][reg];
-        red[((D / 32 + t) * 16 + reg) * 64 + lane] = dv[t][reg];
-      }
-  }
-  __syncthreads();
-  if (half == 1 || !active) return;
-#pragma unroll
-  for (int t = 0; t < D / 32; ++t)
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      dk[t][reg] += red[(t * 16 + reg) * 64 + lane];
-      dv[t][reg] += red[((D / 32 + t) * 16 + reg) * 64 + lane];
-    }
-  __bf16* dkb = a.dk + b * a.dk_sb + hk * a.dk_sh;
-  __bf16* dvb = a.dv + b * a.dk_sb + hk * a.dk_sh;
-#pragma unroll
-  for (int t = 0; t < D / 32; ++t)
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      if (kb + acc_row(reg, hf) >= a.T) continue;
-      const int64_t off = static_cast<int64_t>(kb + acc_row(reg, hf)) * a.dk_st + 32 * t + r;
-      st_bf16(dkb + off, dk[t][reg] * a.scale);
-      st_bf16(dvb + off, dv[t][reg]);
-    }
-  if (a.colsum != nullptr) {  // bias-gradient partials of the k and v columns (H == Hkv)
-    float* cs = a.colsum + static_cast<int64_t>(b * ntiles + ktile) * (3 * a.H * D) + hk * D;
-#pragma unroll
-    for (int t = 0; t < D / 32; ++t) {
-      float sk = 0.f, sv = 0.f;
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        if (kb + acc_row(reg, hf) >= a.T) continue;
-        sk += static_cast<float>(static_cast<__bf16>(dk[t][reg] * a.scale));
-        sv += static_cast<float>(static_cast<__bf16>(dv[t][reg]));
-      }
-      sk = xsum32(sk);
-      sv = xsum32(sv);
-      if (hf == 0) {
-        cs[a.H * D + 32 * t + r] = sk;
-        cs[2 * a.H * D + 32 * t + r] = sv;
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------------------ launchers
 // ceil(tiles / 4) blocks of 4 waves per head
 static inline int64_t tile_blocks(int64_t nbh, int T) { return nbh * ((((T + 31) >> 5) + 3) >> 2); }
@@ -1388,45 +902,26 @@ hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
   return hipGetLastError();
 }
 
-// backward kernel choice (A/B while the ping-pong kernels are being measured):
-// DLION_ATTN_PP bit 1 = the ping-pong dQ, bit 2 = the ping-pong dK/dV (D = 64)
-static int attn_pp_mask() {
-  static const int m = [] {
-    const char* e = getenv("DLION_ATTN_PP");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
-}
-
 hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) {
   const dim3 bq(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T)));
   const dim3 bkv(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.Hkv, a.T)));
-  const bool pp_dq = (attn_pp_mask() & 1) != 0, pp_dkv = (attn_pp_mask() & 2) != 0;
   // dQ first: it also computes delta = rowsum(dO * O), which dKV reads
+#define BWD(DD)                                                                         \
+  if (drop) {                                                                           \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, true, 1>), bq, dim3(256), 0, st, a);    \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), bkv, dim3(256), 0, st, a);     \
+  } else {                                                                              \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, false, 1>), bq, dim3(256), 0, st, a);   \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), bkv, dim3(256), 0, st, a);    \
+  }
   if (D == 64) {
-    if (drop) {
-      if (pp_dq) hipLaunchKernelGGL((attn_bwd_dq_pp_kernel<64, true>), bq, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, true, 1>), bq, dim3(256), 0, st, a);
-      if (pp_dkv) hipLaunchKernelGGL((attn_bwd_dkv_pp_kernel<64, true>), bkv, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((attn_bwd_dkv_kernel<64, true>), bkv, dim3(256), 0, st, a);
-    } else {
-      if (pp_dq) hipLaunchKernelGGL((attn_bwd_dq_pp_kernel<64, false>), bq, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, false, 1>), bq, dim3(256), 0, st, a);
-      if (pp_dkv) hipLaunchKernelGGL((attn_bwd_dkv_pp_kernel<64, false>), bkv, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((attn_bwd_dkv_kernel<64, false>), bkv, dim3(256), 0, st, a);
-    }
+    BWD(64)
   } else if (D == 128) {
-    // (the ping-pong kernels' register-resident operands / LDS rings do not fit at D = 128)
-    if (drop) {
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<128, true, 1>), bq, dim3(256), 0, st, a);
-      hipLaunchKernelGGL((attn_bwd_dkv_kernel<128, true>), bkv, dim3(256), 0, st, a);
-    } else {
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<128, false, 1>), bq, dim3(256), 0, st, a);
-      hipLaunchKernelGGL((attn_bwd_dkv_kernel<128, false>), bkv, dim3(256), 0, st, a);
-    }
+    BWD(128)
   } else {
     return hipErrorInvalidValue;
   }
+#undef BWD
   return hipGetLastError();
 }
 
