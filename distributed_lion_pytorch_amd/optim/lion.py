@@ -496,6 +496,8 @@ class Lion(Optimizer):
                     if reset:
                         w.reset()
             out.update(tot.snapshot())
+        if self._executor is not None:
+            out["executor"] = type(self._executor).__name__  # HipExecutor: the gfx950 kernels ran
         if self._plan is not None:
             out["numel"] = sum(s.numel for s in self._plan.segments)
             out["n_buckets"] = len(self._plan.buckets)

@@ -123,3 +123,39 @@ def test_visible_gpu_count_without_hip():
     from distributed_lion_pytorch_amd.utils.devices import visible_gpu_count
 
     assert visible_gpu_count() == torch.cuda.device_count() >= 1
+
+
+def test_run_clm_torchrun_two_ranks_one_gpu(tmp_path):
+    """the drop-in HF path as the 8-GPU run will use it --
+    torchrun, accelerate's DDP wrap of the native model, no_sync, the fusion
+    window writing weight gradients into param.grad, the fused clip and the
+    HIP Lion -- with W = 2 (both ranks on the one GPU, gloo transport: RCCL
+    refuses two ranks on one device; accelerate maps LOCAL_RANK 1 to cuda:0)."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "clm")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), "run_clm.py", "--config_name", "gpt2-tiny", "--synthetic_data",
+           "--synthetic_samples", "64", "--block_size", "128", "--per_device_train_batch_size", "2",
+           "--gradient_accumulation_steps", "2", "--lion", "--async_grad", "--bf16", "--torch_dtype", "bfloat16",
+           "--max_steps", "4", "--warmup_steps", "1", "--learning_rate", "1e-3", "--logging_steps", "1",
+           "--do_train", "--ddp_backend", "gloo", "--report_to", "none", "--save_strategy", "no",
+           "--output_dir", out]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-5000:]
+    recs = [json.loads(x) for x in open(os.path.join(out, "metrics.jsonl"))]
+    end = [x for x in recs if "replicas_identical" in x]
+    assert end and end[-1]["replicas_identical"] == 1.0 and end[-1]["world_end"] == 2.0, recs[-2:]
+    lion = [x["lion"] for x in recs if "lion" in x]
+    assert lion and all(s["world"] == 2 for s in lion)
+    assert sum(s.get("wire_bytes_sent", 0) for s in lion) > 0  # the vote really went over the transport
+    assert {s.get("executor") for s in lion} == {"HipExecutor"}
