@@ -76,6 +76,8 @@ hipError_t launch_sum_partials_split(const float* const* ptrs, const int64_t* ro
 // Needs K % 128 == 0, N % 8 == 0, leading dims % 8 == 0.
 void set_gemm_persist(int on);
 int gemm_persist_enabled();
+void set_gemm_stagger(int units);
+int gemm_stagger();
 hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
                           void* aux, int ldaux, int M, int N, int K, int epi, float* part, hipStream_t st);
 

@@ -10,3 +10,5 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 3 > $O/bench.json 2> $O/be
 tail -1 $O/bench.json | cut -c1-240
 timeout -k 10 900 python tools/r5/elastic_ab.py 3 $O/elastic_ab.jsonl || exit 1
 bash tools/gpu_prof_llama3.sh || exit 1
+timeout -k 10 300 python tools/r5/bench_gemm_stagger.py > $O/gemm_stagger.txt 2>&1 || { tail -20 $O/gemm_stagger.txt; exit 1; }
+cat $O/gemm_stagger.txt
