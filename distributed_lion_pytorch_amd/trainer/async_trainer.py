@@ -217,6 +217,7 @@ class AsyncMixin:
         return loss
 
     def train(self, *a, **kw):
+        _share_gpus_if_oversubscribed(self.args)
         if getattr(self.args, "lion_elastic_timeout", None) is not None:
             # no forward-time buffer broadcast on DDP's (possibly stale) group;
             # buffers are deterministic and every rank builds them identically
@@ -371,6 +372,17 @@ class AsyncMixin:
             logger.info("restored per-rank optimizer state from %s", path)
 
 
+def _share_gpus_if_oversubscribed(args) -> None:
+    """More ranks than GPUs (rehearsals: W gloo ranks on one MI355X): accelerate
+    places rank r on cuda:(r mod #GPUs) but builds DDP with device_ids=[r],
+    which moves rank r's inputs to a device that does not exist.  Without
+    device_ids DDP uses the module's device."""
+    if not torch.cuda.is_available() or getattr(args, "world_size", 1) <= 1:
+        return
+    if getattr(args, "local_process_index", 0) >= torch.cuda.device_count():
+        os.environ["ACCELERATE_BYPASS_DEVICE_MAP"] = "true"
+
+
 def param_digest(model: torch.nn.Module, chunk: int = 1 << 24) -> torch.Tensor:
     """Order-dependent digest of every parameter's raw bits, computed ON the
     parameters' device (a 2-element int64 tensor).  Per tensor: the sum and the
@@ -444,6 +456,10 @@ class RankShardedLoaderMixin:
     iterable data) or wrap it in an ``IterableDatasetShard`` that drops
     (W-1)/W of the already-sharded batches.  Batches are moved to the device by
     ``_prepare_inputs``."""
+
+    def train(self, *a, **kw):
+        _share_gpus_if_oversubscribed(self.args)
+        return super().train(*a, **kw)
 
     def get_train_dataloader(self):
         ds = self.train_dataset
