@@ -1092,15 +1092,10 @@ TORCH_LIBRARY(dlion, m) {
       " Tensor? own, Tensor(b!)? agree) -> ()");
   m.def("vote_reduce(Tensor recv, int nbytes, Tensor alive, int tie, Tensor(a!) out, Tensor(b!)? neg_out,"
         " Tensor(c!)? ties=None) -> ()");
-  // persistent NT GEMM switch (A/B); returns the previous setting
+  // GEMM first-round start stagger (A/B); returns the previous setting
   m.def("set_gemm_stagger(int units) -> int", [](int64_t units) -> int64_t {
     const int prev = dlion::gemm_stagger();
     dlion::set_gemm_stagger(static_cast<int>(units));
-    return prev;
-  });
-  m.def("set_gemm_persist(int on) -> int", [](int64_t on) -> int64_t {
-    const int prev = dlion::gemm_persist_enabled();
-    dlion::set_gemm_persist(static_cast<int>(on));
     return prev;
   });
 }

@@ -76,12 +76,6 @@ template <> struct Elem<kF32> {
     reinterpret_cast<float4*>(p)[0] = make_float4(o[0], o[1], o[2], o[3]);
     reinterpret_cast<float4*>(p)[1] = make_float4(o[4], o[5], o[6], o[7]);
   }
-  // streaming (non-temporal) variant: data written once and not re-read soon
-  __device__ __forceinline__ static void store8nt(S* p, const float (&o)[8]) {
-    typedef float nt_f32x4 __attribute__((ext_vector_type(4)));
-    __builtin_nontemporal_store(nt_f32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<nt_f32x4*>(p));
-    __builtin_nontemporal_store(nt_f32x4{o[4], o[5], o[6], o[7]}, reinterpret_cast<nt_f32x4*>(p) + 1);
-  }
   // round-trip through storage precision (identity for f32)
   __device__ __forceinline__ static float rnd(float v) { return v; }
 };
@@ -110,15 +104,6 @@ template <int DT> struct Elem16 {
       w[i] = static_cast<uint32_t>(from_f(o[2 * i])) |
              (static_cast<uint32_t>(from_f(o[2 * i + 1])) << 16);
     *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
-  }
-  __device__ __forceinline__ static void store8nt(S* p, const float (&o)[8]) {
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      w[i] = static_cast<uint32_t>(from_f(o[2 * i])) |
-             (static_cast<uint32_t>(from_f(o[2 * i + 1])) << 16);
-    typedef uint32_t nt_u32x4 __attribute__((ext_vector_type(4)));
-    __builtin_nontemporal_store(nt_u32x4{w[0], w[1], w[2], w[3]}, reinterpret_cast<nt_u32x4*>(p));
   }
   __device__ __forceinline__ static float rnd(float v) { return to_f(from_f(v)); }
 };

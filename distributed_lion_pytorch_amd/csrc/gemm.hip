@@ -41,15 +41,12 @@
 // the next tile's first K-tiles during the current tile's tail and stores
 // straight from the accumulators (8-byte stores, operands swapped so a lane
 // owns 4 consecutive columns) measured 4-10 % SLOWER: the scattered 8-byte
-// epilogue stores cost more than the hidden prologue saved.
+// epilogue stores cost more than the hidden prologue saved; a second one that
+// parked through spare LDS and overlapped the next tile's prologue with the
+// epilogue measured neutral (profiles/r4/gemm_epi_persist.txt) and was removed.
 #include "common.h"
 
 #include <algorithm>
-
-// cache-policy bits of the operand LDS-DMA loads (A/B switch; 2 = nt on gfx950)
-#ifndef DLION_NT_LOAD_AUX
-#define DLION_NT_LOAD_AUX 0
-#endif
 
 namespace dlion {
 
@@ -85,25 +82,17 @@ __device__ __forceinline__ void vm_wait0() { asm volatile("s_waitcnt vmcnt(0)" :
 
 __device__ __forceinline__ void glds16(const uint16_t* src, uint8_t* dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)dst, 16, 0, DLION_NT_LOAD_AUX);
+                                   (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
-// Epilogue store / aux-load flavour: DLION_GEMM_NT_AUX writes / reads the MLP
-// aux tensor (gelu'(z): written here, read once by the backward) with
-// non-temporal hints, DLION_GEMM_NT_C does the same for C.  Same-box GPT-2
+// Epilogue store / aux-load flavour: the MLP epilogues write / read the aux
+// tensor (gelu'(z): written here, read once by the backward) and their C with
+// non-temporal hints (plain / bias outputs keep normal stores).  Same-box GPT-2
 // A/B: 1.019M (both off) -> 1.024M (aux) -> 1.035M tok/s (both)
 // (profiles/r3/nt_stores_ab.txt); in isolation the MLP GEMMs gain only 1-5 us,
 // the rest is what the other kernels of the step no longer lose to the
-// 126 MB outputs streaming through L2 / MALL
-#ifndef DLION_GEMM_NT_AUX
-#define DLION_GEMM_NT_AUX 1
-#endif
-#ifndef DLION_GEMM_NT_C
-#define DLION_GEMM_NT_C 1
-#endif
-#ifndef DLION_GEMM_NT_C_PLAIN
-#define DLION_GEMM_NT_C_PLAIN 0
-#endif
+// 126 MB outputs streaming through L2 / MALL.  Non-temporal operand loads and
+// non-temporal plain-C stores measured neutral and were removed.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 template <bool NT, typename V>
 __device__ __forceinline__ void st16(uint16_t* p, const V& v) {
@@ -118,12 +107,7 @@ __device__ __forceinline__ uint4 ld16(const uint16_t* p) {
   else x = *reinterpret_cast<const u32x4*>(p);
   return make_uint4(x[0], x[1], x[2], x[3]);
 }
-constexpr bool kNtAux = DLION_GEMM_NT_AUX != 0, kNtC = DLION_GEMM_NT_C != 0;
-// diagnostic builds only (tools/bench_gemm_epi.py on variant libraries): 1 = EPI 6/7
-// skip the GELU math (both outputs get z), 2 = EPI 6/7 skip the aux store
-#ifndef DLION_EPI_DIAG
-#define DLION_EPI_DIAG 0
-#endif
+constexpr bool kNtAux = true, kNtC = true;
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -400,7 +384,7 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
       const int gm = row_base + row;
       // plain / bias outputs (input gradients, projections: read at once by the
       // next kernel) keep normal stores; only the MLP epilogues' streams go non-temporal
-      if (gm < g.M && gn < g.N) st16<kNtC && DLION_GEMM_NT_C_PLAIN>(g.C + (int64_t)gm * g.ldc + gn, v);
+      if (gm < g.M && gn < g.N) st16<false>(g.C + (int64_t)gm * g.ldc + gn, v);
     }
     if constexpr (STAMP) {
       DLION_STAMP(st_[4])
@@ -441,15 +425,11 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             float gv, dgv;
-            if constexpr (DLION_EPI_DIAG == 1) {
-              gv = dgv = z[j];
-            } else {
-              gelu_and_grad(z[j] + b8[j], EPI == 7, gv, dgv);
-            }
+            gelu_and_grad(z[j] + b8[j], EPI == 7, gv, dgv);
             hb[j] = static_cast<__bf16>(gv);
             db[j] = static_cast<__bf16>(dgv);
           }
-          if constexpr (DLION_EPI_DIAG != 2) st16<kNtAux>(g.aux + (int64_t)gm * g.ldaux + gn, db);
+          st16<kNtAux>(g.aux + (int64_t)gm * g.ldaux + gn, db);
         }
         st16<kNtC>(g.C + (int64_t)gm * g.ldc + gn, hb);
       }
@@ -519,342 +499,6 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
   }
 }
 
-// ------------------------------------------------------------------ persistent
-// Persistent form (DLION_GEMM_PERSIST): one 512-thread block per CU walks its
-// XCD's contiguous tile range (block j of XCD x takes tiles j, j + G_x, ...),
-// and the NEXT tile's prologue -- its first six half-tiles of LDS-DMA -- is
-// issued right after the current tile's last LDS reads, so the HBM / L2
-// latency of those loads runs under the current tile's epilogue instead of
-// after it (stamp build of the one-tile-per-block kernel, K = 768: prologue
-// 8.6 %, park + drain 12 % of the block time; kernel-launch tail 13 %).
-// The epilogue parks through 64 KB of LDS the next prologue does not touch
-// (dbuf 1's A halves + 32 KB past the operand ring: 160 KiB in all), 8 KB =
-// 64 rows per wave and round, two rounds, each wave reading back only what it
-// parked (no block barrier).  The hand-placed vmcnt waits keep their counts:
-// epilogue stores issued after the prologue DMAs are younger, so a wait can
-// only over-wait, never release a slot early.
-constexpr int kPStage = 8 * 1024;
-
-template <int EPI>
-__global__ void __launch_bounds__(512, 1) gemm_nt_pkernel(const GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kLds + 4 * kPStage];  // 160 KiB
-
-  const int tid = threadIdx.x;
-  const int w = tid >> 6, lane = tid & 63;
-  const int wr = w >> 2, wc = w & 3;
-
-  // ---- persistent tile schedule (grid = #tiles if <= 256, else 256 = 8 x 32)
-  const int nwg = g.tiles_m * g.tiles_n;
-  const int bid = blockIdx.x, nblk = gridDim.x;
-  const int xcd = bid & 7, jx = bid >> 3;
-  const int gx = (nblk >> 3) + (xcd < (nblk & 7) ? 1 : 0);
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int r_begin = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-  const int r_len = q8 + (xcd < r8 ? 1 : 0);
-  if (jx >= r_len) return;  // block-uniform
-  const int ntile = (r_len - jx + gx - 1) / gx;
-  constexpr int GM = 8;
-  auto tile_of = [&](int k, int& m0, int& n0, int& tm) {
-    const int wg = r_begin + jx + k * gx;
-    const int per_group = GM * g.tiles_n;
-    const int grp = wg / per_group;
-    const int first_m = grp * GM;
-    const int gsz = min(g.tiles_m - first_m, GM);
-    const int in_g = wg - grp * per_group;
-    tm = first_m + in_g % gsz;
-    m0 = tm * kBM;
-    n0 = (in_g / gsz) * kBN;
-  };
-  // staging offsets of a tile (see gemm_nt_kernel)
-  auto offsets = [&](int m0, int n0, Stage& st) {
-    const int pc = lane & 7;
-#pragma unroll
-    for (int pi = 0; pi < 2; ++pi) {
-      const int q = 2 * w + pi;
-      const int lr = 8 * q + (lane >> 3);
-      const int c = pc ^ ((lr >> 1) & 7);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int ra = min(m0 + (lr >> 6) * 128 + 64 * h + (lr & 63), g.M - 1);
-        st.off[0][h][pi] = ra * g.lda + c * 8;
-        const int rb = min(n0 + 128 * h + lr, g.N - 1);
-        st.off[1][h][pi] = rb * g.ldb + c * 8;
-      }
-    }
-  };
-  const uint16_t* __restrict__ Ag = g.A;
-  const uint16_t* __restrict__ Bg = g.B;
-  auto stage_t = [&](const Stage& st, int ab, int half, int dbuf, int kt) {
-    const uint16_t* base = (ab == 0 ? Ag : Bg) + kt * kBK;
-    uint8_t* dst = lds + slot(dbuf, ab, half) + (2 * w) * 1024;
-    glds16(base + st.off[ab][half][0], dst);
-    glds16(base + st.off[ab][half][1], dst + 1024);
-  };
-  auto prologue = [&](const Stage& st) {  // T0.{B0,B1,A0,A1}, T1.{B0,B1}
-    stage_t(st, 1, 0, 0, 0);
-    stage_t(st, 1, 1, 0, 0);
-    stage_t(st, 0, 0, 0, 0);
-    stage_t(st, 0, 1, 0, 0);
-    stage_t(st, 1, 0, 1, 1);
-    stage_t(st, 1, 1, 1, 1);
-  };
-
-  const int lr16 = lane & 15;
-  const int swz = (lr16 >> 1) & 7;
-  const int foff0 = lr16 * 128 + (((lane >> 4) ^ swz) << 4);
-  const int foff1 = lr16 * 128 + (((4 + (lane >> 4)) ^ swz) << 4);
-  const int a_row_base = wr * 64 * 128;
-  const int b_base_off = ((wc >> 1) * kHalf) + (wc & 1) * 64 * 128;
-
-  f32x4 acc[8][4];
-  bf16x8 bfr[4][2];
-  bf16x8 afr[2][2];
-  auto read_b = [&](int dbuf) {
-    const uint8_t* base = lds + slot(dbuf, 1, 0) + b_base_off;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      bfr[nt][0] = *reinterpret_cast<const bf16x8*>(base + nt * 16 * 128 + foff0);
-      bfr[nt][1] = *reinterpret_cast<const bf16x8*>(base + nt * 16 * 128 + foff1);
-    }
-  };
-  auto read_a = [&](int dbuf, int p) {
-    const uint8_t* base = lds + slot(dbuf, 0, p >> 1) + a_row_base + (2 * (p & 1)) * 16 * 128;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      afr[mt][0] = *reinterpret_cast<const bf16x8*>(base + mt * 16 * 128 + foff0);
-      afr[mt][1] = *reinterpret_cast<const bf16x8*>(base + mt * 16 * 128 + foff1);
-    }
-  };
-#define DLION_PGEMM_MFMA(P)                                                       \
-  do {                                                                            \
-    __builtin_amdgcn_s_setprio(1);                                                \
-    _Pragma("unroll") for (int mt = 0; mt < 2; ++mt)                              \
-    _Pragma("unroll") for (int nt = 0; nt < 4; ++nt)                              \
-    _Pragma("unroll") for (int s = 0; s < 2; ++s)                                 \
-      acc[2 * (P) + mt][nt] = mfma16(bfr[nt][s], afr[mt][s], acc[2 * (P) + mt][nt]); \
-    __builtin_amdgcn_s_setprio(0);                                                \
-  } while (0)
-#define DLION_PGEMM_PHASE_MATH(P)                    \
-  __builtin_amdgcn_s_barrier();                      \
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
-  __builtin_amdgcn_sched_barrier(0);                 \
-  DLION_PGEMM_MFMA(P);                               \
-  __builtin_amdgcn_sched_barrier(0);                 \
-  __builtin_amdgcn_s_barrier();
-
-  const int nk = g.K / kBK;  // even, >= 2
-  const int nit = nk / 2;
-
-  int m0, n0, tm;
-  tile_of(0, m0, n0, tm);
-  Stage st;
-  offsets(m0, n0, st);
-  prologue(st);
-  vm_wait6();
-  __builtin_amdgcn_s_barrier();
-
-  // per-wave epilogue staging: 64 rows x 128 B, outside the slots the next prologue fills
-  uint8_t* reg = lds + (w < 4 ? slot(1, 0, 0) + w * kPStage : kLds + (w - 4) * kPStage);
-
-  for (int k = 0; k < ntile; ++k) {
-    if (wr == 1) __builtin_amdgcn_s_barrier();  // wave-group stagger (see gemm_nt_kernel)
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int it = 0; it < nit; ++it) {
-      const int kt = 2 * it;
-      const bool more = it + 1 < nit;
-      read_b(0);
-      read_a(0, 0);
-      stage_t(st, 0, 0, 1, kt + 1);
-      DLION_PGEMM_PHASE_MATH(0)
-      read_a(0, 1);
-      stage_t(st, 0, 1, 1, kt + 1);
-      vm_wait8();
-      DLION_PGEMM_PHASE_MATH(1)
-      read_a(0, 2);
-      if (more) stage_t(st, 1, 0, 0, kt + 2);
-      DLION_PGEMM_PHASE_MATH(2)
-      read_a(0, 3);
-      if (more) {
-        stage_t(st, 1, 1, 0, kt + 2);
-        vm_wait6();
-      } else {
-        vm_wait2();
-      }
-      DLION_PGEMM_PHASE_MATH(3)
-      read_b(1);
-      read_a(1, 0);
-      if (more) stage_t(st, 0, 0, 0, kt + 2);
-      DLION_PGEMM_PHASE_MATH(0)
-      read_a(1, 1);
-      if (more) {
-        stage_t(st, 0, 1, 0, kt + 2);
-        vm_wait8();
-      } else {
-        vm_wait0();
-      }
-      DLION_PGEMM_PHASE_MATH(1)
-      read_a(1, 2);
-      if (more) stage_t(st, 1, 0, 1, kt + 3);
-      DLION_PGEMM_PHASE_MATH(2)
-      read_a(1, 3);
-      if (more) {
-        stage_t(st, 1, 1, 1, kt + 3);
-        vm_wait6();
-      }
-      DLION_PGEMM_PHASE_MATH(3)
-    }
-    if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align: every MFMA and LDS read of this tile is done
-
-    // ---- next tile: its aux loads (EPI 4/5/8, for THIS tile) go first, then the next prologue
-    const bool next = k + 1 < ntile;
-    const int row_base = m0 + wr * 128, col_base = n0 + wc * 64;
-    const int ch = lane & 7;
-    const int gn = col_base + ch * 8;
-    // z rows of one epilogue round (64 rows: 8 per lane); round 0's go before
-    // the next prologue's DMAs, round 1's after round 0's park (32 VGPRs, not 64)
-    uint4 zr[8];
-    auto load_z = [&](int rd) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int gm = min(row_base + 64 * rd + i * 8 + (lane >> 3), g.M - 1);
-        zr[i] = gn < g.N ? ld16<kNtAux>(g.aux + (int64_t)gm * g.ldaux + gn) : make_uint4(0, 0, 0, 0);
-      }
-    };
-    if constexpr (EPI == 4 || EPI == 5 || EPI == 8) load_z(0);
-    int m0n = 0, n0n = 0, tmn = 0;
-    if (next) {
-      tile_of(k + 1, m0n, n0n, tmn);
-      offsets(m0n, n0n, st);  // st is dead until the next mainloop: no second offset set across the epilogue
-      prologue(st);
-    }
-
-    // ---- epilogue of this tile: two rounds of 64 rows through the wave's staging
-    float bv[4][4] = {};
-    if constexpr (EPI == 1) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int n = n0 + wc * 64 + nt * 16 + 4 * (lane >> 4) + j;
-          bv[nt][j] = n < g.N ? bf16_to_f32(g.bias[n]) : 0.f;
-        }
-    }
-    float b8[8], cs[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) cs[j] = 0.f;
-    if constexpr (EPI >= 2) {
-      if (EPI != 8 && gn < g.N) {
-        Elem<kBF16>::load8(g.bias + gn, b8);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) b8[j] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int rd = 0; rd < 2; ++rd) {
-      // park rows 64rd .. 64rd+63 (m-tiles 4rd .. 4rd+3), 16-byte chunk ^= row & 7
-#pragma unroll
-      for (int mq = 0; mq < 4; ++mq)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const int mt = 4 * rd + mq;
-          const int row = mq * 16 + (lane & 15);
-          const int col = nt * 16 + 4 * (lane >> 4);
-          const int chunk = (col >> 3) ^ (row & 7);
-          uint32_t v[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float x = acc[mt][nt][j];
-            if constexpr (EPI == 1) x += bv[nt][j];
-            v[j] = __builtin_bit_cast(uint16_t, static_cast<__bf16>(x));
-          }
-          *reinterpret_cast<uint2*>(reg + row * 128 + chunk * 16 + (col & 7) * 2) =
-              make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
-        }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      if constexpr (EPI == 4 || EPI == 5 || EPI == 8) {
-        if (rd == 1) load_z(1);
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int row = i * 8 + (lane >> 3);
-        const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((ch ^ (row & 7)) << 4));
-        const int gm = row_base + 64 * rd + row;
-        if (gm >= g.M || gn >= g.N) continue;
-        if constexpr (EPI <= 1) {
-          st16<kNtC && DLION_GEMM_NT_C_PLAIN>(g.C + (int64_t)gm * g.ldc + gn, v);
-        } else if constexpr (EPI <= 3 || EPI == 6 || EPI == 7) {
-          float z[8];
-          Elem<kBF16>::load8(reinterpret_cast<const uint16_t*>(&v), z);
-          bf16x8 hb;
-          if constexpr (EPI <= 3) {
-            st16<kNtAux>(g.aux + (int64_t)gm * g.ldaux + gn, v);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) hb[j] = static_cast<__bf16>(gelu_f(z[j] + b8[j], EPI == 3));
-          } else {
-            bf16x8 db;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              float gv, dgv;
-              gelu_and_grad(z[j] + b8[j], EPI == 7, gv, dgv);
-              hb[j] = static_cast<__bf16>(gv);
-              db[j] = static_cast<__bf16>(dgv);
-            }
-            st16<kNtAux>(g.aux + (int64_t)gm * g.ldaux + gn, db);
-          }
-          st16<kNtC>(g.C + (int64_t)gm * g.ldc + gn, hb);
-        } else {
-          float gv[8], z[8];
-          Elem<kBF16>::load8(reinterpret_cast<const uint16_t*>(&v), gv);
-          Elem<kBF16>::load8(reinterpret_cast<const uint16_t*>(&zr[i]), z);
-          bf16x8 ob;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float o;
-            if constexpr (EPI == 8) {
-              o = gv[j] * z[j];
-            } else {
-              o = gv[j] * gelu_grad(z[j] + b8[j], EPI == 5);
-            }
-            ob[j] = static_cast<__bf16>(o);
-            cs[j] += static_cast<float>(ob[j]);
-          }
-          st16<kNtC>(g.C + (int64_t)gm * g.ldc + gn, ob);
-        }
-      }
-      // the next round re-parks into the same bytes: every lane's read-back is done
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-    }
-    if constexpr (EPI == 4 || EPI == 5 || EPI == 8) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        cs[j] += __shfl_xor(cs[j], 8);
-        cs[j] += __shfl_xor(cs[j], 16);
-        cs[j] += __shfl_xor(cs[j], 32);
-      }
-      if (lane < 8 && gn < g.N) {
-        float* dst = g.part + (int64_t)(2 * tm + wr) * g.N + gn;
-        *reinterpret_cast<float4*>(dst) = make_float4(cs[0], cs[1], cs[2], cs[3]);
-        *reinterpret_cast<float4*>(dst + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
-      }
-    }
-    if (next) {
-      m0 = m0n;
-      n0 = n0n;
-      tm = tmn;
-      vm_wait6();  // the next tile's T0.{B0,B1,A0} (over-waits the younger epilogue stores)
-      __builtin_amdgcn_s_barrier();
-    }
-  }
-#undef DLION_PGEMM_PHASE_MATH
-#undef DLION_PGEMM_MFMA
-}
-
 }  // namespace
 
 // diagnostic: plain GEMM (EPI 0) with per-block timestamps into stamps[grid][8]
@@ -878,16 +522,9 @@ hipError_t launch_gemm_nt_stamped(const void* A, int lda, const void* B, int ldb
   return hipGetLastError();
 }
 
-// persistent NT kernel on / off (DLION_GEMM_PERSIST at build time; set_gemm_persist at run time for A/B)
-#ifndef DLION_GEMM_PERSIST
-#define DLION_GEMM_PERSIST 0
-#endif
-static int g_gemm_persist = DLION_GEMM_PERSIST;
-void set_gemm_persist(int on) { g_gemm_persist = on; }
 static int g_gemm_stagger = 0;
 void set_gemm_stagger(int units) { g_gemm_stagger = units; }
 int gemm_stagger() { return g_gemm_stagger; }
-int gemm_persist_enabled() { return g_gemm_persist; }
 
 hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
                           void* aux, int ldaux, int M, int N, int K, int epi, float* part, hipStream_t st) {
@@ -917,22 +554,6 @@ hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* 
   g.tiles_n = (N + kBN - 1) / kBN;
   g.stagger = gemm_stagger();
   const dim3 grid(g.tiles_m * g.tiles_n), block(512);
-  if (gemm_persist_enabled()) {
-    const dim3 pgrid(static_cast<unsigned>(std::min(g.tiles_m * g.tiles_n, 256)));
-    switch (epi) {
-      case 0: hipLaunchKernelGGL(gemm_nt_pkernel<0>, pgrid, block, 0, st, g); break;
-      case 1: hipLaunchKernelGGL(gemm_nt_pkernel<1>, pgrid, block, 0, st, g); break;
-      case 2: hipLaunchKernelGGL(gemm_nt_pkernel<2>, pgrid, block, 0, st, g); break;
-      case 3: hipLaunchKernelGGL(gemm_nt_pkernel<3>, pgrid, block, 0, st, g); break;
-      case 4: hipLaunchKernelGGL(gemm_nt_pkernel<4>, pgrid, block, 0, st, g); break;
-      case 5: hipLaunchKernelGGL(gemm_nt_pkernel<5>, pgrid, block, 0, st, g); break;
-      case 6: hipLaunchKernelGGL(gemm_nt_pkernel<6>, pgrid, block, 0, st, g); break;
-      case 7: hipLaunchKernelGGL(gemm_nt_pkernel<7>, pgrid, block, 0, st, g); break;
-      case 8: hipLaunchKernelGGL(gemm_nt_pkernel<8>, pgrid, block, 0, st, g); break;
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
   switch (epi) {
     case 0: hipLaunchKernelGGL(gemm_nt_kernel<0>, grid, block, 0, st, g); break;
     case 1: hipLaunchKernelGGL(gemm_nt_kernel<1>, grid, block, 0, st, g); break;

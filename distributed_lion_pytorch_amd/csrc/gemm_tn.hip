@@ -30,10 +30,6 @@
 //     fp32-partial traffic, ~11 ms per step).
 #include "common.h"
 
-// cache-policy bits of the operand LDS-DMA loads (A/B switch; 2 = nt on gfx950)
-#ifndef DLION_TN_LOAD_AUX
-#define DLION_TN_LOAD_AUX 0
-#endif
 
 namespace dlion {
 
@@ -72,7 +68,7 @@ __device__ __forceinline__ void tn_wait0() { asm volatile("s_waitcnt vmcnt(0)" :
 
 __device__ __forceinline__ void tn_glds16(const uint16_t* src, uint8_t* dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)dst, 16, 0, DLION_TN_LOAD_AUX);
+                                   (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 
 __device__ __forceinline__ tn_f32x4 tn_mfma(const tn_bf16x8& a, const tn_bf16x8& b, const tn_f32x4& c) {

@@ -26,28 +26,17 @@
 
 namespace dlion {
 
-// Tuning switches (A/B: tools/bench_lion.py with variant builds)
-#ifndef DLION_K2_NT
-#define DLION_K2_NT 0  // non-temporal p stores in the K2 fast path
-#endif
-#ifndef DLION_K2_PAIR
-#define DLION_K2_PAIR 1  // pre-voted apply: two chunks per block (one metadata chain per 16k params);
-                         // GPT-2 122 -> 113 us, Llama-3-8B unchanged (profiles/r3/lion_pair_ab.txt)
-#endif
-#ifndef DLION_K2_PAIR_MAJ
-#define DLION_K2_PAIR_MAJ 1  // the same for the majority vote over W <= 15 planes (all-gather exchange):
-                             // W=8 GPT-2 170 -> 155 us, Llama-3-8B 9.3 -> 8.5 ms (profiles/r3/lion_pair_maj_ab.txt)
-#endif
-#ifndef DLION_K2_CPB
-#define DLION_K2_CPB 2  // chunks per block of the paired apply kernels (2 or 4)
-#endif
-#ifndef DLION_K4_UNROLL
-#define DLION_K4_UNROLL 2  // K4 sliced path: words per thread per grid-stride iteration (1 or 2);
-                           // GPT-2 shard 8.1 -> 7.4 us, Llama-3-8B unchanged
-#endif
-#ifndef DLION_K4_MAXBLOCKS
-#define DLION_K4_MAXBLOCKS 2048  // K4 grid cap (grid-stride beyond)
-#endif
+// Launch shape, fixed by A/B measurement (tools/bench_lion.py, profiles/r3/):
+// * the pre-voted and majority applies run two chunks per block (one metadata
+//   chain per 16k params): GPT-2 122 -> 113 us, W=8 majority 170 -> 155 us,
+//   Llama-3-8B majority 9.3 -> 8.5 ms (profiles/r3/lion_pair_ab.txt,
+//   lion_pair_maj_ab.txt); four chunks per block and non-temporal p stores
+//   measured neutral and were removed;
+// * the sliced K4 vote loads two words per thread per grid-stride step
+//   (GPT-2 shard 8.1 -> 7.4 us) on a grid capped at 2048 blocks.
+constexpr int kPairChunks = 2;
+constexpr int kK4Unroll = 2;
+constexpr int kK4MaxBlocks = 2048;
 
 constexpr int kThreads = 256;
 constexpr int kIters = 4;
@@ -495,8 +484,7 @@ lion_vote_apply32_kernel(const int64_t* __restrict__ seg, const int64_t* __restr
         const float delta = static_cast<float>(static_cast<int>((pos >> j) & 1) - static_cast<int>((neg >> j) & 1));
         pv[j] = __fmaf_rn(neg_lr, delta, E::rnd(pv[j] * decay));
       }
-      if constexpr (DLION_K2_NT) E::store8nt(p + e, pv);
-      else E::store8(p + e, pv);
+      E::store8(p + e, pv);
     }
     return;
   }
@@ -612,7 +600,7 @@ lion_apply_pair_kernel(const int64_t* __restrict__ seg, const int64_t* __restric
                        int world, int tie, const uint8_t* __restrict__ neg_plane, float decay, float neg_lr) {
   using E = Elem<DT>;
   using S = typename E::S;
-  // CPB chunks per block (DLION_K2_CPB): every chunk's metadata chain is in
+  // CPB chunks per block (kPairChunks): every chunk's metadata chain is in
   // flight together, and when all are full every p vector (and pre-voted
   // plane word) is loaded before the first use
   const int64_t c0 = CPB * static_cast<int64_t>(blockIdx.x);
@@ -690,7 +678,7 @@ vote_reduce_kernel(const uint8_t* __restrict__ recv, int64_t nbytes, const uint8
     // (a 16-byte-per-plane variant measured slower: 31 vs 40 % of HBM at Llama-3-8B)
     const int64_t stride = (int64_t)gridDim.x * kThreads;
     int64_t w = blockIdx.x * (int64_t)kThreads + threadIdx.x;
-    if constexpr (DLION_K4_UNROLL == 2) {
+    {
       // two words per iteration, every plane load of both issued first
       // (one word per lane keeps only W dwords in flight per wave)
       for (; w + stride < nwords; w += 2 * stride) {
@@ -869,14 +857,14 @@ hipError_t launch_lion_vote_apply(int dt, const int64_t* seg, const int64_t* chu
                                   int mode, int tie, const uint8_t* neg, float decay, float neg_lr,
                                   const uint8_t* own, unsigned long long* agree, hipStream_t st) {
   if (n_chunks == 0) return hipSuccess;
-  if (DLION_K2_PAIR && mode == 2 && agree == nullptr) {
-    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_apply_pair_kernel<DT, false, DLION_K2_CPB>), dim3((n_chunks + DLION_K2_CPB - 1) / DLION_K2_CPB),
+  if (mode == 2 && agree == nullptr) {
+    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_apply_pair_kernel<DT, false, kPairChunks>), dim3((n_chunks + kPairChunks - 1) / kPairChunks),
                                           dim3(kThreads), 0, st, seg, chunks, n_chunks, planes, plane_stride, alive,
                                           world, tie, neg, decay, neg_lr));
     return hipGetLastError();
   }
-  if (DLION_K2_PAIR_MAJ && mode == 0 && world <= kMaxSliced && agree == nullptr) {
-    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_apply_pair_kernel<DT, true, DLION_K2_CPB>), dim3((n_chunks + DLION_K2_CPB - 1) / DLION_K2_CPB),
+  if (mode == 0 && world <= kMaxSliced && agree == nullptr) {
+    DLION_DISPATCH(dt, hipLaunchKernelGGL((lion_apply_pair_kernel<DT, true, kPairChunks>), dim3((n_chunks + kPairChunks - 1) / kPairChunks),
                                           dim3(kThreads), 0, st, seg, chunks, n_chunks, planes, plane_stride, alive,
                                           world, tie, neg, decay, neg_lr));
     return hipGetLastError();
@@ -910,9 +898,9 @@ hipError_t launch_vote_reduce(const uint8_t* recv, int64_t nbytes, const uint8_t
                               uint8_t* out, uint8_t* neg_out, unsigned long long* ties, hipStream_t st) {
   const int64_t nwords = nbytes >> 2;
   if (nwords == 0) return hipSuccess;
-  const int64_t per_block = static_cast<int64_t>(kThreads) * (world <= kMaxSliced ? DLION_K4_UNROLL : 1);
+  const int64_t per_block = static_cast<int64_t>(kThreads) * (world <= kMaxSliced ? kK4Unroll : 1);
   int64_t blocks = (nwords + per_block - 1) / per_block;
-  if (blocks > DLION_K4_MAXBLOCKS) blocks = DLION_K4_MAXBLOCKS;
+  if (blocks > kK4MaxBlocks) blocks = kK4MaxBlocks;
   if (world <= kMaxSliced)
     hipLaunchKernelGGL(vote_reduce_kernel<true>, dim3(blocks), dim3(kThreads), 0, st, recv, nbytes, alive, world, tie,
                        out, neg_out, ties);

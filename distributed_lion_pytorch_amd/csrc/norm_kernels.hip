@@ -41,29 +41,18 @@ __device__ __forceinline__ void ld4(const uint16_t* p, float (&o)[4]) {
   o[2] = bf16_to_f32(v.y & 0xffffu);
   o[3] = bf16_to_f32(v.y >> 16);
 }
-// DLION_NORM_NT: the residual / normalised / gradient rows leave with
-// non-temporal hints (A/B switch, see the NT GEMM's epilogue stores)
-#ifndef DLION_NORM_NT
-#define DLION_NORM_NT 0
-#endif
+// row loads / stores use the default cache policy: non-temporal hints on the
+// row streams (as on the MLP GEMM epilogues) measured neutral here
 typedef unsigned int norm_u32x2 __attribute__((ext_vector_type(2)));
-// DLION_NORM_NTLOAD: the row streams read once (x, y forward; dh, xo, dxo
-// backward) with non-temporal hints (A/B switch)
-#ifndef DLION_NORM_NTLOAD
-#define DLION_NORM_NTLOAD 0
-#endif
 __device__ __forceinline__ uint2 ldrow(const uint16_t* p) {
-  norm_u32x2 v;
-  if constexpr (DLION_NORM_NTLOAD != 0) v = __builtin_nontemporal_load(reinterpret_cast<const norm_u32x2*>(p));
-  else v = *reinterpret_cast<const norm_u32x2*>(p);
+  const norm_u32x2 v = *reinterpret_cast<const norm_u32x2*>(p);
   return make_uint2(v[0], v[1]);
 }
 __device__ __forceinline__ void st4(uint16_t* p, const float (&o)[4]) {
   norm_u32x2 v;
   v[0] = static_cast<uint32_t>(f32_to_bf16(o[0])) | (static_cast<uint32_t>(f32_to_bf16(o[1])) << 16);
   v[1] = static_cast<uint32_t>(f32_to_bf16(o[2])) | (static_cast<uint32_t>(f32_to_bf16(o[3])) << 16);
-  if constexpr (DLION_NORM_NT != 0) __builtin_nontemporal_store(v, reinterpret_cast<norm_u32x2*>(p));
-  else *reinterpret_cast<norm_u32x2*>(p) = v;
+  *reinterpret_cast<norm_u32x2*>(p) = v;
 }
 
 // Row groups: WPR waves cooperate on one row (WPR = 1 for C <= 1024; 2..8 for

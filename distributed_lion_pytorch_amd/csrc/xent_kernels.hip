@@ -11,12 +11,6 @@
 #include <cstdlib>
 #include <cstring>
 
-// DLION_XENT_NT: the packed kernel's in-place dlogits rows leave with
-// non-temporal hints (A/B switch)
-#ifndef DLION_XENT_NT
-#define DLION_XENT_NT 0
-#endif
-
 namespace dlion {
 
 constexpr int kXentThreads = 1024;
@@ -262,8 +256,7 @@ softmax_xent_packed_kernel(uint16_t* __restrict__ logits, const int64_t* __restr
       const int rel = lab - e;  // the one-hot column, if it is in this chunk
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = __expf(f[j] - mx) * inv - (rel == j ? 1.f : 0.f);
-      if constexpr (DLION_XENT_NT != 0) E::store8nt(x + e, o);
-      else E::store8(x + e, o);
+      E::store8(x + e, o);
     }
   }
   if (tid == 0) row_loss[row] = lab >= 0 ? (mx + __logf(sum)) - tgt : 0.f;

@@ -99,36 +99,3 @@ def test_gemm_nt_gelu_matches_unfused(exact):
     assert torch.equal(h, ops.bias_gelu_fwd(z_ref, bias, exact))
     ref = torch.nn.functional.gelu(_ref(a, b, bias), approximate="none" if exact else "tanh")
     _check(h, ref, K)
-
-
-@pytest.mark.parametrize("M,N,K", [(4160, 4352, 256), (5000, 3000, 384), (300, 136, 256)])
-def test_persistent_kernel_bit_identical(M, N, K):
-    """The persistent NT kernel (set_gemm_persist) runs the same MFMA chain per tile
-    and the same epilogue math as the one-tile-per-block kernel: every epilogue
-    must agree bit for bit, edge tiles and multi-tile blocks included."""
-    ops = _ops()
-    torch.manual_seed(5)
-    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
-    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
-    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
-    z = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
-
-    def run_all():
-        outs = [ops.gemm_nt(a, b, None), ops.gemm_nt(a, b, bias)]
-        for exact in (False, True):
-            outs += list(ops.gemm_nt_gelu(a, b, bias, exact))
-            outs += list(ops.gemm_nt_dgelu(a, b, bias, z, exact))
-            outs += list(ops.gemm_nt_gelu_d(a, b, bias, exact))
-        outs += list(ops.gemm_nt_dmul(a, b, z))
-        torch.cuda.synchronize()
-        return outs
-
-    prev = ops.set_gemm_persist(0)
-    try:
-        base = run_all()
-        ops.set_gemm_persist(1)
-        pers = run_all()
-    finally:
-        ops.set_gemm_persist(prev)
-    for i, (x, y) in enumerate(zip(base, pers)):
-        assert torch.equal(x, y), f"output {i}: {(x.float() - y.float()).abs().max().item()}"

@@ -44,14 +44,6 @@ def main():
         "own EPI6 gelu,gelu'": lambda: ops.gemm_nt_gelu_d(a, b, bias, False),
         "own EPI8 *gelu',colsum": lambda: ops.gemm_nt_dmul(a, b, d),
     }
-    if hasattr(ops, "set_gemm_persist"):  # the persistent kernel of the same epilogues
-        def persist(f):
-            def g():
-                prev = ops.set_gemm_persist(1)
-                f()
-                ops.set_gemm_persist(prev)
-            return g
-        variants.update({"P " + k[4:]: persist(f) for k, f in list(variants.items()) if k.startswith("own")})
     for f in variants.values():
         f()
     torch.cuda.synchronize()
