@@ -142,8 +142,10 @@ def test_run_clm_torchrun_two_ranks_one_gpu(tmp_path):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     out = str(tmp_path / "clm")
+    logs = tmp_path / "logs"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-           "--master-port", str(port), "run_clm.py", "--config_name", "gpt2-tiny",
+           "--master-port", str(port), "--log-dir", str(logs), "--redirects", "3",
+           "run_clm.py", "--config_name", "gpt2-tiny",
            "--config_overrides", "n_embd=128,n_head=2", "--synthetic_data",  # head_dim 64: the flash kernels
            "--synthetic_samples", "64", "--block_size", "128", "--per_device_train_batch_size", "2",
            "--gradient_accumulation_steps", "2", "--lion", "--async_grad", "--bf16", "--torch_dtype", "bfloat16",
@@ -152,8 +154,9 @@ def test_run_clm_torchrun_two_ranks_one_gpu(tmp_path):
            "--output_dir", out]
     env = dict(os.environ, OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=400)
-    first = [ln for ln in (r.stdout + r.stderr).splitlines() if "Error" in ln or "error" in ln][:20]
-    assert r.returncode == 0, "\n".join(first) + "\n" + r.stderr[-4000:]
+    if r.returncode != 0:  # each rank's own stderr (torchrun --redirects), not the interleaved tail
+        tails = [f"--- {f.parent.name}: " + f.read_text()[-2500:] for f in sorted(logs.rglob("stderr.log"))]
+        raise AssertionError("\n".join(tails) + "\n--- launcher: " + r.stderr[-1500:])
     recs = [json.loads(x) for x in open(os.path.join(out, "metrics.jsonl"))]
     end = [x for x in recs if "replicas_identical" in x]
     assert end and end[-1]["replicas_identical"] == 1.0 and end[-1]["world_end"] == 2.0, recs[-2:]
