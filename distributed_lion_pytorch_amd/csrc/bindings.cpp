@@ -1092,12 +1092,6 @@ TORCH_LIBRARY(dlion, m) {
       " Tensor? own, Tensor(b!)? agree) -> ()");
   m.def("vote_reduce(Tensor recv, int nbytes, Tensor alive, int tie, Tensor(a!) out, Tensor(b!)? neg_out,"
         " Tensor(c!)? ties=None) -> ()");
-  // GEMM first-round start stagger (A/B); returns the previous setting
-  m.def("set_gemm_stagger(int units) -> int", [](int64_t units) -> int64_t {
-    const int prev = dlion::gemm_stagger();
-    dlion::set_gemm_stagger(static_cast<int>(units));
-    return prev;
-  });
 }
 
 TORCH_LIBRARY_IMPL(dlion, CUDA, m) {

@@ -70,7 +70,6 @@ struct GemmArgs {
   int lda, ldb, ldc, ldaux;
   int M, N, K;
   int tiles_m, tiles_n;
-  int stagger;  // A/B: first-round start delay per CU group, in 64-cycle s_sleep units (0 = off)
 };
 
 __device__ __forceinline__ constexpr int slot(int dbuf, int ab, int half) { return ((dbuf * 2 + ab) * 2 + half) * kHalf; }
@@ -141,13 +140,6 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
   DLION_RSTAMP(st_[5])
   DLION_STAMP(st_[0])
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
-  // A/B (set_gemm_stagger): the first round's blocks of each XCD start in 4
-  // groups offset by `stagger` x 64 cycles, so the CUs' epilogue store bursts
-  // no longer coincide (blocks b and b + 8 share an XCD)
-  if (g.stagger > 0 && blockIdx.x < 256u) {
-    const int n = static_cast<int>((blockIdx.x >> 3) & 3u) * g.stagger;
-    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(1);
-  }
 
   const int tid = threadIdx.x;
   const int w = tid >> 6, lane = tid & 63;
@@ -522,9 +514,6 @@ hipError_t launch_gemm_nt_stamped(const void* A, int lda, const void* B, int ldb
   return hipGetLastError();
 }
 
-static int g_gemm_stagger = 0;
-void set_gemm_stagger(int units) { g_gemm_stagger = units; }
-int gemm_stagger() { return g_gemm_stagger; }
 
 hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
                           void* aux, int ldaux, int M, int N, int K, int epi, float* part, hipStream_t st) {
@@ -552,7 +541,6 @@ hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* 
   g.K = K;
   g.tiles_m = (M + kBM - 1) / kBM;
   g.tiles_n = (N + kBN - 1) / kBN;
-  g.stagger = gemm_stagger();
   const dim3 grid(g.tiles_m * g.tiles_n), block(512);
   switch (epi) {
     case 0: hipLaunchKernelGGL(gemm_nt_kernel<0>, grid, block, 0, st, g); break;

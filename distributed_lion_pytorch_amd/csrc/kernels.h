@@ -74,8 +74,6 @@ hipError_t launch_sum_partials_split(const float* const* ptrs, const int64_t* ro
 // aux = bf16(gelu'(z + bias)) (output); 8 C = bf16(A.B^T) * aux with aux that derivative (input)
 // and the part column sums of 4 (no bias).
 // Needs K % 128 == 0, N % 8 == 0, leading dims % 8 == 0.
-void set_gemm_stagger(int units);
-int gemm_stagger();
 hipError_t launch_gemm_nt(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
                           void* aux, int ldaux, int M, int N, int K, int epi, float* part, hipStream_t st);
 

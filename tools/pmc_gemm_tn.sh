@@ -4,7 +4,8 @@ cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp
 rm -rf gpurun_out/pmc_gemm; mkdir -p gpurun_out/pmc_gemm
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES" \
-           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM_RD SQ_INSTS_SALU"; do
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INSTS_VALU" \
+           "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   PYTHONPATH=. timeout -s KILL 90 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc_gemm -o pmc$i --pmc $grp \
     -- python3 tools/gemm_pmc_driver.py > gpurun_out/pmc_gemm/log$i.txt 2>&1 || { tail -5 gpurun_out/pmc_gemm/log$i.txt; exit 1; }
