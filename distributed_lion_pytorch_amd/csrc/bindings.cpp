@@ -826,7 +826,6 @@ std::tuple<Tensor, Tensor> gemm_nt_dgelu(const Tensor& a, const Tensor& b, const
 }
 
 // ------------------------------------------------------------- weight-gradient GEMM
-static int g_gemm_tn_tail = 1;  // A/B: split the last partial wave of an unsplit bf16 TN GEMM
 // out [splits, M, N] fp32: out[z] = sum over split z's rows of P^T Q, the rows running over the
 // concatenation of the segments P[i] [rows, M] / Q[i] [rows, N] (same shape and row stride each)
 void gemm_tn_check_launch(at::TensorList P, at::TensorList Q, int64_t splits, const Tensor& out, bool accumulate) {
@@ -860,29 +859,10 @@ void gemm_tn_check_launch(at::TensorList P, at::TensorList Q, int64_t splits, co
                 "dlion gemm_tn: out must be a contiguous fp32 [splits, M, N] tensor");
   }
   const c10::DeviceGuard g(P[0].device());
-  // unsplit bf16 output: split the last, partial wave of tiles over K (ws / cnt: see kernels.h)
-  int full_tiles = 0, tail_splits = 1;
-  Tensor ws, cnt;
-  if (bf16_out && g_gemm_tn_tail) {
-    static int cus_of[64] = {};
-    const int dev = P[0].device().index();
-    if (dev >= 0 && dev < 64 && cus_of[dev] == 0)
-      check_hip(hipDeviceGetAttribute(&cus_of[dev], hipDeviceAttributeMultiprocessorCount, dev), "CU count");
-    const int cus = dev >= 0 && dev < 64 ? cus_of[dev] : 0;
-    tail_splits = dlion::gemm_tn_tail_plan(static_cast<int>(M), static_cast<int>(N), rows * static_cast<int64_t>(P.size()),
-                                           cus, &full_tiles);
-    if (tail_splits > 1) {
-      const int64_t tail = (M + 255) / 256 * ((N + 255) / 256) - full_tiles;
-      ws = at::empty({tail * tail_splits * 65536}, out.options().dtype(at::kFloat));
-      cnt = at::zeros({tail}, out.options().dtype(at::kInt));
-    }
-  }
   check_hip(dlion::launch_gemm_tn(pp.data(), qq.data(), static_cast<int>(P.size()), rows, static_cast<int>(ldp),
                                   static_cast<int>(ldq), bf16_out ? nullptr : out.data_ptr<float>(),
                                   static_cast<int>(M), static_cast<int>(N), static_cast<int>(splits), accumulate,
-                                  cur_stream(), bf16_out ? out.data_ptr() : nullptr, full_tiles, tail_splits,
-                                  tail_splits > 1 ? ws.data_ptr<float>() : nullptr,
-                                  tail_splits > 1 ? reinterpret_cast<unsigned*>(cnt.data_ptr<int>()) : nullptr),
+                                  cur_stream(), bf16_out ? out.data_ptr() : nullptr),
             "gemm_tn");
 }
 
@@ -1112,12 +1092,6 @@ TORCH_LIBRARY(dlion, m) {
       " Tensor? own, Tensor(b!)? agree) -> ()");
   m.def("vote_reduce(Tensor recv, int nbytes, Tensor alive, int tie, Tensor(a!) out, Tensor(b!)? neg_out,"
         " Tensor(c!)? ties=None) -> ()");
-  // tail split of the unsplit bf16 TN GEMM on / off (A/B); returns the previous setting
-  m.def("set_gemm_tn_tail(int on) -> int", [](int64_t on) -> int64_t {
-    const int prev = g_gemm_tn_tail;
-    g_gemm_tn_tail = static_cast<int>(on);
-    return prev;
-  });
 }
 
 TORCH_LIBRARY_IMPL(dlion, CUDA, m) {

@@ -30,8 +30,6 @@
 //     fp32-partial traffic, ~11 ms per step).
 #include "common.h"
 
-#include <algorithm>
-
 
 namespace dlion {
 
@@ -59,14 +57,6 @@ struct TnArgs {
   int splits;
   int tiles_m, tiles_n;
   int accumulate;  // C += result (the fp32 split-K accumulators of a fusion window)
-  // tail split (bf16 output only, tail_splits > 1): tiles [0, full_tiles) of the
-  // tile order run unsplit, one block each; the remaining tiles -- the last,
-  // partial wave of blocks -- run tail_splits ways over K, park their fp32
-  // partials in ws and the last block of each tile (a per-tile counter in cnt,
-  // zero on entry and left zero) sums them in split order and runs the epilogue
-  int full_tiles, tail_splits;
-  float* ws;
-  unsigned* cnt;
 };
 
 __device__ __forceinline__ constexpr int tslot(int dbuf, int ab, int half) { return ((dbuf * 2 + ab) * 2 + half) * kTHalf; }
@@ -112,22 +102,14 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
   const int w = tid >> 6, lane = tid & 63;
   const int wr = w >> 2, wc = w & 3;
 
-  // ---- XCD-aware order over (split, tile); tiles grouped 8 M-tiles deep.  With
-  // a tail split the unsplit range [0, full_tiles) and the tail's (split, tile)
-  // range get the order separately (full_tiles % 8 == 0: block b still runs on
-  // XCD b % 8).
+  // ---- XCD-aware order over (split, tile); tiles grouped 8 M-tiles deep
   const int tiles = g.tiles_m * g.tiles_n;
+  const int nwg = tiles * g.splits;
   const int bid = blockIdx.x;
-  const bool tail = g.tail_splits > 1 && bid >= g.full_tiles;
-  const int nsplit = g.tail_splits > 1 ? (tail ? g.tail_splits : 1) : g.splits;
-  const int first = tail ? g.full_tiles : 0;  // first tile of this block's range
-  const int range = g.tail_splits > 1 ? (tail ? tiles - g.full_tiles : g.full_tiles) : tiles;
-  const int local = bid - (tail ? g.full_tiles : 0);
-  const int nwg = range * nsplit;
-  const int xcd = local & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg_all = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (local >> 3);
-  const int z = wg_all / range;
-  const int wg = first + (wg_all - z * range);
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg_all = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int z = wg_all / tiles;
+  const int wg = wg_all - z * tiles;
   constexpr int GM = 8;
   const int per_group = GM * g.tiles_n;
   const int grp = wg / per_group;
@@ -138,8 +120,8 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
   const int tn = in_g / gsz;
   const int m0 = tm * kTBM, n0 = tn * kTBN;
   // this split's k-tile pairs
-  const int p0 = static_cast<int>((static_cast<int64_t>(z) * g.kpairs) / nsplit);
-  const int p1 = static_cast<int>((static_cast<int64_t>(z + 1) * g.kpairs) / nsplit);
+  const int p0 = static_cast<int>((static_cast<int64_t>(z) * g.kpairs) / g.splits);
+  const int p1 = static_cast<int>((static_cast<int64_t>(z + 1) * g.kpairs) / g.splits);
   const int nit = p1 - p0;  // >= 1 (splits <= kpairs)
 
   // ---- staging offsets (elements, relative to the k-tile's first row).  Lane ->
@@ -167,31 +149,31 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
     }
   }
 
-  // K-tile pair bases, walked incrementally (segment changes are rare): the
-  // current pair's and the next pair's operand pointers are scalars known one
-  // iteration ahead, so no staging waits on a pointer-table load.
+  // K-tile pair bases, walked incrementally: the current pair's and the next
+  // pair's operand pointers are scalars known one iteration ahead, advanced by
+  // one pair stride; the segment pointer table is read only when the walk
+  // crosses into the next segment (a table read per pair put a scalar load and
+  // its lgkmcnt(0) wait in every iteration).
   const int seg_pairs = g.seg_kt / 2;
   int sg = p0 / seg_pairs, lc = p0 - sg * seg_pairs;
-  auto pair_base = [&](int ab, int s_, int l_) -> const uint16_t* {
-    return ab == 0 ? g.P[s_] + static_cast<int64_t>(l_) * (2 * kTBK) * g.ldp
-                   : g.Q[s_] + static_cast<int64_t>(l_) * (2 * kTBK) * g.ldq;
-  };
+  const int64_t kstepP = static_cast<int64_t>(kTBK) * g.ldp, kstepQ = static_cast<int64_t>(kTBK) * g.ldq;
+  const uint16_t* cP = g.P[sg] + lc * (2 * kstepP);
+  const uint16_t* cQ = g.Q[sg] + lc * (2 * kstepQ);
+  const uint16_t* nP = cP;
+  const uint16_t* nQ = cQ;
+  // nP / nQ <- the pair after the current next one
   auto advance = [&]() {
     if (++lc == seg_pairs) {
       ++sg;
       lc = 0;
+      nP = g.P[sg];
+      nQ = g.Q[sg];
+    } else {
+      nP += 2 * kstepP;
+      nQ += 2 * kstepQ;
     }
   };
-  const int64_t kstepP = static_cast<int64_t>(kTBK) * g.ldp, kstepQ = static_cast<int64_t>(kTBK) * g.ldq;
-  const uint16_t* cP = pair_base(0, sg, lc);
-  const uint16_t* cQ = pair_base(1, sg, lc);
-  const uint16_t* nP = cP;
-  const uint16_t* nQ = cQ;
-  if (nit > 1) {
-    advance();
-    nP = pair_base(0, sg, lc);
-    nQ = pair_base(1, sg, lc);
-  }
+  if (nit > 1) advance();
   // stage half `half` of operand ab (0 = P, 1 = Q) of the K-tile at `base` into buffer dbuf
   auto stage = [&](int ab, int half, int dbuf, const uint16_t* base) {
     uint8_t* dst = lds + tslot(dbuf, ab, half) + (2 * w) * 1024;
@@ -327,39 +309,11 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
     DLION_TN_PHASE_MATH(3)
     cP = nP;
     cQ = nQ;
-    if (it + 2 < nit) {
-      advance();
-      nP = pair_base(0, sg, lc);
-      nQ = pair_base(1, sg, lc);
-    }
+    if (it + 2 < nit) advance();
   }
 #undef DLION_TN_PHASE_MATH
 #undef DLION_TN_MFMA
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the wave groups
-
-  if (tail) {
-    // park this split's partial (lane-linear: 1 KiB per wave-instruction), then
-    // the tile's last block sums every split's partial in split order (the
-    // same sum whichever block arrives last) into its accumulators
-    const int t = wg - g.full_tiles;
-    tn_f32x4* ws = reinterpret_cast<tn_f32x4*>(g.ws) + static_cast<int64_t>(t) * g.tail_splits * (32 * 512);
-#pragma unroll
-    for (int q = 0; q < 32; ++q) ws[(z * 32 + q) * 512 + tid] = acc[q >> 2][q & 3];
-    __shared__ int last_block;
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) last_block = atomicAdd(g.cnt + t, 1u) == static_cast<unsigned>(g.tail_splits - 1);
-    __syncthreads();
-    if (!last_block) return;
-    __threadfence();
-#pragma unroll
-    for (int q = 0; q < 32; ++q) acc[q >> 2][q & 3] = ws[q * 512 + tid];
-    for (int zz = 1; zz < g.tail_splits; ++zz) {
-#pragma unroll
-      for (int q = 0; q < 32; ++q) acc[q >> 2][q & 3] += ws[(zz * 32 + q) * 512 + tid];
-    }
-    if (tid == 0) g.cnt[t] = 0u;  // zero again for the next launch
-  }
 
   // ---- epilogue: acc[mt][nt][j] = C[wr*128 + 16mt + (lane&15)][wc*64 + 16nt + 4(lane>>4) + j]
   if (g.Cb != nullptr) {  // unsplit: bf16(acc (+ old bf16)), the sum_partials rounding
@@ -414,18 +368,8 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
 
 }  // namespace
 
-int gemm_tn_tail_plan(int M, int N, int64_t rows, int cus, int* full_tiles) {
-  const int tiles = ((M + kTBM - 1) / kTBM) * ((N + kTBN - 1) / kTBN);
-  const int kpairs = static_cast<int>(rows / (2 * kTBK));
-  const int rem = cus > 0 ? tiles % cus : 0;
-  *full_tiles = tiles - rem;
-  if (rem == 0 || rem * 2 > cus || *full_tiles % 8 != 0) return 1;
-  return std::max(1, std::min({cus / rem, 8, kpairs}));
-}
-
 hipError_t launch_gemm_tn(const void* const* P, const void* const* Q, int nseg, int64_t seg_rows, int ldp, int ldq,
-                          float* C, int M, int N, int splits, bool accumulate, hipStream_t st, void* Cb,
-                          int full_tiles, int tail_splits, float* ws, unsigned* cnt) {
+                          float* C, int M, int N, int splits, bool accumulate, hipStream_t st, void* Cb) {
   if (Cb != nullptr && (splits != 1 || reinterpret_cast<uintptr_t>(Cb) % 8 != 0)) return hipErrorInvalidValue;
   if (M <= 0 || N <= 0) return hipSuccess;
   if (nseg < 1 || nseg > kMaxSeg || seg_rows <= 0 || seg_rows % (2 * kTBK) != 0) return hipErrorInvalidValue;
@@ -452,22 +396,7 @@ hipError_t launch_gemm_tn(const void* const* P, const void* const* Q, int nseg, 
   if (splits < 1 || splits > g.kpairs) return hipErrorInvalidValue;
   g.tiles_m = (M + kTBM - 1) / kTBM;
   g.tiles_n = (N + kTBN - 1) / kTBN;
-  const int tiles = g.tiles_m * g.tiles_n;
-  g.full_tiles = 0;
-  g.tail_splits = 1;
-  g.ws = nullptr;
-  g.cnt = nullptr;
-  int64_t blocks = static_cast<int64_t>(tiles) * splits;
-  if (tail_splits > 1) {
-    if (Cb == nullptr || splits != 1 || ws == nullptr || cnt == nullptr || full_tiles < 0 || full_tiles >= tiles ||
-        full_tiles % 8 != 0 || tail_splits > g.kpairs)
-      return hipErrorInvalidValue;
-    g.full_tiles = full_tiles;
-    g.tail_splits = tail_splits;
-    g.ws = ws;
-    g.cnt = cnt;
-    blocks = full_tiles + static_cast<int64_t>(tiles - full_tiles) * tail_splits;
-  }
+  const int64_t blocks = static_cast<int64_t>(g.tiles_m) * g.tiles_n * splits;
   if (blocks >= (1ll << 31)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(gemm_tn_kernel, dim3(static_cast<unsigned>(blocks)), dim3(512), 0, st, g);
   return hipGetLastError();

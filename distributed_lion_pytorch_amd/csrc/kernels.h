@@ -95,14 +95,8 @@ hipError_t launch_scale_acc(const void* x, const float* s, void* y, int64_t n, i
 // nseg segments (P_i [seg_rows, >= M] ld ldp, Q_i [seg_rows, >= N] ld ldq; bf16, 16-byte aligned).
 // Needs seg_rows % 128 == 0, M % 8 == N % 8 == 0, 1 <= splits <= nseg * seg_rows / 128, nseg <= 16.
 // Cb non-null (splits == 1): C ignored, Cb [M, N] bf16 (+)= bf16(P^T Q) instead (the gradient itself).
-// Tail split (Cb only): tiles [0, full_tiles) run unsplit, the rest tail_splits ways over K with
-// their fp32 partials in ws (tail tiles x tail_splits x 256 KiB) and per-tile counters cnt (tail
-// tiles, zero on entry, left zero); gemm_tn_tail_plan picks (full_tiles, tail_splits) for a grid of
-// `cus` compute units: a last wave of at most half the CUs is split to fill them (1 = no tail split).
 hipError_t launch_gemm_tn(const void* const* P, const void* const* Q, int nseg, int64_t seg_rows, int ldp, int ldq,
-                          float* C, int M, int N, int splits, bool accumulate, hipStream_t st, void* Cb = nullptr,
-                          int full_tiles = 0, int tail_splits = 1, float* ws = nullptr, unsigned* cnt = nullptr);
-int gemm_tn_tail_plan(int M, int N, int64_t rows, int cus, int* full_tiles);
+                          float* C, int M, int N, int splits, bool accumulate, hipStream_t st, void* Cb = nullptr);
 
 // diagnostic build of the plain GEMM with per-block timestamps (tools/gemm_stamps.py)
 hipError_t launch_gemm_nt_stamped(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,

@@ -327,38 +327,23 @@ _TN_CU_RATE = 4.9e12  # FLOP/s of one CU in the TN kernel (1.25 PF/s over 256 CU
 _TN_BW = 5.0e12  # B/s for the fp32 partials (written once, read once by the reduction)
 
 
-def tn_tail_plan(M: int, R: int, C: int) -> tuple:
-    """csrc/gemm_tn.hip gemm_tn_tail_plan for the unsplit bf16-output launch:
-    (full tiles, splits of the remaining tiles).  A last wave of at most half
-    the CUs is split over the tokens so its blocks fill the CUs (their fp32
-    partials summed by the tile's last block): Llama-3-8B q/k/v 384 tiles ->
-    256 + 128 x 2, down_proj 896 -> 768 + 128 x 2."""
-    tiles = math.ceil(R / 256) * math.ceil(C / 256)
-    rem = tiles % _TN_WAVE
-    if rem == 0 or 2 * rem > _TN_WAVE:
-        return tiles, 1
-    return tiles - rem, max(1, min(_TN_WAVE // rem, 8, M // 128))
-
-
 def tn_split_factor(M: int, R: int, C: int, max_split: int = 16, direct: bool = False) -> int:
     """Splits of the token axis for the own TN kernel: minimises waves of
     (256x256 tiles x splits) blocks x per-block time + the fp32 partial
     traffic (splits x R x C x 8 bytes).  GPT-2 c_fc: 7 (252 blocks, one wave),
     c_attn: 9; the LM head's 591 tiles: 3 (7 waves instead of 3 long ones).
-    direct: the unsplit launch writes the bf16 gradient itself (no partials)
-    and splits only its last partial wave (tn_tail_plan), so Llama-sized
-    weights take s = 1 (q/k/v and down_proj used to pick 2 for the wave
-    quantisation and paid 0.5 GB of fp32 partials each)."""
+    direct: the unsplit launch writes the bf16 gradient itself (no fp32
+    partials, no reduction pass), and a last wave that holds only part of
+    the CUs runs ~0.7 x a full wave's time (the blocks get the chip's HBM and
+    power to themselves): Llama-3-8B down_proj (896 tiles) 810 us unsplit vs
+    814 + 108 us at s = 2 (tools/r5/bench_tn_llama.py, profiles/r5/)."""
     tiles = math.ceil(R / 256) * math.ceil(C / 256)
     best, best_cost = 1, None
     t_full = (2.0 * 65536 * M) / _TN_CU_RATE
     for s in range(1, max(1, min(max_split, M // 128)) + 1):
         if direct and s == 1:
-            full, ts = tn_tail_plan(M, R, C)
-            cost = (full // _TN_WAVE) * t_full
-            if full < tiles:
-                cost += (t_full / ts if ts > 1 else t_full) + (16.0 * 65536 * (tiles - full) * ts / _TN_BW
-                                                                 if ts > 1 else 0.0)
+            full_waves, rem = divmod(tiles, _TN_WAVE)
+            cost = (full_waves + (0.7 if rem else 0.0)) * t_full
         else:
             waves = math.ceil(tiles * s / _TN_WAVE)
             cost = waves * (2.0 * 65536 * M / s) / _TN_CU_RATE + 8.0 * s * R * C / _TN_BW

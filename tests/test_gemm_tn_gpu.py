@@ -147,70 +147,18 @@ def test_gemm_tn_bf16_out_matches_fp32(cuda, M, N, rows, nseg):
     P = [torch.randn(rows, M, device=cuda, dtype=torch.bfloat16) for _ in range(nseg)]
     Q = [torch.randn(rows, N, device=cuda, dtype=torch.bfloat16) for _ in range(nseg)]
     ref = torch.cat(P).float().t() @ torch.cat(Q).float()
-    ops = hip.ops()
-    prev = ops.set_gemm_tn_tail(0)  # one block per tile (no tail split)
-    try:
-        out = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
-        ops.gemm_tn_(P, Q, out, False)
-        assert (out.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
-        # same rounding as the fp32-partial path it replaces
-        part = ops.gemm_tn(P, Q, 1)
-        assert torch.equal(out, ops.sum_partials(part.view(1, -1)).view(M, N))
-        old = torch.randn(M, N, device=cuda, dtype=torch.bfloat16)
-        acc = old.clone()
-        ops.gemm_tn_(P, Q, acc, True)
-        exp = old.clone()
-        ops.sum_partials_acc_(part.view(1, -1), exp.view(-1))
-        assert torch.equal(acc, exp)
-    finally:
-        ops.set_gemm_tn_tail(prev)
-
-
-def _tail_plan(M, N, rows):
-    """csrc/gemm_tn.hip gemm_tn_tail_plan: (full tiles, splits of the rest)."""
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
-    tiles = -(-M // 256) * -(-N // 256)
-    rem = tiles % cus
-    if rem == 0 or 2 * rem > cus:
-        return tiles, 1
-    return tiles - rem, max(1, min(cus // rem, 8, rows // 128))
-
-
-@pytest.mark.parametrize("M,N,rows,nseg", [(256, 256, 128, 1), (776, 264, 256, 2), (1024, 4096, 1024, 1),
-                                           (4096, 4352, 512, 1), (6144, 4096, 256, 2)])
-def test_gemm_tn_bf16_tail_split(cuda, M, N, rows, nseg):
-    """Unsplit bf16 output with the last partial wave of tiles split over K:
-    the tail tiles equal the fp32 split-partial path at the tail's split count
-    (same k ranges, partials summed in split order, one rounding), the other
-    tiles the unsplit path -- bit for bit, plain and accumulating -- and the
-    per-tile counters are left zero (a second launch gives the same bits)."""
-    hip.require()
-    torch.manual_seed(4)
-    ops = hip.ops()
-    P = [torch.randn(rows, M, device=cuda, dtype=torch.bfloat16) for _ in range(nseg)]
-    Q = [torch.randn(rows, N, device=cuda, dtype=torch.bfloat16) for _ in range(nseg)]
-    full, ts = _tail_plan(M, N, rows * nseg)
-    old = torch.randn(M, N, device=cuda, dtype=torch.bfloat16)
-    exp_s1, exp_ts = old.clone(), old.clone()
-    ops.sum_partials_acc_(ops.gemm_tn(P, Q, 1).view(1, -1), exp_s1.view(-1))
-    ops.sum_partials_acc_(ops.gemm_tn(P, Q, ts).view(ts, -1), exp_ts.view(-1))
-    # which tiles are in the tail: the kernel's grouped tile order (8 M-tiles deep)
-    tm_n, tn_n = -(-M // 256), -(-N // 256)
-    tail_mask = torch.zeros(M, N, dtype=torch.bool, device=cuda)
-    for wg in range(full, tm_n * tn_n):
-        grp, in_g = divmod(wg, 8 * tn_n)
-        gsz = min(tm_n - 8 * grp, 8)
-        tm, tn = 8 * grp + in_g % gsz, in_g // gsz
-        tail_mask[256 * tm:256 * (tm + 1), 256 * tn:256 * (tn + 1)] = True
-    exp = torch.where(tail_mask, exp_ts, exp_s1)
-    for _ in range(2):
-        acc = old.clone()
-        ops.gemm_tn_(P, Q, acc, True)
-        assert torch.equal(acc, exp), (full, ts)
-    out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
-    ops.gemm_tn_(P, Q, out, False)
-    ref = torch.cat(P).float().t() @ torch.cat(Q).float()
+    out = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+    hip.ops().gemm_tn_(P, Q, out, False)
     assert (out.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    # same rounding as the fp32-partial path it replaces
+    part = hip.ops().gemm_tn(P, Q, 1)
+    assert torch.equal(out, hip.ops().sum_partials(part.view(1, -1)).view(M, N))
+    old = torch.randn(M, N, device=cuda, dtype=torch.bfloat16)
+    acc = old.clone()
+    hip.ops().gemm_tn_(P, Q, acc, True)
+    exp = old.clone()
+    hip.ops().sum_partials_acc_(part.view(1, -1), exp.view(-1))
+    assert torch.equal(acc, exp)
 
 
 def test_unsplit_wgrad_into_and_fused_projection_grads(cuda):

@@ -31,13 +31,6 @@ for name, R, C in [("o", 4096, 4096), ("qkv", 6144, 4096), ("down", 4096, 14336)
     line = f"{name:8s} [{R}x{C}] "
     t1 = timeit(lambda: ops.gemm_tn_([dy], [x], out, False))
     line += f"TN s=1 bf16 {t1:7.1f}us {flop / t1 / 1e9:4.2f}PF"
-    prev = ops.set_gemm_tn_tail(0)
-    ref = torch.empty_like(out)
-    t0 = timeit(lambda: ops.gemm_tn_([dy], [x], ref, False))
-    ops.set_gemm_tn_tail(prev)
-    ops.gemm_tn_([dy], [x], out, False)
-    err = ((out.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
-    line += f" (no tail split {t0:7.1f}us, rel diff {err:.1e})"
     for s in (2, 3, 4):
         part = torch.empty(s, R, C, device="cuda", dtype=torch.float32)
         ts = timeit(lambda: ops.gemm_tn_([dy], [x], part, False))
