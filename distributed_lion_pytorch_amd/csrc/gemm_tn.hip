@@ -155,8 +155,8 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
   // crosses into the next segment (a table read per pair put a scalar load and
   // its lgkmcnt(0) wait in every iteration).
   const int seg_pairs = g.seg_kt / 2;
-  int sg = p0 / seg_pairs, lc = p0 - sg * seg_pairs;
   const int64_t kstepP = static_cast<int64_t>(kTBK) * g.ldp, kstepQ = static_cast<int64_t>(kTBK) * g.ldq;
+  int sg = p0 / seg_pairs, lc = p0 - sg * seg_pairs;
   const uint16_t* cP = g.P[sg] + lc * (2 * kstepP);
   const uint16_t* cQ = g.Q[sg] + lc * (2 * kstepQ);
   const uint16_t* nP = cP;
