@@ -1080,6 +1080,7 @@ def _lm_dgrad(g: torch.Tensor, weight: torch.Tensor, wp: torch.Tensor) -> torch.
 _LM_TN = os.environ.get("DLION_LM_TN", "1") != "0"  # A/B switch for _lm_wgrad_partials
 _LM_FWD_OWN = os.environ.get("DLION_LM_FWD_OWN", "0") == "1"  # A/B switch: LM-head logits on the own NT GEMM
 _LM_DEFER = os.environ.get("DLION_LM_DEFER", "1") != "0"  # LM-head weight gradient in the window-level TN GEMM
+_LM_LATE = os.environ.get("DLION_LM_LATE", "1") != "0"  # unsplit LM-head weight gradient in the backward (bf16)
 
 
 def _lm_wgrad_partials(g: torch.Tensor, h2d: torch.Tensor, v: int):
@@ -1137,6 +1138,17 @@ class _LMHeadCE(torch.autograd.Function):
                 ctx.has_dw = True
                 ctx.weight = weight
                 return loss
+            if ctx.needs_input_grad[1] and _lm_late_ok(weight, logits, h2d, v):
+                # unsplit (Llama-sized head): the backward runs one TN GEMM of
+                # (softmax - onehot) against s * h writing the bf16 gradient itself --
+                # no fp32 [Vp, C] partials between the passes, no reduction pass
+                ctx.save_for_backward(dh, logits, n_valid, h2d)
+                ctx.late = True
+                ctx.v = v
+                from .linear import _fuse_target
+
+                ctx.weight = weight if _fuse_target(weight) else None
+                return loss
             if ctx.needs_input_grad[1]:
                 dw = _lm_wgrad_partials(logits, h2d, v)
                 ctx.dw_parts = dw is not None
@@ -1154,6 +1166,8 @@ class _LMHeadCE(torch.autograd.Function):
     def backward(ctx, g):
         if getattr(ctx, "defer", False):
             return _LMHeadCE._backward_deferred(ctx, g)
+        if getattr(ctx, "late", False):
+            return _LMHeadCE._backward_late(ctx, g)
         dh, dw, n_valid = ctx.saved_tensors
         if not (dh.is_cuda and dh.dtype == torch.bfloat16 and _use_hip(dh)):
             scale = (g / n_valid).to(dh.dtype)
@@ -1215,6 +1229,49 @@ class _LMHeadCE(torch.autograd.Function):
             part = ops.gemm_tn([logits], [hs], split)  # over budget / window closed: now
             linear.deposit_grad(w, part.view(split, -1)[:, : v * c], defer=False)
         return gh, None, None, None
+
+
+    @staticmethod
+    def _backward_late(ctx, g):
+        """Backward of an unsplit head: w.grad (+)= bf16((softmax - onehot)^T (s h))
+        from the TN kernel's bf16 epilogue (the window path's operand scaling)."""
+        dh, logits, n_valid, h2d = ctx.saved_tensors
+        s = (g.float() / n_valid).reshape(1)
+        ops = hip.ops()
+        gh = gw = None
+        if ctx.needs_input_grad[0]:
+            gh = torch.empty_like(dh)
+            ops.scale_acc_(dh, s, gh, False)
+        hs = torch.empty_like(h2d)
+        ops.scale_acc_(h2d.contiguous(), s, hs, False)
+        lv = logits[:, : ctx.v]  # row stride Vp: the vocabulary padding is never read
+        w = ctx.weight
+        if w is not None and w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:
+            ops.gemm_tn_([lv], [hs], w.grad, True)
+        else:
+            out = torch.empty(ctx.v, h2d.shape[1], dtype=torch.bfloat16, device=h2d.device)
+            ops.gemm_tn_([lv], [hs], out, False)
+            if w is not None:
+                w.grad = out if w.grad is None else w.grad + out
+            else:
+                gw = out
+        return gh, gw, None, None
+
+
+def _lm_late_ok(weight, logits, h2d, v) -> bool:
+    """The head's weight gradient runs unsplit in the backward (bf16 straight
+    from the TN kernel): a bf16 weight, v % 8 == 0 (the kernel reads the
+    unpadded columns of the padded logits), TN-eligible operands, and the split
+    model choosing one split for the unsplit launch (Llama-3-8B's 128256 x 4096:
+    7.4 ms GEMM + 0.6 ms partial reduction before)."""
+    from . import linear
+
+    if not (_LM_TN and _LM_LATE and logits.is_cuda and weight.dtype == torch.bfloat16 and v % 8 == 0
+            and hip.available()):
+        return False
+    lv = logits[:, :v]
+    return (linear._tn_eligible(lv, h2d)
+            and linear.tn_split_factor(logits.shape[0], v, h2d.shape[1], direct=True) == 1)
 
 
 def _lm_defer_ok(weight, logits, h2d) -> bool:

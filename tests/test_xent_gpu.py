@@ -95,3 +95,36 @@ def test_lm_head_ce_weight_grad_on_tn_kernel(cuda, preexisting_grad):
     want = wr.grad + (g0.float() if g0 is not None else 0.0)
     assert (w.grad.float() - want).abs().max().item() < 2e-2 * want.abs().max().item() + 1e-4
     assert (h.grad.float() - hr.grad).abs().max().item() < 2e-2 * hr.grad.abs().max().item() + 1e-4
+
+
+@pytest.mark.parametrize("preexisting_grad", [False, True])
+def test_lm_head_ce_late_unsplit_weight_grad(cuda, preexisting_grad, monkeypatch):
+    """Llama-3 vocabulary (128256, % 8 == 0) and a head the split model runs
+    unsplit: the weight gradient is computed in the backward by one TN GEMM of
+    the padded logits' first v columns against s * h, bf16 straight into (or
+    onto) .grad (ops/fused._LMHeadCE._backward_late)."""
+    from distributed_lion_pytorch_amd.ops import linear
+
+    hip.require()
+    torch.manual_seed(5)
+    V, C = 128256, 256
+    assert linear.tn_split_factor(256, V, C, direct=True) == 1
+    h = torch.randn(2, 128, C, device=cuda).bfloat16().requires_grad_()
+    w = torch.nn.Parameter((0.05 * torch.randn(V, C, device=cuda)).bfloat16())
+    g0 = (0.01 * torch.randn(V, C, device=cuda)).bfloat16() if preexisting_grad else None
+    if g0 is not None:
+        w.grad = g0.clone()
+    labels = torch.randint(0, V, (2, 128), device=cuda)
+    labels[0, :5] = -100
+    calls = []
+    late = fused._LMHeadCE._backward_late
+    monkeypatch.setattr(fused._LMHeadCE, "_backward_late", staticmethod(lambda ctx, g: calls.append(1) or late(ctx, g)))
+    loss = 2.5 * fused.lm_head_cross_entropy(h, w, labels)
+    loss.backward()
+    assert calls == [1]
+    hr, wr = h.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    ref = 2.5 * torch.nn.functional.cross_entropy((hr @ wr.t()).view(-1, V), labels.view(-1))
+    ref.backward()
+    want = wr.grad + (g0.float() if g0 is not None else 0.0)
+    assert (w.grad.float() - want).abs().max().item() < 2e-2 * want.abs().max().item() + 1e-4
+    assert (h.grad.float() - hr.grad).abs().max().item() < 2e-2 * hr.grad.abs().max().item() + 1e-4
