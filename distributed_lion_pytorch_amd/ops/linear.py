@@ -896,12 +896,25 @@ _CAT_CACHE: dict = {}  # tuple(id(w)) -> (weakrefs, key, concatenated weight)
 
 def cat_weights(ws) -> torch.Tensor:
     """[W1; W2; ...] along the output dim, cached until any of them changes
-    (in place, or via the next Lion step: see bump_weight_generation)."""
+    (in place, or via the next Lion step: see bump_weight_generation).  When
+    the weights are consecutive row blocks of one buffer (pack_projections)
+    the result is that buffer's view -- no copy at all."""
     import weakref
 
     if len(ws) == 1:
         return ws[0]
     ck = tuple(id(w) for w in ws)
+    adj = _adjacent_rows([w.detach() for w in ws])
+    if adj is not None:
+        # one stable view object per weight set (the W^T cache is keyed by it)
+        hit = _CAT_CACHE.get(ck)
+        if (hit is not None and all(r() is w for r, w in zip(hit[0], ws)) and hit[1] == "adjacent"
+                and hit[2].data_ptr() == adj.data_ptr() and hit[2].shape == adj.shape):
+            return hit[2]
+        if hit is None:
+            weakref.finalize(ws[0], _CAT_CACHE.pop, ck, None)
+        _CAT_CACHE[ck] = ([weakref.ref(w) for w in ws], "adjacent", adj)
+        return adj
     # the optimizer's kernels write trainable weights through raw pointers (no
     # _version bump): those are re-concatenated after every step; frozen ones
     # (LoRA base weights, a DPO reference model) stay cached -- the re-cat of a
@@ -913,7 +926,7 @@ def cat_weights(ws) -> torch.Tensor:
     if same and hit[1] == key:
         return hit[2]
     with torch.no_grad():
-        old = hit[2] if same else None
+        old = hit[2] if same and hit[1] != "adjacent" else None
         if (old is not None and old.dtype == ws[0].dtype and old.shape[0] == sum(w.shape[0] for w in ws)
                 and old.shape[1:] == ws[0].shape[1:]):
             # refreshed in place after an optimizer step (trainable Llama q/k/v, gate/up):
@@ -1066,6 +1079,34 @@ def _adjacent_rows(ts):
     return t0.as_strided((off,) + tuple(t0.shape[1:]), t0.stride())
 
 
+_PACK_PROJ = os.environ.get("DLION_PACK_PROJ", "1") != "0"  # A/B switch for pack_projections
+
+
+def pack_projections(ws) -> bool:
+    """Re-point trainable weights that one fused GEMM uses together (Llama
+    q/k/v, gate/up) at consecutive row blocks of ONE buffer, so that their
+    concatenation is a view instead of a per-step copy (Llama-3-8B: 64 copies,
+    ~3.5 ms per step).  Done once, on first fused use on the GPU (after
+    `.to(device)`; a later `.to()` that moves them apart just brings the copy
+    back).  Safe for the optimizers (the Lion pointer tables follow data_ptr,
+    others hold the Parameter objects), for load_state_dict (copies in place)
+    and for save_pretrained (disjoint views of one storage are cloned on save).
+    Returns True when the weights are (now) adjacent."""
+    if _adjacent_rows([w.detach() for w in ws]) is not None:
+        return True
+    if not (_PACK_PROJ and len(ws) > 1 and all(isinstance(w, torch.nn.Parameter) and w.requires_grad and w.is_cuda
+                                                and w.is_contiguous() for w in ws)
+            and len({(w.dtype, w.device, tuple(w.shape[1:])) for w in ws}) == 1):
+        return False
+    with torch.no_grad():
+        buf = torch.cat([w.detach() for w in ws], 0)
+        off = 0
+        for w in ws:
+            w.data = buf[off:off + w.shape[0]]
+            off += w.shape[0]
+    return True
+
+
 def linear_multi_nk(x: torch.Tensor, ws) -> tuple:
     """(x @ W1^T, x @ W2^T, ...) for nn.Linear-layout weights sharing the input
     x, as one fused GEMM (CUDA) -- outputs are column views of one buffer."""
@@ -1073,6 +1114,7 @@ def linear_multi_nk(x: torch.Tensor, ws) -> tuple:
     lead = x.shape[:-1]
     if not x.is_cuda:
         return tuple(torch.nn.functional.linear(x2d, w).view(lead + (w.shape[0],)) for w in ws)
+    pack_projections(ws)
     x2d, *ws = autocast_inputs(x2d, *ws)
     with torch.autocast("cuda", enabled=False):
         outs = _LinearMultiNK.apply(x2d, *ws)

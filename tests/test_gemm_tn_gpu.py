@@ -213,6 +213,47 @@ def test_cat_weights_refreshes_in_place_after_step(cuda):
     assert c2.data_ptr() == ptr and torch.equal(c2, torch.cat([w.detach() for w in ws]))
 
 
+def test_pack_projections_zero_copy_fused_weights(cuda):
+    """Trainable q/k/v-style weights are re-pointed at one buffer on first fused
+    use: the concatenation is then a view (no per-step copy), the HIP Lion step
+    -- whose pointer table was built before the move -- updates the new storage,
+    and the state dict still round-trips."""
+    from distributed_lion_pytorch_amd import Lion
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    torch.manual_seed(11)
+    ws = [torch.nn.Parameter((0.02 * torch.randn(n, 256, device=cuda)).to(torch.bfloat16)) for n in (256, 128, 128)]
+    opt = Lion(ws, lr=1e-2, weight_decay=0.0)
+    x = torch.randn(384, 256, device=cuda, dtype=torch.bfloat16)
+    for w in ws:
+        w.grad = torch.randn_like(w)
+    opt.step()  # plan + pointer table on the original storage
+    before = [w.detach().clone() for w in ws]
+    outs = L.linear_multi_nk(x, ws)  # packs
+    assert L._adjacent_rows([w.detach() for w in ws]) is not None
+    for o, w in zip(outs, before):
+        ref = x.float() @ w.float().t()
+        assert (o.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+    cat = L.cat_weights(ws)
+    assert cat.data_ptr() == ws[0].data_ptr() and L.cat_weights(ws) is cat
+    grads = [torch.randn_like(w) for w in ws]
+    for w, g in zip(ws, grads):
+        w.grad = g.clone()
+    opt.step()  # must write through the new pointers
+    for w, b0 in zip(ws, before):
+        assert not torch.equal(w.detach(), b0), "the step did not reach the packed storage"
+    L.bump_weight_generation()
+    assert torch.equal(L.cat_weights(ws), torch.cat([w.detach() for w in ws]))
+    sd = {f"w{i}": w.detach().clone() for i, w in enumerate(ws)}
+    with torch.no_grad():
+        for w in ws:
+            w.zero_()
+        for i, w in enumerate(ws):
+            w.copy_(sd[f"w{i}"])
+    assert all(torch.equal(w.detach(), sd[f"w{i}"]) for i, w in enumerate(ws))
+
+
 def test_gemm_autotune_candidates_agree(cuda):
     """Every candidate the per-shape GEMM choice may pick (ATen NN/NT, own NT,
     tuned hipBLASLt) computes the same product; the pick is cached per shape."""
