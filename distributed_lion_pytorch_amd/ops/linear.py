@@ -1094,6 +1094,8 @@ def pack_projections(ws) -> bool:
     Returns True when the weights are (now) adjacent."""
     if _adjacent_rows([w.detach() for w in ws]) is not None:
         return True
+    if torch.is_inference_mode_enabled():  # the new buffer would be an inference tensor, unusable for training
+        return False
     if not (_PACK_PROJ and len(ws) > 1 and all(isinstance(w, torch.nn.Parameter) and w.requires_grad and w.is_cuda
                                                 and w.is_contiguous() for w in ws)
             and len({(w.dtype, w.device, tuple(w.shape[1:])) for w in ws}) == 1):
