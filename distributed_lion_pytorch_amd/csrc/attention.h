@@ -31,7 +31,6 @@ struct AttnArgs {
   uint32_t thresh16; // dropout threshold (keep if u16 >= thresh16), 0 = no dropout
   float inv_keep;
   uint32_t seed;
-  int delta_ready;  // the backward's delta was computed by attn_delta_kernel (dQ reads it)
 };
 
 }  // namespace dlion

@@ -28,8 +28,6 @@
 // 16-bit resolution, so forward and both backward kernels regenerate the
 // identical mask in any register layout.
 #include "common.h"
-
-#include <cstdlib>
 #include "attention.h"
 
 // Occupancy floors (waves per SIMD), A/B-measured (profiles/r3/attn_occupancy_ab.txt):
@@ -527,42 +525,6 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 // ring; NT key tiles per barrier (see the forward; dQ runs NT = 1: NT = 2 was
 // 4 % slower, profiles/r4/attn_dq_nt2_ab.txt).  (Round 3's software-pipelined
 // and sequential-NT variants measured neutral and were removed.)
-// delta = rowsum(dO * O) of the lane's row (lanes r and r + 32 hold its two
-// halves, dof = the lane's dO fragments), scaled by 1-p under dropout (see the
-// forward's lse note); the same operation order in both callers
-template <int D>
-__device__ __forceinline__ float delta_rows(const AttnArgs& a, const bf16x8 (&dof)[D / 16], int b, int h, int qc) {
-  const int hf = (threadIdx.x & 63) >> 5;
-  const __bf16* op = a.o + b * a.o_sb + static_cast<int64_t>(qc) * a.o_st + h * a.o_sh + 8 * hf;
-  float part = 0.f;
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
-    const bf16x8 of = ld8(op + 16 * s);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) part += static_cast<float>(of[j]) * static_cast<float>(dof[s][j]);
-  }
-  float dlt = xsum32(part);
-  if (a.thresh16) dlt /= a.inv_keep;
-  return dlt;
-}
-
-// delta pre-pass for the concurrent backward (dQ and dK/dV on two streams):
-// one wave per 32 query rows, QBlock's grid
-template <int D>
-__global__ void __launch_bounds__(256) attn_delta_kernel(AttnArgs a) {
-  const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
-  const QBlock blk(a.B * a.H, ntiles32(a.T));
-  if (!blk.active) return;
-  const int bh = blk.bh, b = bh / a.H, h = bh % a.H;
-  const int q = blk.qtile * 32 + r, qc = min(q, a.T - 1);
-  bf16x8 dof[D / 16];
-  const __bf16* dop = a.dout + b * a.o_sb + static_cast<int64_t>(qc) * a.o_st + h * a.o_sh + 8 * hf;
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) dof[s] = ld8(dop + 16 * s);
-  const float dlt = delta_rows<D>(a, dof, b, h, qc);
-  if (hf == 0 && q < a.T) const_cast<float*>(a.delta)[static_cast<int64_t>(bh) * a.T + q] = dlt;
-}
-
 template <int D, bool DROP, int NT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? DLION_DQ_WAVES64 : 1)))
 attn_bwd_dq_kernel(AttnArgs a) {
@@ -588,16 +550,21 @@ attn_bwd_dq_kernel(AttnArgs a) {
       dof[s] = ld8(dop + 16 * s);
     }
     lse2 = a.lse[static_cast<int64_t>(bh) * a.T + qc];
-    if (a.delta_ready) {
-      dlt = a.delta[static_cast<int64_t>(bh) * a.T + qc];
-    } else {
-      // delta = rowsum(dO * O) for this wave's 32 rows, computed here (the dQ
-      // kernel already holds the dO rows) and published for the dKV kernel that
-      // runs next -- instead of a separate pass over O and dO.  Lanes r and r+32
-      // hold the two halves of row q.
-      dlt = delta_rows<D>(a, dof, b, h, qc);
-      if (hf == 0 && q < a.T) const_cast<float*>(a.delta)[static_cast<int64_t>(bh) * a.T + q] = dlt;
+    // delta = rowsum(dO * O) for this wave's 32 rows, computed here (the dQ
+    // kernel already holds the dO rows) and published for the dKV kernel that
+    // runs next -- instead of a separate pass over O and dO.  Lanes r and r+32
+    // hold the two halves of row q.
+    const __bf16* op = a.o + b * a.o_sb + static_cast<int64_t>(qc) * a.o_st + h * a.o_sh + 8 * hf;
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      const bf16x8 of = ld8(op + 16 * s);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += static_cast<float>(of[j]) * static_cast<float>(dof[s][j]);
     }
+    dlt = xsum32(part);
+    if (a.thresh16) dlt /= a.inv_keep;  // delta * (1-p), see the forward's lse note
+    if (hf == 0 && q < a.T) const_cast<float*>(a.delta)[static_cast<int64_t>(bh) * a.T + q] = dlt;
   }
   const uint32_t arow = drop_row(a.seed, bh, q), hoff = static_cast<uint32_t>(2 * hf) * kKeyMul;
   const uint32_t tm1 = drop_tm1(a.thresh16);
@@ -935,65 +902,17 @@ hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
   return hipGetLastError();
 }
 
-static int g_attn_bwd_concurrent = [] {
-  const char* e = std::getenv("DLION_ATTN_BWD_CONCURRENT");
-  return e != nullptr && e[0] == '1' ? 1 : 0;
-}();
-void set_attn_bwd_concurrent(int on) { g_attn_bwd_concurrent = on; }
-int attn_bwd_concurrent() { return g_attn_bwd_concurrent; }
-
-namespace {
-// per-device side stream + fork / join events of the concurrent backward
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-hipError_t side_stream(SideStream** out) {
-  static SideStream ss[64];
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess || dev < 0 || dev >= 64) return e != hipSuccess ? e : hipErrorInvalidDevice;
-  SideStream& x = ss[dev];
-  if (x.s == nullptr) {
-    if ((e = hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&x.fork, hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&x.join, hipEventDisableTiming)) != hipSuccess) return e;
-  }
-  *out = &x;
-  return hipSuccess;
-}
-}  // namespace
-
-hipError_t launch_attn_bwd(const AttnArgs& a0, int D, bool drop, hipStream_t st) {
-  const dim3 bq(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a0.B) * a0.H, a0.T)));
-  const dim3 bkv(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a0.B) * a0.Hkv, a0.T)));
-  AttnArgs a = a0;
-  a.delta_ready = 0;
-  hipStream_t skv = st;  // dK/dV's stream
-  SideStream* ss = nullptr;
-  if (g_attn_bwd_concurrent) {
-    // delta first, then dK/dV on the side stream concurrently with dQ: the two
-    // latency-bound kernels share the CUs instead of running back to back
-    hipError_t e = side_stream(&ss);
-    if (e != hipSuccess) return e;
-    if (D == 64) hipLaunchKernelGGL((attn_delta_kernel<64>), bq, dim3(256), 0, st, a);
-    else if (D == 128) hipLaunchKernelGGL((attn_delta_kernel<128>), bq, dim3(256), 0, st, a);
-    else return hipErrorInvalidValue;
-    a.delta_ready = 1;
-    if ((e = hipEventRecord(ss->fork, st)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(ss->s, ss->fork, 0)) != hipSuccess) return e;
-    skv = ss->s;
-  }
-  // sequential: dQ first, it also computes delta = rowsum(dO * O), which dKV reads
+hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) {
+  const dim3 bq(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T)));
+  const dim3 bkv(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.Hkv, a.T)));
+  // dQ first: it also computes delta = rowsum(dO * O), which dKV reads
 #define BWD(DD)                                                                         \
   if (drop) {                                                                           \
-    if (ss) hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), bkv, dim3(256), 0, skv, a); \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, true, 1>), bq, dim3(256), 0, st, a);    \
-    if (!ss) hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), bkv, dim3(256), 0, skv, a); \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), bkv, dim3(256), 0, st, a);     \
   } else {                                                                              \
-    if (ss) hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), bkv, dim3(256), 0, skv, a); \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, false, 1>), bq, dim3(256), 0, st, a);   \
-    if (!ss) hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), bkv, dim3(256), 0, skv, a); \
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), bkv, dim3(256), 0, st, a);    \
   }
   if (D == 64) {
     BWD(64)
@@ -1003,11 +922,7 @@ hipError_t launch_attn_bwd(const AttnArgs& a0, int D, bool drop, hipStream_t st)
     return hipErrorInvalidValue;
   }
 #undef BWD
-  hipError_t e = hipGetLastError();
-  if (e == hipSuccess && ss != nullptr) {
-    if ((e = hipEventRecord(ss->join, ss->s)) == hipSuccess) e = hipStreamWaitEvent(st, ss->join, 0);
-  }
-  return e;
+  return hipGetLastError();
 }
 
 }  // namespace dlion

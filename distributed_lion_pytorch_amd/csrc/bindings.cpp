@@ -1092,12 +1092,6 @@ TORCH_LIBRARY(dlion, m) {
       " Tensor? own, Tensor(b!)? agree) -> ()");
   m.def("vote_reduce(Tensor recv, int nbytes, Tensor alive, int tie, Tensor(a!) out, Tensor(b!)? neg_out,"
         " Tensor(c!)? ties=None) -> ()");
-  // attention backward: delta pre-pass + dQ || dK/dV on a side stream (A/B); returns the previous setting
-  m.def("set_attn_bwd_concurrent(int on) -> int", [](int64_t on) -> int64_t {
-    const int prev = dlion::attn_bwd_concurrent();
-    dlion::set_attn_bwd_concurrent(static_cast<int>(on));
-    return prev;
-  });
 }
 
 TORCH_LIBRARY_IMPL(dlion, CUDA, m) {

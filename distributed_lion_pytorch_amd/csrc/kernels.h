@@ -28,8 +28,6 @@ hipError_t launch_vote_reduce(const uint8_t* recv, int64_t nbytes, const uint8_t
 // ---- flash attention (attention.hip)
 hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st);
 hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st);
-void set_attn_bwd_concurrent(int on);  // A/B: delta pre-pass, then dQ || dK/dV on a side stream
-int attn_bwd_concurrent();
 
 // ---- fused residual + dropout + LayerNorm/RMSNorm (norm_kernels.hip)
 // backward: `parts` blocks (4 rows of C <= 1024, or one wide row, per block

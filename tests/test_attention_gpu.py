@@ -70,35 +70,6 @@ def test_flash_attention_fwd_bwd(B, T, H, Hkv, D, p, cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,T,H,Hkv,D,p", [(2, 200, 4, 4, 64, 0.1), (1, 256, 8, 2, 128, 0.0)])
-def test_concurrent_backward_bit_identical(B, T, H, Hkv, D, p, cuda):
-    """The concurrent backward (delta pre-pass, then dK/dV on a side stream
-    beside dQ; set_attn_bwd_concurrent) gives the sequential kernels' bits."""
-    hip.require()
-    ops = hip.ops()
-    torch.manual_seed(2)
-    q = torch.randn(B, T, H, D, device=cuda, dtype=torch.bfloat16)
-    k = torch.randn(B, T, Hkv, D, device=cuda, dtype=torch.bfloat16)
-    v = torch.randn(B, T, Hkv, D, device=cuda, dtype=torch.bfloat16)
-    dout = torch.randn(B, T, H * D, device=cuda, dtype=torch.bfloat16)
-    grads = []
-    prev = ops.set_attn_bwd_concurrent(0)
-    try:
-        for mode in (0, 1, 0, 1):
-            ops.set_attn_bwd_concurrent(mode)
-            qs, ks, vs = (t.clone().requires_grad_() for t in (q, k, v))
-            out = fused._FlashAttn.apply(qs, ks, vs, p, 99).view(B, T, H * D)
-            out.backward(dout)
-            grads.append((qs.grad, ks.grad, vs.grad))
-    finally:
-        ops.set_attn_bwd_concurrent(prev)
-    torch.cuda.synchronize()
-    for g in grads[1:]:
-        for a, b in zip(grads[0], g):
-            assert torch.equal(a, b)
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_packed_qkv_attention_matches_reference(p, cuda):
     hip.require()
