@@ -31,6 +31,10 @@ struct AttnArgs {
   uint32_t thresh16; // dropout threshold (keep if u16 >= thresh16), 0 = no dropout
   float inv_keep;
   uint32_t seed;
+  // nullable [T][D] bf16 rotary tables: the backward stores dq / dk through the
+  // inverse rotation (the gradient of rope(q), rope(k) w.r.t. q, k)
+  const __bf16* rope_cos;
+  const __bf16* rope_sin;
 };
 
 }  // namespace dlion

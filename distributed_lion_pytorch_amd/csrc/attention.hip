@@ -525,6 +525,32 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 // ring; NT key tiles per barrier (see the forward; dQ runs NT = 1: NT = 2 was
 // 4 % slower, profiles/r4/attn_dq_nt2_ab.txt).  (Round 3's software-pipelined
 // and sequential-NT variants measured neutral and were removed.)
+// Inverse rotary embedding of a [32 rows (registers)] x [D (lane + 32 t)]
+// accumulator set, in place, before the store: with x = (x1 | x2) halves,
+// dx1 = g1 cos1 + g2 sin2, dx2 = g2 cos2 - g1 sin1 (the gradient of
+// rope(x) = x cos + rotate_half(x) sin; csrc/elementwise_kernels.hip
+// rope_kernel, inverse) -- column d and d + D/2 sit in the same lane and
+// register of tiles t and t + D/64.  Rows past T read row T-1's tables.
+template <int D>
+__device__ __forceinline__ void unrope(f32x16 (&x)[D / 32], const AttnArgs& a, int row0, int hf, int r) {
+  constexpr int TH = D / 64;  // tiles per half
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int64_t pos = min(row0 + acc_row(reg, hf), a.T - 1);
+    const __bf16* cr = a.rope_cos + pos * D;
+    const __bf16* sr = a.rope_sin + pos * D;
+#pragma unroll
+    for (int t = 0; t < TH; ++t) {
+      const int d = 32 * t + r;
+      const float c1 = static_cast<float>(cr[d]), c2 = static_cast<float>(cr[d + D / 2]);
+      const float s1 = static_cast<float>(sr[d]), s2 = static_cast<float>(sr[d + D / 2]);
+      const float g1 = x[t][reg], g2 = x[t + TH][reg];
+      x[t][reg] = g1 * c1 + g2 * s2;
+      x[t + TH][reg] = g2 * c2 - g1 * s1;
+    }
+  }
+}
+
 template <int D, bool DROP, int NT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 64 ? DLION_DQ_WAVES64 : 1)))
 attn_bwd_dq_kernel(AttnArgs a) {
@@ -638,6 +664,7 @@ attn_bwd_dq_kernel(AttnArgs a) {
   if (!blk.active) return;
   // dq[t]: rows = q (registers), cols = d (lane)
   __bf16* base = a.dq + b * a.dq_sb + h * a.dq_sh;
+  if (a.rope_cos != nullptr) unrope<D>(dq, a, qtile * 32, hf, r);
 #pragma unroll
   for (int t = 0; t < D / 32; ++t)
 #pragma unroll
@@ -849,6 +876,7 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   if (!active) return;
   // dk/dv[t]: rows = key (registers), cols = d (lane)
   __bf16* dkb = a.dk + b * a.dk_sb + hk * a.dk_sh;
+  if (a.rope_cos != nullptr) unrope<D>(dk, a, kb, hf, r);
   __bf16* dvb = a.dv + b * a.dk_sb + hk * a.dk_sh;
 #pragma unroll
   for (int t = 0; t < D / 32; ++t)

@@ -239,7 +239,8 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tens
 
 void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& out, const Tensor& dout,
               const Tensor& lse, double p, int64_t seed, const Tensor& dq, const Tensor& dk, const Tensor& dv,
-              const std::optional<Tensor>& colsum) {
+              const std::optional<Tensor>& colsum, const std::optional<Tensor>& rope_cos,
+              const std::optional<Tensor>& rope_sin) {
   auto a = attn_args(q, k, v, p, seed);
   check_bthd(out, "out");
   check_bthd(dout, "dout");
@@ -269,6 +270,18 @@ void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
                     colsum->size(1) == 3 * q.size(2) * q.size(3),
                 "dlion attn: colsum must be fp32 [B * ceil(T / 32), 3 * H * D]");
     a.colsum = colsum->data_ptr<float>();
+  }
+  a.rope_cos = a.rope_sin = nullptr;
+  if (rope_cos.has_value() || rope_sin.has_value()) {
+    TORCH_CHECK(rope_cos.has_value() && rope_sin.has_value() && !colsum.has_value(),
+                "dlion attn: rope tables come as a pair, and not with bias-gradient partials");
+    for (const Tensor* t : {&*rope_cos, &*rope_sin}) {
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->dim() == 2 &&
+                      t->size(0) >= q.size(1) && t->size(1) == q.size(3),
+                  "dlion attn: rope tables must be contiguous bf16 [>= T, D]");
+    }
+    a.rope_cos = static_cast<const __bf16*>(rope_cos->data_ptr());
+    a.rope_sin = static_cast<const __bf16*>(rope_sin->data_ptr());
   }
   check_hip(dlion::launch_attn_bwd(a, static_cast<int>(q.size(3)), a.thresh16 > 0, cur_stream()), "attn_bwd");
 }
@@ -1074,7 +1087,8 @@ TORCH_LIBRARY(dlion, m) {
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float p, int seed) -> (Tensor, Tensor)");
   m.def(
       "attn_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout, Tensor lse, float p, int seed,"
-      " Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor(d!)? colsum=None) -> ()");
+      " Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor(d!)? colsum=None, Tensor? rope_cos=None,"
+      " Tensor? rope_sin=None) -> ()");
   m.def("softmax_xent_(Tensor(a!) logits, Tensor labels, int v, int variant=0) -> Tensor");
   m.def(
       "lion_local(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, float decay, float neg_lr,"

@@ -868,6 +868,11 @@ class _RopeAttention(torch.autograd.Function):
         buf = torch.empty(B, T, H + 2 * Hkv, D, dtype=qr.dtype, device=qr.device)
         dq, dk, dv = buf[:, :, :H], buf[:, :, H:H + Hkv], buf[:, :, H + Hkv:]
         ops = hip.ops()
+        if _ROPE_BWD_FUSED and cos.shape[-1] == D:
+            # the kernels store dq / dk through the inverse rotation (no extra pass)
+            ops.attn_bwd(qr, kr, v, out, dout.contiguous(), lse, ctx.p, ctx.seed, dq, dk, dv, None,
+                         cos.reshape(-1, D), sin.reshape(-1, D))
+            return dq, dk, dv, None, None, None, None
         ops.attn_bwd(qr, kr, v, out, dout.contiguous(), lse, ctx.p, ctx.seed, dq, dk, dv)
         if _ROPE_MERGE:
             ops.rope_(buf[:, :, :H + Hkv], cos, sin, True)  # dq | dk: one in-place inverse rotation
@@ -878,6 +883,7 @@ class _RopeAttention(torch.autograd.Function):
 
 
 _ROPE_ATTN = os.environ.get("DLION_ROPE_ATTN", "1") != "0"  # A/B switch for _RopeAttention
+_ROPE_BWD_FUSED = os.environ.get("DLION_ROPE_BWD_FUSED", "1") != "0"  # inverse rotation in the bwd kernels' stores
 
 
 def rope_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,

@@ -155,8 +155,9 @@ def test_linear_multi_matches_separate(fuse, cuda):
         assert err < 2e-2, err
 
 
-@pytest.mark.parametrize("H,Hkv", [(4, 4), (8, 2)])
-def test_rope_attention_packed_grads(H, Hkv, cuda):
+@pytest.mark.parametrize("fused_bwd", [True, False])
+@pytest.mark.parametrize("H,Hkv,T", [(4, 4, 128), (8, 2, 128), (8, 2, 100)])
+def test_rope_attention_packed_grads(H, Hkv, T, fused_bwd, cuda, monkeypatch):
     """Fused RoPE + GQA attention on column views of a fused q|k|v output: the
     values and gradients match rope_reference + SDPA in fp32, and the three
     gradients come back as adjacent column blocks of one buffer (the fused
@@ -165,8 +166,11 @@ def test_rope_attention_packed_grads(H, Hkv, cuda):
     from distributed_lion_pytorch_amd.ops.linear import _adjacent_views
 
     hip.require()
+    # fused_bwd: the attention backward kernels store dq / dk through the inverse
+    # rotation; else a separate in-place rope pass over dq | dk
+    monkeypatch.setattr(fused, "_ROPE_BWD_FUSED", fused_bwd)
     torch.manual_seed(H)
-    B, T, D = 2, 128, 128
+    B, D = 2, 128
     W = (H + 2 * Hkv) * D
     qkv = torch.randn(B, T, W, device=cuda).bfloat16().requires_grad_(True)
     q = qkv[..., :H * D].view(B, T, H, D)
