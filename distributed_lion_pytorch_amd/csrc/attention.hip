@@ -32,13 +32,16 @@
 
 // Occupancy floors (waves per SIMD), A/B-measured (profiles/r3/attn_occupancy_ab.txt):
 // dK/dV D=64 at 3 waves fits 168 VGPRs without spills and is ~4 % faster over
-// fwd+bwd; forcing dQ D=64 to 4 waves (128 VGPRs, 12 dwords of spill) or
-// dK/dV D=128 to 2 waves (~30 dwords of spill) does not pay.
+// fwd+bwd; dK/dV D=128 at 2 waves (~30 dwords of spill) does not pay.  dQ D=64
+// at 4 waves: 12 dwords of spill in round 3 (slower); since the round-4/5
+// kernel changes it fits 128 VGPRs with 3 dwords spilled outside the key loop
+// (its epilogue addresses) and runs the GPT-2 bench 1.070-1.071M -> 1.075-1.077M
+// (profiles/r5/attn_dq4_c14.txt).
 #ifndef DLION_DKV_WAVES64
 #define DLION_DKV_WAVES64 3
 #endif
 #ifndef DLION_DQ_WAVES64
-#define DLION_DQ_WAVES64 1
+#define DLION_DQ_WAVES64 4
 #endif
 // key tiles per barrier in the D = 64 forward
 #ifndef DLION_FWD_NT64
