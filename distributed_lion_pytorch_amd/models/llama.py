@@ -16,7 +16,7 @@ from typing import Optional
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
-from transformers import LlamaConfig, PreTrainedModel
+from transformers import LlamaConfig, MistralConfig, PreTrainedModel, Qwen2Config
 from transformers.modeling_outputs import CausalLMOutputWithPast
 
 from ..ops import fused
@@ -35,9 +35,20 @@ LLAMA_SIZES = {
     "llama-tiny": dict(hidden_size=128, intermediate_size=352, num_hidden_layers=2, num_attention_heads=2,
                        num_key_value_heads=1, vocab_size=512, rope_theta=10000.0, max_position_embeddings=512,
                        rms_norm_eps=1e-5),
+    # Llama-architecture families (models below): Mistral-7B v0.1 and Qwen2 sizes
+    "mistral-7b": dict(model_type="mistral", hidden_size=4096, intermediate_size=14336, num_hidden_layers=32,
+                       num_attention_heads=32, num_key_value_heads=8, vocab_size=32000, rope_theta=10000.0,
+                       max_position_embeddings=32768, sliding_window=4096, rms_norm_eps=1e-5),
+    "qwen2-0.5b": dict(model_type="qwen2", hidden_size=896, intermediate_size=4864, num_hidden_layers=24,
+                       num_attention_heads=14, num_key_value_heads=2, vocab_size=151936, rope_theta=1000000.0,
+                       max_position_embeddings=32768, rms_norm_eps=1e-6, tie_word_embeddings=True),
+    "qwen2-7b": dict(model_type="qwen2", hidden_size=3584, intermediate_size=18944, num_hidden_layers=28,
+                     num_attention_heads=28, num_key_value_heads=4, vocab_size=152064, rope_theta=1000000.0,
+                     max_position_embeddings=32768, rms_norm_eps=1e-6),
 }
 _ALIASES = {"Llama-2-7b-hf": "llama-2-7b", "Llama-2-7b": "llama-2-7b", "Meta-Llama-3-8B": "llama-3-8b",
-            "Llama-3-8B": "llama-3-8b", "Llama-2-13b-hf": "llama-2-13b"}
+            "Llama-3-8B": "llama-3-8b", "Llama-2-13b-hf": "llama-2-13b", "Mistral-7B-v0.1": "mistral-7b",
+            "Qwen2-0.5B": "qwen2-0.5b", "Qwen2-7B": "qwen2-7b"}
 
 
 def llama_config(name: str = "llama-2-7b", **overrides) -> LlamaConfig:
@@ -48,7 +59,8 @@ def llama_config(name: str = "llama-2-7b", **overrides) -> LlamaConfig:
     kw = dict(LLAMA_SIZES[key])
     kw.update(overrides)
     kw.setdefault("tie_word_embeddings", False)
-    return LlamaConfig(**kw)
+    cls = {"mistral": MistralConfig, "qwen2": Qwen2Config}.get(kw.pop("model_type", "llama"), LlamaConfig)
+    return cls(**kw)
 
 
 class RMSNorm(nn.Module):
@@ -102,16 +114,35 @@ def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.T
     return fused.rope(x, cos, sin)
 
 
+def _attention_biases(cfg) -> tuple:
+    """(q/k/v bias, o bias): Llama's ``attention_bias`` covers all four
+    projections; Qwen2 always has q/k/v biases and none on o_proj."""
+    if getattr(cfg, "model_type", "") == "qwen2":
+        return True, False
+    b = bool(getattr(cfg, "attention_bias", False))
+    return b, b
+
+
+def _sliding_window(cfg) -> Optional[int]:
+    """The attention window a config asks for (None: full causal).  Mistral
+    sets ``sliding_window`` (4096 in v0.1); Qwen2 only with ``use_sliding_window``."""
+    if getattr(cfg, "model_type", "") == "qwen2" and not getattr(cfg, "use_sliding_window", False):
+        return None
+    w = getattr(cfg, "sliding_window", None)
+    return int(w) if w else None
+
+
 class LlamaAttention(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
         self.n_head = cfg.num_attention_heads
         self.n_kv = cfg.num_key_value_heads
         self.head_dim = getattr(cfg, "head_dim", None) or cfg.hidden_size // cfg.num_attention_heads
-        self.q_proj = nn.Linear(cfg.hidden_size, self.n_head * self.head_dim, bias=False)
-        self.k_proj = nn.Linear(cfg.hidden_size, self.n_kv * self.head_dim, bias=False)
-        self.v_proj = nn.Linear(cfg.hidden_size, self.n_kv * self.head_dim, bias=False)
-        self.o_proj = nn.Linear(self.n_head * self.head_dim, cfg.hidden_size, bias=False)
+        qkv_bias, o_bias = _attention_biases(cfg)
+        self.q_proj = nn.Linear(cfg.hidden_size, self.n_head * self.head_dim, bias=qkv_bias)
+        self.k_proj = nn.Linear(cfg.hidden_size, self.n_kv * self.head_dim, bias=qkv_bias)
+        self.v_proj = nn.Linear(cfg.hidden_size, self.n_kv * self.head_dim, bias=qkv_bias)
+        self.o_proj = nn.Linear(self.n_head * self.head_dim, cfg.hidden_size, bias=o_bias)
         self.attn_dropout = float(getattr(cfg, "attention_dropout", 0.0) or 0.0)
 
     def forward(self, x, cos, sin):
@@ -136,15 +167,15 @@ def _proj(x, layers):
     concatenated weights (ops/linear.py linear_multi_nk); LoRA-wrapped layers
     contribute their frozen base weight to the fused GEMM and add their
     adapter path to their own output.  Falls back to one GEMM per layer off the
-    GPU, with biases, or for unknown wrappers."""
+    GPU or for unknown wrappers; biases (Qwen2 q/k/v) are added to the fused
+    GEMM's outputs."""
     from .lora import LoraLinear
     from .quant import Linear4bit, linear4bit_multi
 
-    bases, q4 = [], []
+    bases, q4, biases = [], [], []
     for layer in layers:
         base = layer.base_layer if isinstance(layer, LoraLinear) else layer
-        if getattr(base, "bias", None) is not None:
-            return tuple(_lin(layer, x) for layer in layers)
+        biases.append(getattr(base, "bias", None))
         if type(base) is nn.Linear:
             bases.append(base.weight)
         elif isinstance(base, Linear4bit):  # QLoRA base: one expansion + one GEMM (models/quant.py)
@@ -152,13 +183,16 @@ def _proj(x, layers):
         else:
             return tuple(_lin(layer, x) for layer in layers)
     if q4:
-        if bases:
+        if bases or any(b is not None for b in biases):
             return tuple(_lin(layer, x) for layer in layers)
         outs = linear4bit_multi(x, q4)
     elif not x.is_cuda or len({w.dtype for w in bases}) != 1:
         return tuple(_lin(layer, x) for layer in layers)
     else:
         outs = linear_multi_nk(x, bases)
+        # Qwen2's q/k/v biases: one small add per output keeps the single fused GEMM
+        # (its gradient passes the output gradient through unchanged)
+        outs = tuple(o if b is None else o + b.to(o.dtype) for o, b in zip(outs, biases))
     return tuple(layer.add_adapter(x, o) if isinstance(layer, LoraLinear) else o for layer, o in zip(layers, outs))
 
 
@@ -195,10 +229,18 @@ class LlamaModel(nn.Module):
         self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         head_dim = getattr(cfg, "head_dim", None) or cfg.hidden_size // cfg.num_attention_heads
         self.rotary = Rotary(head_dim, _rope_theta(cfg))
+        self.sliding_window = _sliding_window(cfg)
+        if getattr(cfg, "model_type", "") == "qwen2" and getattr(cfg, "use_sliding_window", False):
+            raise NotImplementedError("Qwen2 with use_sliding_window (per-layer windows): use the HF model")
         self.gradient_checkpointing = False
 
     def forward(self, input_ids):
         T = input_ids.shape[1]
+        w = self.sliding_window
+        if w is not None and T > w:
+            # within the window a sliding-window model attends like a full causal one
+            raise NotImplementedError(f"sequence length {T} exceeds the model's sliding attention window {w}: "
+                                      "the native attention is full causal (use native=False for the HF model)")
         x = self.embed_tokens(input_ids)
         cos, sin = self.rotary.tables(T, x.device, x.dtype)
         if self.gradient_checkpointing and self.training:
@@ -286,6 +328,23 @@ class LlamaForCausalLM(PreTrainedModel):
         c = self.config
         n = self.num_parameters() - (0 if c.tie_word_embeddings else 0)
         return 6 * n + 12 * c.num_hidden_layers * c.hidden_size * seq_len
+
+
+class MistralForCausalLM(LlamaForCausalLM):
+    """Mistral: the Llama architecture (GQA, RoPE, SwiGLU, RMSNorm) with HF's
+    Mistral parameter names (identical to Llama's); its sliding attention
+    window (4096 in v0.1) equals full causal attention for sequences up to the
+    window, longer ones are refused."""
+
+    config_class = MistralConfig
+
+
+class Qwen2ForCausalLM(LlamaForCausalLM):
+    """Qwen2: the Llama architecture with q/k/v projection biases (the fused
+    q/k/v GEMM then runs per projection) and, for the small sizes, tied input /
+    output embeddings; HF's Qwen2 parameter names."""
+
+    config_class = Qwen2Config
 
 
 def sequence_logps(model, input_ids: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:

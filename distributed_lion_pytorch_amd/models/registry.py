@@ -8,9 +8,11 @@ import torch
 from transformers import AutoConfig, PretrainedConfig
 
 from .gpt2 import GPT2_SIZES, GPT2LMHeadModel, gpt2_config
-from .llama import LLAMA_SIZES, LlamaForCausalLM, llama_config, _ALIASES as _LLAMA_ALIASES
+from .llama import (LLAMA_SIZES, LlamaForCausalLM, MistralForCausalLM, Qwen2ForCausalLM, llama_config,
+                    _ALIASES as _LLAMA_ALIASES)
 
-NATIVE = {"gpt2": GPT2LMHeadModel, "llama": LlamaForCausalLM}
+NATIVE = {"gpt2": GPT2LMHeadModel, "llama": LlamaForCausalLM, "mistral": MistralForCausalLM,
+          "qwen2": Qwen2ForCausalLM}
 
 
 def load_config(name_or_path: str, overrides: Optional[str] = None) -> PretrainedConfig:
@@ -20,7 +22,7 @@ def load_config(name_or_path: str, overrides: Optional[str] = None) -> Pretraine
         key = name_or_path.rstrip("/").split("/")[-1]
         if key in GPT2_SIZES or key == "gpt2":
             cfg = gpt2_config(key)
-        elif key.lower() in LLAMA_SIZES or key in _LLAMA_ALIASES or key == "llama":
+        elif key.lower() in LLAMA_SIZES or key in _LLAMA_ALIASES or key == "llama":  # incl. Mistral / Qwen2
             cfg = llama_config("llama-2-7b" if key == "llama" else key)
         else:
             raise KeyError(f"unknown model {name_or_path!r} (no hub access): use a local directory or one of "

@@ -53,6 +53,48 @@ def test_llama_gqa_matches_hf():
     _grads_close(ours, hf)
 
 
+def _small(cls, **kw):
+    return cls(vocab_size=97, hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+               num_key_value_heads=2, max_position_embeddings=128, **kw)
+
+
+@pytest.mark.parametrize("family", ["mistral", "qwen2"])
+def test_mistral_qwen2_match_hf(family):
+    from distributed_lion_pytorch_amd.models import llama as L
+    from distributed_lion_pytorch_amd.models.registry import NATIVE
+    if family == "mistral":
+        cfg, ours_cls, hf_cls = _small(transformers.MistralConfig, sliding_window=48), L.MistralForCausalLM, \
+            transformers.MistralForCausalLM
+    else:
+        cfg, ours_cls, hf_cls = _small(transformers.Qwen2Config, tie_word_embeddings=True), L.Qwen2ForCausalLM, \
+            transformers.Qwen2ForCausalLM
+    assert NATIVE[family] is ours_cls
+    torch.manual_seed(0)
+    ours = ours_cls(cfg)
+    if family == "qwen2":  # q/k/v biases, none on o_proj; tied head
+        at = ours.model.layers[0].self_attn
+        assert at.q_proj.bias is not None and at.o_proj.bias is None
+        assert ours.lm_head.weight is ours.model.embed_tokens.weight
+        with torch.no_grad():
+            for layer in ours.model.layers:  # non-zero biases so the parity covers them
+                for p in (layer.self_attn.q_proj, layer.self_attn.k_proj, layer.self_attn.v_proj):
+                    p.bias.normal_(0, 0.1)
+    with tempfile.TemporaryDirectory() as d:
+        ours.save_pretrained(d)
+        hf = hf_cls.from_pretrained(d)
+        back = ours_cls.from_pretrained(d)
+    ids = torch.randint(0, cfg.vocab_size, (2, 40))
+    la, lb = ours(ids, labels=ids).loss, hf(ids, labels=ids).loss
+    assert abs(la.item() - lb.item()) < 1e-5
+    assert abs(back(ids, labels=ids).loss.item() - la.item()) < 1e-6
+    la.backward()
+    lb.backward()
+    _grads_close(ours, hf)
+    if family == "mistral":  # past the sliding window the native full-causal attention refuses
+        with pytest.raises(NotImplementedError, match="sliding"):
+            ours(torch.randint(0, cfg.vocab_size, (1, 49)))
+
+
 def test_fused_ce_matches_reference_and_normalizer():
     torch.manual_seed(0)
     h = torch.randn(3, 17, 16, requires_grad=True)

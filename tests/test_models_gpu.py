@@ -16,7 +16,7 @@ def _rel(a, b):
     return (a - b).abs().max().item() / (b.abs().max().item() + 1e-8)
 
 
-@pytest.mark.parametrize("kind", ["gpt2", "llama"])
+@pytest.mark.parametrize("kind", ["gpt2", "llama", "mistral", "qwen2"])
 def test_native_matches_hf_on_gpu(kind, cuda, tmp_path):
     hip.require()
     torch.manual_seed(0)
@@ -25,11 +25,28 @@ def test_native_matches_hf_on_gpu(kind, cuda, tmp_path):
         ours = GPT2LMHeadModel(cfg)
         ours.save_pretrained(tmp_path)
         hf = transformers.GPT2LMHeadModel.from_pretrained(tmp_path)
-    else:
+    elif kind == "llama":
         cfg = llama_config("llama-tiny")
         ours = LlamaForCausalLM(cfg)
         ours.save_pretrained(tmp_path)
         hf = transformers.LlamaForCausalLM.from_pretrained(tmp_path)
+    else:  # Llama-architecture families: GQA + sliding window (mistral), q/k/v biases + tied head (qwen2)
+        from distributed_lion_pytorch_amd.models import llama as L
+        kw = dict(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+                  num_key_value_heads=2, max_position_embeddings=512)
+        if kind == "mistral":
+            cfg, cls, hf_cls = transformers.MistralConfig(sliding_window=256, **kw), L.MistralForCausalLM, \
+                transformers.MistralForCausalLM
+        else:
+            cfg, cls, hf_cls = transformers.Qwen2Config(tie_word_embeddings=True, **kw), L.Qwen2ForCausalLM, \
+                transformers.Qwen2ForCausalLM
+        ours = cls(cfg)
+        with torch.no_grad():
+            for n, p in ours.named_parameters():
+                if n.endswith("proj.bias"):
+                    p.normal_(0, 0.1)
+        ours.save_pretrained(tmp_path)
+        hf = hf_cls.from_pretrained(tmp_path)
     ours, hf = ours.to(cuda, torch.bfloat16), hf.to(cuda, torch.bfloat16)
     ids = torch.randint(0, cfg.vocab_size, (4, 128), device=cuda)
     la = ours(ids, labels=ids).loss
