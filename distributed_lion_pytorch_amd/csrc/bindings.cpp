@@ -17,8 +17,8 @@
 #include "kernels.h"
 
 namespace dlion {
-bool lt_gemm_nt(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, const void* bias,
-                int64_t M, int64_t N, int64_t K, int epi, int device, hipStream_t s);
+bool lt_gemm(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, const void* bias,
+             int64_t M, int64_t N, int64_t K, int epi, int device, hipStream_t s, bool nn);
 }
 
 namespace {
@@ -697,9 +697,22 @@ bool lt_gemm_nt(const Tensor& a, const Tensor& b, const std::optional<Tensor>& b
                 "dlion lt_gemm: bias must be a contiguous bf16 [N] tensor");
   }
   const c10::DeviceGuard g(a.device());
-  return dlion::lt_gemm_nt(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
-                           bias.has_value() ? bias->data_ptr() : nullptr, a.size(0), b.size(0), a.size(1),
-                           static_cast<int>(epi), a.device().index(), cur_stream());
+  return dlion::lt_gemm(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
+                        bias.has_value() ? bias->data_ptr() : nullptr, a.size(0), b.size(0), a.size(1),
+                        static_cast<int>(epi), a.device().index(), cur_stream(), false);
+}
+
+// out [M, N] = a [M, K] . b [K, N] (b row-major, e.g. an nn.Linear weight in an
+// input gradient dY . W); plain epilogue.  False when hipBLASLt has no kernel.
+bool lt_gemm_nn(const Tensor& a, const Tensor& b, const Tensor& out) {
+  check_gemm_operand(a, "a");
+  check_gemm_operand(b, "b");
+  check_gemm_operand(out, "out");
+  TORCH_CHECK(a.size(1) == b.size(0) && out.size(0) == a.size(0) && out.size(1) == b.size(1),
+              "dlion lt_gemm_nn: shape mismatch a=", a.sizes(), " b=", b.sizes(), " out=", out.sizes());
+  const c10::DeviceGuard g(a.device());
+  return dlion::lt_gemm(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0), nullptr,
+                        a.size(0), b.size(1), a.size(1), 0, a.device().index(), cur_stream(), true);
 }
 
 // ------------------------------------------------------------- embedding
@@ -1063,6 +1076,7 @@ TORCH_LIBRARY(dlion, m) {
       " float p, int seed) -> ()");
   m.def("scale_acc_(Tensor x, Tensor s, Tensor(a!) y, bool accumulate) -> ()");
   m.def("lt_gemm_nt(Tensor a, Tensor b, Tensor? bias, int epi, Tensor(a!) out) -> bool");
+  m.def("lt_gemm_nn(Tensor a, Tensor b, Tensor(a!) out) -> bool");
   m.def("gemm_nt(Tensor a, Tensor b, Tensor? bias) -> Tensor");
   m.def("gemm_nt_out(Tensor a, Tensor b, Tensor? bias, Tensor(a!) out) -> ()");
   m.def("gemm_nt_gelu(Tensor a, Tensor b, Tensor bias, bool exact) -> (Tensor, Tensor)");
@@ -1144,6 +1158,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("embed_bwd_", &embed_bwd_);
   m.impl("scale_acc_", &scale_acc_);
   m.impl("lt_gemm_nt", &lt_gemm_nt);
+  m.impl("lt_gemm_nn", &lt_gemm_nn);
   m.impl("gemm_tn", &gemm_tn);
   m.impl("gemm_tn_", &gemm_tn_);
   m.impl("lora_rows", &lora_rows);

@@ -4,7 +4,9 @@
 //   epi 0  plain      1  + bias[N]      2  gelu_tanh(z + bias[N])
 //
 // Row-major operands map onto hipBLASLt's column-major convention as
-// D^T[N,M] = op_T(b)[N,K] . a^T[K,M] (transA = T, transB = N).  Epilogue 2 is
+// D^T[N,M] = op_T(b)[N,K] . a^T[K,M] (transA = T, transB = N).  The NN form
+// out[M,N] = a[M,K] . b[K,N] (lt_gemm_nn: an input gradient dY . W against the
+// nn.Linear weight as stored, no W^T copy) is D^T = b_cm[N,K] . a^T (transA = N).  Epilogue 2 is
 // the GPT-2 MLP up-projection when no backward follows (evaluation, frozen
 // reference models): one GEMM instead of GEMM + a bias+GELU pass over the
 // [tokens, 4C] activation.  Training keeps the separate kernel because the
@@ -60,7 +62,7 @@ struct DevState {
   at::Tensor workspace;
 };
 
-using Key = std::array<int64_t, 8>;  // m, n, k, lda, ldb, ldc, epi, device
+using Key = std::array<int64_t, 9>;  // m, n, k, lda, ldb, ldc, epi, device, nn
 
 struct Plan {
   hipblasLtMatmulDesc_t desc = nullptr;
@@ -118,13 +120,13 @@ bool exhaustive() {
 }
 
 Plan& get_plan(DevState& st, const Key& key, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldc,
-               int epi, const void* bias) {
+               int epi, const void* bias, bool nn) {
   auto it = g_plans.find(key);
   if (it != g_plans.end()) return it->second;
   Plan& p = g_plans[key];
   lt_check(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F), "hipblasLtMatmulDescCreate");
   const int32_t opT = HIPBLAS_OP_T, opN = HIPBLAS_OP_N;
-  set_attr(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opT, sizeof(opT));
+  set_attr(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, nn ? &opN : &opT, sizeof(opT));
   set_attr(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opN, sizeof(opN));
   const hipblasLtEpilogue_t e = epilogue_of(epi);
   set_attr(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e));
@@ -133,8 +135,8 @@ Plan& get_plan(DevState& st, const Key& key, int64_t m, int64_t n, int64_t k, in
     set_attr(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
   }
   bind_pointers(p, bias);
-  // A_cm: b viewed column-major [K, N] (ld = ldb); B_cm: a as [K, M] (ld = lda); D: [N, M] (ld = ldc)
-  lt_check(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, k, n, ldb), "layout A");
+  // A_cm: b viewed column-major [K, N] (NN: [N, K]) (ld = ldb); B_cm: a as [K, M] (ld = lda); D: [N, M] (ld = ldc)
+  lt_check(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, nn ? n : k, nn ? k : n, ldb), "layout A");
   lt_check(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, k, m, lda), "layout B");
   lt_check(hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_16BF, n, m, ldc), "layout D");
   hipblasLtMatmulPreference_t pref;
@@ -158,7 +160,8 @@ Plan& get_plan(DevState& st, const Key& key, int64_t m, int64_t n, int64_t k, in
   p.n_heur = static_cast<int>(p.cand.size());
   if (exhaustive()) {
     std::vector<hipblasLtMatmulHeuristicResult_t> all;
-    if (hipblaslt_ext::getAllAlgos(st.handle, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, HIPBLAS_OP_T, HIPBLAS_OP_N,
+    if (hipblaslt_ext::getAllAlgos(st.handle, hipblaslt_ext::GemmType::HIPBLASLT_GEMM,
+                                   nn ? HIPBLAS_OP_N : HIPBLAS_OP_T, HIPBLAS_OP_N,
                                    HIP_R_16BF, HIP_R_16BF, HIP_R_16BF, HIP_R_16BF, HIPBLAS_COMPUTE_32F,
                                    all) == HIPBLAS_STATUS_SUCCESS) {
       const float alpha = 1.f, beta = 0.f;
@@ -285,12 +288,12 @@ void tune(DevState& st, Plan& p, const void* a, const void* b, void* c, hipStrea
 
 // Returns false (and does nothing) when hipBLASLt has no kernel for this
 // shape/epilogue, so the caller can take its unfused path.
-bool lt_gemm_nt(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, const void* bias,
-                int64_t M, int64_t N, int64_t K, int epi, int device, hipStream_t s) {
+bool lt_gemm(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, const void* bias,
+             int64_t M, int64_t N, int64_t K, int epi, int device, hipStream_t s, bool nn) {
   std::lock_guard<std::mutex> lk(g_mu);
   DevState& st = dev_state(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
-  const Key key{M, N, K, lda, ldb, ldc, epi, device};
-  Plan& p = get_plan(st, key, M, N, K, lda, ldb, ldc, epi, bias);
+  const Key key{M, N, K, lda, ldb, ldc, epi, device, nn ? 1 : 0};
+  Plan& p = get_plan(st, key, M, N, K, lda, ldb, ldc, epi, bias, nn);
   if (!p.ok) return false;
   bind_pointers(p, bias);
   if (!p.tuned) tune(st, p, a, b, c, s);

@@ -803,9 +803,29 @@ def gemm_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
     return cands[_pick(key, cands)]()
 
 
+_LT_NN = os.environ.get("DLION_LT_NN", "1") != "0"  # A/B switch: 0 drops the hipBLASLt NN candidate
+
+
+def _lt_nn(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dy @ w (w [N, K] row-major) through hipBLASLt's NN form with the tuned
+    algorithm (csrc/lt_gemm.cpp): no W^T copy."""
+    from . import hip
+
+    out = torch.empty(dy.shape[0], w.shape[1], dtype=dy.dtype, device=dy.device)
+    if not hip.ops().lt_gemm_nn(dy, w, out):
+        return dy @ w
+    return out
+
+
+def _lt_nn_ok(dy: torch.Tensor, w: torch.Tensor) -> bool:
+    return (dy.stride(1) == 1 and dy.stride(0) % 8 == 0 and w.is_contiguous() and w.shape[1] % 8 == 0
+            and dy.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
+
+
 def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, frozen: bool) -> torch.Tensor:
-    """dy @ w (w [N, K]): the NN product, or for frozen weights the measured-
-    fastest NT form against a cached w^T [K, N]."""
+    """dy @ w (w [N, K]): the NN product (ATen, or hipBLASLt's NN form with the
+    searched algorithm), or the measured-fastest NT form against a w^T [K, N]
+    (cached for good for frozen weights, rebuilt per optimizer step otherwise)."""
     M, N = dy.shape
     K = w.shape[1]
     if not (_tunable(dy, M, N, K) and w.dtype == torch.bfloat16 and w.dim() == 2):
@@ -814,10 +834,14 @@ def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, frozen: bool) -> torch.Tensor:
     name = _GEMM_PICK.get(key)
     if name == "nn":
         return dy @ w
+    if name == "lt_nn":
+        return _lt_nn(dy, w)
     if name is None:
         # time the NT forms with the transpose included for a trainable weight (its W^T is
         # rebuilt once per optimizer step, i.e. at most once per micro-batch)
         timed = {"nn": lambda: dy @ w}
+        if _LT_NN and _lt_nn_ok(dy, w):
+            timed["lt_nn"] = lambda: _lt_nn(dy, w)
         wt_t = cached_derived(w, "t", lambda t: fast_transpose(t)) if frozen else None
         probe = _nt_candidates(dy, wt_t if frozen else fast_transpose(w), "nt_")
         for n in probe:
@@ -825,6 +849,8 @@ def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, frozen: bool) -> torch.Tensor:
         name = _pick(key, timed)
         if name == "nn":
             return dy @ w
+        if name == "lt_nn":
+            return _lt_nn(dy, w)
     wt = cached_derived(w, "t", lambda t: fast_transpose(t))  # frozen: for good; trainable: per step
     return _nt_candidates(dy, wt, "nt_")[name]()
 

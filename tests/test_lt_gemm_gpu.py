@@ -36,6 +36,20 @@ def test_lt_gemm_epilogues(M, N, K, epi, cuda):
     assert torch.equal(out, out2)
 
 
+@pytest.mark.parametrize("M,N,K", [(2048, 768, 3072), (1000, 520, 136)])
+def test_lt_gemm_nn(M, N, K, cuda):
+    """out = a . b with b [K, N] row-major (the input gradient dY . W without a W^T copy)."""
+    hip.require()
+    torch.manual_seed(3)
+    a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    b = (torch.randn(K, N, device=cuda) / K ** 0.5).to(torch.bfloat16)
+    out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    assert hip.ops().lt_gemm_nn(a, b, out)
+    assert _rel(out, a.float() @ b.float()) < 1e-2
+    out2 = torch.empty_like(out)
+    assert hip.ops().lt_gemm_nn(a, b, out2) and torch.equal(out, out2)
+
+
 def test_lt_gemm_strided_rows(cuda):
     hip.require()
     torch.manual_seed(1)

@@ -39,6 +39,10 @@ def main():
         # input gradients as NT against W^T: dX[M, K_in] = dY[M, N_out] . (W^T)^T with W^T [K_in, N_out]
         "qkv_dgrad": (4096, 12288), "o_dgrad": (4096, 4096), "gate_up_dgrad": (4096, 22016), "down_dgrad": (11008, 4096),
     }
+    if os.environ.get("MODEL") == "llama3":  # Llama-3-8B (GQA q/k/v 6144, MLP 14336); TOKENS=8192 for its preset
+        shapes = {"qkv_fwd": (6144, 4096), "o_fwd": (4096, 4096), "gate_up_fwd": (28672, 4096),
+                  "down_fwd": (4096, 14336), "qkv_dgrad": (4096, 6144), "o_dgrad": (4096, 4096),
+                  "gate_up_dgrad": (4096, 28672), "down_dgrad": (14336, 4096)}
     for name, (N, K) in shapes.items():
         a = torch.randn(M, K, device=dev).to(bf)
         w = (torch.randn(N, K, device=dev) * 0.02).to(bf)  # NT operand
@@ -48,6 +52,10 @@ def main():
         if name.endswith("dgrad"):
             wt = w.t().contiguous()  # the stored nn.Linear weight [K_out... ] for the NN form
             res["aten_nn_us"] = timeit(lambda: a @ wt)
+            nn_out = torch.empty(M, N, device=dev, dtype=bf)
+            if ops.lt_gemm_nn(a, wt, nn_out):  # hipBLASLt NN with the searched algorithm
+                res["lt_tuned_nn_us"] = timeit(lambda: ops.lt_gemm_nn(a, wt, nn_out))
+            res["transpose_us"] = timeit(lambda: w.t().contiguous())  # W^T rebuild for a trainable weight
         out = torch.empty(M, N, device=dev, dtype=bf)
         ok = ops.lt_gemm_nt(a, w, None, 0, out)
         if ok:
