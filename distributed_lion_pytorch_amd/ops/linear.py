@@ -181,9 +181,12 @@ def _run_deferred(key) -> None:
 
     params, cols, segs_a, segs_b, vers = _ST.wdefer.pop(key)
     _ST.wdefer_bytes[0] -= sum(t.numel() * t.element_size() for t in segs_a + segs_b)
-    for t, v in zip(segs_a + segs_b, vers):
+    for i, (t, v) in enumerate(zip((x for pair in zip(segs_a, segs_b) for x in pair), vers)):
         if t._version != v:
-            raise RuntimeError("dlion: an operand kept for a deferred weight gradient was modified in place")
+            shapes = [tuple(r().shape) if r() is not None else None for r in params]
+            raise RuntimeError(f"dlion: an operand kept for a deferred weight gradient was modified in place "
+                               f"(weights {shapes}, micro-batch {i // 2}, operand {'ab'[i % 2]} {tuple(t.shape)}, "
+                               f"version {v} -> {t._version})")
     ent = _ST.acc[key]
     accumulate = key in _ST.pending
     hip.ops().gemm_tn_(segs_a, segs_b, ent[1], accumulate)
