@@ -17,8 +17,9 @@
 #include "kernels.h"
 
 namespace dlion {
+enum class Layout : int { NT = 0, NN = 1, TN = 2 };
 bool lt_gemm(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, const void* bias,
-             int64_t M, int64_t N, int64_t K, int epi, int device, hipStream_t s, bool nn);
+             int64_t M, int64_t N, int64_t K, int epi, int device, hipStream_t s, Layout lay, bool accumulate);
 }
 
 namespace {
@@ -699,7 +700,7 @@ bool lt_gemm_nt(const Tensor& a, const Tensor& b, const std::optional<Tensor>& b
   const c10::DeviceGuard g(a.device());
   return dlion::lt_gemm(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
                         bias.has_value() ? bias->data_ptr() : nullptr, a.size(0), b.size(0), a.size(1),
-                        static_cast<int>(epi), a.device().index(), cur_stream(), false);
+                        static_cast<int>(epi), a.device().index(), cur_stream(), dlion::Layout::NT, false);
 }
 
 // out [M, N] = a [M, K] . b [K, N] (b row-major, e.g. an nn.Linear weight in an
@@ -712,7 +713,20 @@ bool lt_gemm_nn(const Tensor& a, const Tensor& b, const Tensor& out) {
               "dlion lt_gemm_nn: shape mismatch a=", a.sizes(), " b=", b.sizes(), " out=", out.sizes());
   const c10::DeviceGuard g(a.device());
   return dlion::lt_gemm(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0), nullptr,
-                        a.size(0), b.size(1), a.size(1), 0, a.device().index(), cur_stream(), true);
+                        a.size(0), b.size(1), a.size(1), 0, a.device().index(), cur_stream(), dlion::Layout::NN, false);
+}
+
+// out [M, N] (+)= a [K, M]^T . b [K, N] (a weight gradient over the token axis; accumulate: beta = 1).
+bool lt_gemm_tn(const Tensor& a, const Tensor& b, const Tensor& out, bool accumulate) {
+  check_gemm_operand(a, "a");
+  check_gemm_operand(b, "b");
+  check_gemm_operand(out, "out");
+  TORCH_CHECK(a.size(0) == b.size(0) && out.size(0) == a.size(1) && out.size(1) == b.size(1),
+              "dlion lt_gemm_tn: shape mismatch a=", a.sizes(), " b=", b.sizes(), " out=", out.sizes());
+  const c10::DeviceGuard g(a.device());
+  return dlion::lt_gemm(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0), nullptr,
+                        a.size(1), b.size(1), a.size(0), 0, a.device().index(), cur_stream(), dlion::Layout::TN,
+                        accumulate);
 }
 
 // ------------------------------------------------------------- embedding
@@ -1077,6 +1091,7 @@ TORCH_LIBRARY(dlion, m) {
   m.def("scale_acc_(Tensor x, Tensor s, Tensor(a!) y, bool accumulate) -> ()");
   m.def("lt_gemm_nt(Tensor a, Tensor b, Tensor? bias, int epi, Tensor(a!) out) -> bool");
   m.def("lt_gemm_nn(Tensor a, Tensor b, Tensor(a!) out) -> bool");
+  m.def("lt_gemm_tn(Tensor a, Tensor b, Tensor(a!) out, bool accumulate) -> bool");
   m.def("gemm_nt(Tensor a, Tensor b, Tensor? bias) -> Tensor");
   m.def("gemm_nt_out(Tensor a, Tensor b, Tensor? bias, Tensor(a!) out) -> ()");
   m.def("gemm_nt_gelu(Tensor a, Tensor b, Tensor bias, bool exact) -> (Tensor, Tensor)");
@@ -1159,6 +1174,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("scale_acc_", &scale_acc_);
   m.impl("lt_gemm_nt", &lt_gemm_nt);
   m.impl("lt_gemm_nn", &lt_gemm_nn);
+  m.impl("lt_gemm_tn", &lt_gemm_tn);
   m.impl("gemm_tn", &gemm_tn);
   m.impl("gemm_tn_", &gemm_tn_);
   m.impl("lora_rows", &lora_rows);

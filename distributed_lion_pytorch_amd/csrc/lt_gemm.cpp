@@ -6,7 +6,10 @@
 // Row-major operands map onto hipBLASLt's column-major convention as
 // D^T[N,M] = op_T(b)[N,K] . a^T[K,M] (transA = T, transB = N).  The NN form
 // out[M,N] = a[M,K] . b[K,N] (lt_gemm_nn: an input gradient dY . W against the
-// nn.Linear weight as stored, no W^T copy) is D^T = b_cm[N,K] . a^T (transA = N).  Epilogue 2 is
+// nn.Linear weight as stored, no W^T copy) is D^T = b_cm[N,K] . a^T (transA = N);
+// the TN form out[M,N] (+)= a[K,M]^T . b[K,N] (lt_gemm_tn: a weight gradient
+// dY^T X over the token axis) is D^T = b_cm[N,K] . op_T(a_cm[M,K]) (transB = T),
+// with beta = 1 to accumulate onto the gradient (tuned on a scratch output).  Epilogue 2 is
 // the GPT-2 MLP up-projection when no backward follows (evaluation, frozen
 // reference models): one GEMM instead of GEMM + a bias+GELU pass over the
 // [tokens, 4C] activation.  Training keeps the separate kernel because the
@@ -47,6 +50,9 @@
 #include <vector>
 
 namespace dlion {
+
+enum class Layout : int { NT = 0, NN = 1, TN = 2 };
+
 namespace {
 
 constexpr int kCand = 12;
@@ -62,13 +68,14 @@ struct DevState {
   at::Tensor workspace;
 };
 
-using Key = std::array<int64_t, 9>;  // m, n, k, lda, ldb, ldc, epi, device, nn
+using Key = std::array<int64_t, 10>;  // m, n, k, lda, ldb, ldc, epi, device, layout, beta
 
 struct Plan {
   hipblasLtMatmulDesc_t desc = nullptr;
   hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
   hipblasLtMatmulAlgo_t algo{};
   size_t ws = 0;
+  float beta = 0.f;
   bool ok = false;
   bool tuned = false;
   int n_heur = 0;  // cand[0, n_heur): hipBLASLt's heuristic picks, the rest: exhaustive search
@@ -108,7 +115,7 @@ void bind_pointers(Plan& p, const void* bias) {
 
 hipblasStatus_t run(DevState& st, Plan& p, const hipblasLtMatmulAlgo_t& algo, const void* a, const void* b, void* c,
                     hipStream_t s) {
-  const float alpha = 1.f, beta = 0.f;
+  const float alpha = 1.f, beta = p.beta;
   // column-major: A_cm = b (op T), B_cm = a (op N), D_cm = out
   return hipblasLtMatmul(st.handle, p.desc, &alpha, b, p.la, a, p.lb, &beta, c, p.lc, c, p.lc, &algo,
                          st.workspace.data_ptr(), kWorkspace, s);
@@ -120,14 +127,16 @@ bool exhaustive() {
 }
 
 Plan& get_plan(DevState& st, const Key& key, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldc,
-               int epi, const void* bias, bool nn) {
+               int epi, const void* bias, Layout lay, float beta) {
   auto it = g_plans.find(key);
   if (it != g_plans.end()) return it->second;
   Plan& p = g_plans[key];
+  p.beta = beta;
+  const bool nn = lay == Layout::NN, tn = lay == Layout::TN;
   lt_check(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F), "hipblasLtMatmulDescCreate");
   const int32_t opT = HIPBLAS_OP_T, opN = HIPBLAS_OP_N;
-  set_attr(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, nn ? &opN : &opT, sizeof(opT));
-  set_attr(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opN, sizeof(opN));
+  set_attr(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, nn || tn ? &opN : &opT, sizeof(opT));
+  set_attr(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, tn ? &opT : &opN, sizeof(opN));
   const hipblasLtEpilogue_t e = epilogue_of(epi);
   set_attr(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e));
   if (epi == 1 || epi == 2) {
@@ -135,9 +144,10 @@ Plan& get_plan(DevState& st, const Key& key, int64_t m, int64_t n, int64_t k, in
     set_attr(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
   }
   bind_pointers(p, bias);
-  // A_cm: b viewed column-major [K, N] (NN: [N, K]) (ld = ldb); B_cm: a as [K, M] (ld = lda); D: [N, M] (ld = ldc)
-  lt_check(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, nn ? n : k, nn ? k : n, ldb), "layout A");
-  lt_check(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, k, m, lda), "layout B");
+  // A_cm: b viewed column-major [K, N] (NN / TN: [N, K]) (ld = ldb); B_cm: a as [K, M] (TN: [M, K])
+  // (ld = lda); D: [N, M] (ld = ldc)
+  lt_check(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, nn || tn ? n : k, nn || tn ? k : n, ldb), "layout A");
+  lt_check(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, tn ? m : k, tn ? k : m, lda), "layout B");
   lt_check(hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_16BF, n, m, ldc), "layout D");
   hipblasLtMatmulPreference_t pref;
   lt_check(hipblasLtMatmulPreferenceCreate(&pref), "preference");
@@ -161,10 +171,10 @@ Plan& get_plan(DevState& st, const Key& key, int64_t m, int64_t n, int64_t k, in
   if (exhaustive()) {
     std::vector<hipblasLtMatmulHeuristicResult_t> all;
     if (hipblaslt_ext::getAllAlgos(st.handle, hipblaslt_ext::GemmType::HIPBLASLT_GEMM,
-                                   nn ? HIPBLAS_OP_N : HIPBLAS_OP_T, HIPBLAS_OP_N,
+                                   nn || tn ? HIPBLAS_OP_N : HIPBLAS_OP_T, tn ? HIPBLAS_OP_T : HIPBLAS_OP_N,
                                    HIP_R_16BF, HIP_R_16BF, HIP_R_16BF, HIP_R_16BF, HIPBLAS_COMPUTE_32F,
                                    all) == HIPBLAS_STATUS_SUCCESS) {
-      const float alpha = 1.f, beta = 0.f;
+      const float alpha = 1.f;
       for (auto& r : all) {
         const int idx = hipblaslt_ext::getIndexFromAlgo(r.algo);
         if (seen.count(idx)) continue;
@@ -289,14 +299,22 @@ void tune(DevState& st, Plan& p, const void* a, const void* b, void* c, hipStrea
 // Returns false (and does nothing) when hipBLASLt has no kernel for this
 // shape/epilogue, so the caller can take its unfused path.
 bool lt_gemm(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, const void* bias,
-             int64_t M, int64_t N, int64_t K, int epi, int device, hipStream_t s, bool nn) {
+             int64_t M, int64_t N, int64_t K, int epi, int device, hipStream_t s, Layout lay, bool accumulate) {
   std::lock_guard<std::mutex> lk(g_mu);
-  DevState& st = dev_state(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
-  const Key key{M, N, K, lda, ldb, ldc, epi, device, nn ? 1 : 0};
-  Plan& p = get_plan(st, key, M, N, K, lda, ldb, ldc, epi, bias, nn);
+  const at::Device dev(at::kCUDA, static_cast<c10::DeviceIndex>(device));
+  DevState& st = dev_state(dev);
+  const Key key{M, N, K, lda, ldb, ldc, epi, device, static_cast<int64_t>(lay), accumulate ? 1 : 0};
+  Plan& p = get_plan(st, key, M, N, K, lda, ldb, ldc, epi, bias, lay, accumulate ? 1.f : 0.f);
   if (!p.ok) return false;
   bind_pointers(p, bias);
-  if (!p.tuned) tune(st, p, a, b, c, s);
+  if (!p.tuned) {
+    if (accumulate) {  // the timed runs would add onto the caller's output: tune on a scratch copy of its rows
+      at::Tensor scratch = at::empty({M * ldc}, at::TensorOptions().dtype(at::kBFloat16).device(dev));
+      tune(st, p, a, b, scratch.data_ptr(), s);
+    } else {
+      tune(st, p, a, b, c, s);
+    }
+  }
   lt_check(run(st, p, p.algo, a, b, c, s), "hipblasLtMatmul");
   return true;
 }

@@ -558,10 +558,15 @@ def _unsplit_wgrad(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumula
         name = _GEMM_PICK.get(key)
         if name is None:
             scratch = torch.empty(K, N, dtype=out.dtype, device=out.device)
-            name = _pick(key, {"tn": lambda: hip.ops().gemm_tn_([a], [b], scratch, False),
-                               "blas": lambda: torch.mm(a.t(), b, out=scratch)})
+            cands = {"tn": lambda: hip.ops().gemm_tn_([a], [b], scratch, False),
+                     "blas": lambda: torch.mm(a.t(), b, out=scratch)}
+            if _LT_TN and _lt_nn_ok(a, b):  # hipBLASLt's TN form with the searched algorithm
+                cands["lt"] = lambda: hip.ops().lt_gemm_tn(a, b, scratch, False) or torch.mm(a.t(), b, out=scratch)
+            name = _pick(key, cands)
             del scratch
-        if name == "blas":
+        if name == "lt" and hip.ops().lt_gemm_tn(a, b, out2, accumulate):
+            return
+        if name in ("blas", "lt"):
             if accumulate:
                 out2.addmm_(a.t(), b)
             else:
@@ -807,6 +812,7 @@ def gemm_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
 
 
 _LT_NN = os.environ.get("DLION_LT_NN", "1") != "0"  # A/B switch: 0 drops the hipBLASLt NN candidate
+_LT_TN = os.environ.get("DLION_LT_TN", "1") != "0"  # A/B switch: 0 drops the hipBLASLt TN weight-gradient candidate
 
 
 def _lt_nn(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -821,8 +827,8 @@ def _lt_nn(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 
 def _lt_nn_ok(dy: torch.Tensor, w: torch.Tensor) -> bool:
-    return (dy.stride(1) == 1 and dy.stride(0) % 8 == 0 and w.is_contiguous() and w.shape[1] % 8 == 0
-            and dy.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
+    return (dy.dim() == 2 and w.dim() == 2 and dy.stride(1) == 1 and dy.stride(0) % 8 == 0 and w.stride(1) == 1
+            and w.stride(0) % 8 == 0 and dy.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
 
 
 def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, frozen: bool) -> torch.Tensor:

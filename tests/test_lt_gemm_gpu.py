@@ -50,6 +50,22 @@ def test_lt_gemm_nn(M, N, K, cuda):
     assert hip.ops().lt_gemm_nn(a, b, out2) and torch.equal(out, out2)
 
 
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_lt_gemm_tn(accumulate, cuda):
+    """out (+)= a^T . b over the token axis (a weight gradient), beta = 1 when accumulating."""
+    hip.require()
+    torch.manual_seed(4)
+    a = torch.randn(1024, 384, device=cuda).to(torch.bfloat16)
+    b = (torch.randn(1024, 256, device=cuda) / 32).to(torch.bfloat16)
+    init = torch.randn(384, 256, device=cuda).to(torch.bfloat16)
+    out = init.clone()
+    assert hip.ops().lt_gemm_tn(a, b, out, accumulate)
+    ref = a.float().t() @ b.float() + (init.float() if accumulate else 0)
+    assert _rel(out, ref) < 1e-2
+    out2 = init.clone()  # the tuning runs went to a scratch output: a second call adds once more
+    assert hip.ops().lt_gemm_tn(a, b, out2, accumulate) and torch.equal(out, out2)
+
+
 def test_lt_gemm_strided_rows(cuda):
     hip.require()
     torch.manual_seed(1)
