@@ -544,27 +544,46 @@ def split_k_factor(M: int, K: int, N: int) -> int:
     return s
 
 
-def _unsplit_wgrad(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool) -> None:
-    """out [K, N] bf16 (+)= a^T b unsplit: the own TN kernel's bf16 epilogue, or
-    hipBLASLt's TN GEMM (beta = 1 to accumulate) where the per-shape timing
-    (see gemm_fwd) finds it faster.  Both round the fp32 sum (+ out) once."""
+def _direct_split_pick(a: torch.Tensor, b: torch.Tensor, s: int, own: bool) -> bool:
+    """A split own-TN weight gradient outside a multi-micro-batch window goes
+    through _unsplit_wgrad's per-shape timing instead (the split launch is one
+    of its candidates): hipBLASLt's TN form is faster at some shapes
+    (Llama-3-8B q/k/v: 352 vs 399 us, profiles/r5/wgrad_lt_c20.txt)."""
+    M, K = a.shape
+    return (_LT_TN and own and s > 1 and not (_ST.fuse["on"] and _ST.fuse["multi"]) and a.dtype == torch.bfloat16
+            and _tunable(a, M, b.shape[1], K))
+
+
+def _unsplit_wgrad(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool, split: int = 1) -> None:
+    """out [K, N] bf16 (+)= a^T b: the own TN kernel's unsplit bf16 epilogue,
+    hipBLASLt's TN GEMM (ATen's heuristic or the searched algorithm; beta = 1 to
+    accumulate), or (split > 1) the own kernel's split-K partials + one reduction
+    pass, whichever the per-shape timing (see gemm_fwd) finds fastest.  All
+    round the fp32 sum (+ out) once."""
     from . import hip
 
     M, K = a.shape
     N = b.shape[1]
     out2 = out.view(K, N)
     if _tunable(a, M, N, K):
-        key = ("wgrad", M, K, N, a.stride(0), b.stride(0))
+        key = ("wgrad", M, K, N, a.stride(0), b.stride(0), split)
         name = _GEMM_PICK.get(key)
         if name is None:
             scratch = torch.empty(K, N, dtype=out.dtype, device=out.device)
             cands = {"tn": lambda: hip.ops().gemm_tn_([a], [b], scratch, False),
                      "blas": lambda: torch.mm(a.t(), b, out=scratch)}
+            if split > 1:
+                cands["split"] = lambda: hip.ops().sum_partials_multi_(
+                    [hip.ops().gemm_tn([a], [b], split).view(split, K * N)], scratch.view(-1), False)
             if _LT_TN and _lt_nn_ok(a, b):  # hipBLASLt's TN form with the searched algorithm
                 cands["lt"] = lambda: hip.ops().lt_gemm_tn(a, b, scratch, False) or torch.mm(a.t(), b, out=scratch)
             name = _pick(key, cands)
             del scratch
         if name == "lt" and hip.ops().lt_gemm_tn(a, b, out2, accumulate):
+            return
+        if name == "split":
+            hip.ops().sum_partials_multi_([hip.ops().gemm_tn([a], [b], split).view(split, K * N)], out2.view(-1),
+                                          accumulate)
             return
         if name in ("blas", "lt"):
             if accumulate:
@@ -586,18 +605,19 @@ def wgrad_into(a: torch.Tensor, b: torch.Tensor, w: torch.nn.Parameter) -> None:
         from . import hip
 
         if hip.available():
-            if _ST.fuse["on"] and ((own and _defer_wgrad([w], [(0, K * N)], a, b, s))
-                                      or _acc_gemm([w], [(0, K * N)], a, b, s)):
+            timed = w.dtype == torch.bfloat16 and _direct_split_pick(a, b, s, own)
+            if _ST.fuse["on"] and not timed and ((own and _defer_wgrad([w], [(0, K * N)], a, b, s))
+                                                 or _acc_gemm([w], [(0, K * N)], a, b, s)):
                 return  # reduced into w.grad when the accumulation window closes
             g = w.grad  # _acc_gemm may have flushed earlier partials into it
             grad_ok = g is None or (g.is_contiguous() and g.dtype == w.dtype)
-            if grad_ok and own and s == 1 and w.dtype == torch.bfloat16:
+            if grad_ok and own and (s == 1 or timed) and w.dtype == torch.bfloat16:
                 # unsplit: the TN kernel writes (adds onto) the bf16 gradient itself
                 if g is None:
                     w.grad = g = torch.empty_like(w, memory_format=torch.contiguous_format)
-                    _unsplit_wgrad(a, b, g, False)
+                    _unsplit_wgrad(a, b, g, False, s)
                 else:
-                    _unsplit_wgrad(a, b, g, True)
+                    _unsplit_wgrad(a, b, g, True, s)
                 return
             if grad_ok:
                 part = wgrad_partials(a, b, s).view(s, K * N)
@@ -1065,14 +1085,19 @@ def _multi_wgrad_into(dy, x2d, params, sizes) -> None:
             for n in sizes:
                 cols.append((off * K, n * K))
                 off += n
-            if _ST.fuse["on"] and ((own and _defer_wgrad(list(params), cols, dy, x2d, s))
-                                      or _acc_gemm(list(params), cols, dy, x2d, s)):
+            bf = all(p.dtype == torch.bfloat16 for p in params)
+            gs = [p.grad for p in params]
+            base = _adjacent_rows(gs) if all(g is not None for g in gs) else None
+            timed = (bf and _direct_split_pick(dy, x2d, s, own)
+                     and (all(g is None for g in gs) or (base is not None and base.is_contiguous())))
+            if _ST.fuse["on"] and not timed and ((own and _defer_wgrad(list(params), cols, dy, x2d, s))
+                                                 or _acc_gemm(list(params), cols, dy, x2d, s)):
                 return  # reduced into each params[i].grad when the window closes
-            if own and s == 1 and all(p.dtype == torch.bfloat16 for p in params):
+            if own and (s == 1 or timed) and bf:
                 gs = [p.grad for p in params]
                 if all(g is None for g in gs):  # one buffer; each grad is a row block of it
                     buf = torch.empty(N, K, dtype=torch.bfloat16, device=dy.device)
-                    _unsplit_wgrad(dy, x2d, buf, False)
+                    _unsplit_wgrad(dy, x2d, buf, False, s)
                     off = 0
                     for p, n in zip(params, sizes):
                         p.grad = buf[off:off + n].view_as(p)
@@ -1080,7 +1105,7 @@ def _multi_wgrad_into(dy, x2d, params, sizes) -> None:
                     return
                 base = _adjacent_rows(gs) if all(g is not None for g in gs) else None
                 if base is not None and base.dtype == torch.bfloat16 and base.is_contiguous():
-                    _unsplit_wgrad(dy, x2d, base, True)
+                    _unsplit_wgrad(dy, x2d, base, True, s)
                     return
             flat = wgrad_partials(dy, x2d, s).view(s, N * K)
             off = 0

@@ -288,10 +288,11 @@ def test_gemm_autotune_candidates_agree(cuda):
     assert (d1.float() - dref).abs().max().item() <= 2e-2 * dref.abs().max().item()
 
 
-@pytest.mark.parametrize("choice", ["tn", "blas"])
+@pytest.mark.parametrize("choice", ["tn", "blas", "lt", "split"])
 def test_unsplit_wgrad_choices(cuda, choice):
-    """Both candidates of the unsplit weight gradient (own TN bf16 epilogue,
-    hipBLASLt TN with beta = 1) write and accumulate the same gradient."""
+    """Every candidate of the timed weight gradient (own TN bf16 epilogue,
+    ATen's hipBLASLt TN, hipBLASLt TN with the searched algorithm and beta = 1,
+    own split-K partials + reduction) writes and accumulates the same gradient."""
     from distributed_lion_pytorch_amd.ops import linear as L
 
     hip.require()
@@ -299,10 +300,36 @@ def test_unsplit_wgrad_choices(cuda, choice):
     M, K, N = 2048, 2048, 4096
     a = torch.randn(M, K, device=cuda, dtype=torch.bfloat16)
     b = torch.randn(M, N, device=cuda, dtype=torch.bfloat16)
-    L._GEMM_PICK[("wgrad", M, K, N, a.stride(0), b.stride(0))] = choice
+    split = 2 if choice == "split" else 1
+    L._GEMM_PICK[("wgrad", M, K, N, a.stride(0), b.stride(0), split)] = choice
     ref = a.float().t() @ b.float()
     out = torch.empty(K, N, device=cuda, dtype=torch.bfloat16)
-    L._unsplit_wgrad(a, b, out, False)
+    L._unsplit_wgrad(a, b, out, False, split)
     assert (out.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
-    L._unsplit_wgrad(a, b, out, True)
+    L._unsplit_wgrad(a, b, out, True, split)
     assert (out.float() - 2 * ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+
+
+def test_direct_split_weight_gradient_goes_through_the_timed_pick(cuda, monkeypatch):
+    """Outside a multi-micro-batch window a split weight gradient (Llama-3-8B
+    q/k/v at s = 2) is timed against the unsplit candidates; the fused q/k/v
+    gradient blocks come out right whichever wins."""
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    torch.manual_seed(7)
+    M, K = 4096, 2048
+    sizes = [2048, 512, 512]
+    monkeypatch.setattr(L, "tn_split_factor", lambda *a, **k: 2)
+    monkeypatch.setattr(L, "_GEMM_PICK", {})
+    dy = torch.randn(M, sum(sizes), device=cuda, dtype=torch.bfloat16)
+    x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16)
+    ps = [torch.nn.Parameter(torch.zeros(n, K, device=cuda, dtype=torch.bfloat16)) for n in sizes]
+    assert L._direct_split_pick(dy, x, 2, True)
+    with L.grad_accumulation_fusion(True, micro_batches=1):
+        L._multi_wgrad_into(dy, x, ps, sizes)
+    key = [k for k in L._GEMM_PICK if k[0] == "wgrad"]
+    assert key and key[0][-1] == 2, L._GEMM_PICK
+    ref = dy.float().t() @ x.float()
+    got = torch.cat([p.grad.float() for p in ps], 0)
+    assert (got - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
