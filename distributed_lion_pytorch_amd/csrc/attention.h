@@ -35,6 +35,10 @@ struct AttnArgs {
   // inverse rotation (the gradient of rope(q), rope(k) w.r.t. q, k)
   const __bf16* rope_cos;
   const __bf16* rope_sin;
+  // sliding window (Mistral, Qwen2 sliding layers): query q attends keys
+  // q - window < k <= q; 0 = plain causal.  Key / query tiles wholly outside
+  // the window are skipped, the boundary tiles masked per element.
+  int window;
 };
 
 }  // namespace dlion

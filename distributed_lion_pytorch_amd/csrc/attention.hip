@@ -384,6 +384,42 @@ struct QBlock {
   }
 };
 
+// The sliding window is compiled for D = 128 only (Mistral-7B; the D = 64
+// GPT-2 / Qwen2-0.5B kernels stay as they were -- the window's registers put
+// dQ D = 64 past its 4-wave budget: 12-19 dwords of spill); the host refuses a
+// window at D = 64 (ops/fused.py then takes the masked SDPA path).
+template <int D>
+__device__ __forceinline__ int window_of(const AttnArgs& a) { return D == 128 ? a.window : 0; }
+
+// Sliding-window key range of a query-side wave (fwd, dQ): its first key tile
+// wlo (row qtile*32's lowest key, q - window + 1) and the block's first
+// NT-aligned key tile kstart (its first wave's wlo); window 0 = from key 0.
+struct SlideRange {
+  int wlo, kstart, lim;
+  __device__ __forceinline__ SlideRange(int window, int qtile, int w, int nt) {
+    if (window > 0) {
+      wlo = max(0, qtile * 32 - window + 1) >> 5;
+      kstart = ((max(0, (qtile - w) * 32 - window + 1) >> 5) / nt) * nt;
+      lim = qtile * 32 + 31 - window;  // keys <= lim are outside some row's window
+    } else {
+      wlo = kstart = 0;
+      lim = -1;
+    }
+  }
+  // a key-tile group starting at tile kt holds keys outside some row's window
+  __device__ __forceinline__ bool cut(int kt, int) const { return kt * 32 <= lim; }
+};
+
+// scores with the query on the lane (fwd / dQ orientation): -inf where key <= q - window
+template <int NT>
+__device__ __forceinline__ void window_mask_qlane(f32x16 (&s)[NT], int kt, int q, int window, int hf) {
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg)
+      if ((kt + j) * 32 + acc_row(reg, hf) <= q - window) s[j][reg] = -INFINITY;
+}
+
 // ------------------------------------------------------------------ forward
 // NT key tiles (32 keys each) per barrier: with NT = 2 every wave has two
 // independent QK^T chains and two PV chains per iteration, so hipcc can put one
@@ -403,6 +439,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   // rows past T (tail tile): computed on a copy of row T-1, never stored; keys
   // past T are behind every valid query, so the causal mask already drops them
   const int qc = min(q, a.T - 1);
+  const int win = window_of<D>(a);
+  const SlideRange sw(win, qtile, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), NT);
 
   bf16x8 qf[D / 16];
   if (blk.active) {
@@ -413,7 +451,9 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   f32x16 oacc[D / 32];
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) oacc[t] = zero16();
-  float m = -INFINITY, l = 0.f;
+  // a finite start under a sliding window: a row whose keys in the wave's first
+  // tile are all masked then gets p = 0 there instead of exp2(-inf + inf)
+  float m = win > 0 ? -1e30f : -INFINITY, l = 0.f;
 
   const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
   const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
@@ -431,13 +471,13 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
       vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[buf][j], a.T - row);
     }
   };
-  stage(0, 0);
+  stage(sw.kstart, (sw.kstart / NT) & 1);
   vm_wait0();
   __syncthreads();
-  for (int kt = 0; kt <= last; kt += NT) {
+  for (int kt = sw.kstart; kt <= last; kt += NT) {
     const int buf = (kt / NT) & 1;
     if (kt + NT <= last) stage(kt + NT, buf ^ 1);  // the other buffer was last read before the previous barrier
-    if (blk.active && kt <= qtile) {  // wave-uniform
+    if (blk.active && kt <= qtile && kt + NT - 1 >= sw.wlo) {  // wave-uniform
       f32x16 s[NT];
       DLION_PRIO_ON(kFwdPrio, 1);
 #pragma unroll
@@ -454,6 +494,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
           for (int reg = 0; reg < 16; ++reg)
             if ((kt + j) * 32 + acc_row(reg, hf) > q) s[j][reg] = -INFINITY;
       }
+      if (sw.cut(kt, qtile)) window_mask_qlane<NT>(s, kt, q, win, hf);
       // row max on the raw scores (scale > 0); the scale is folded into the
       // exponent's FMA instead of a separate multiply pass
       float tmax = s[0][0];
@@ -567,6 +608,8 @@ attn_bwd_dq_kernel(AttnArgs a) {
   const int b = bh / a.H, h = bh % a.H, hk = h / (a.H / a.Hkv);
   const int q = qtile * 32 + r;
   const int qc = min(q, a.T - 1);  // tail rows: a copy of row T-1, never stored (see the forward)
+  const int win = window_of<D>(a);
+  const SlideRange sw(win, qtile, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), NT);
 
   bf16x8 qf[D / 16], dof[D / 16];
   float lse2 = 0.f, dlt = 0.f;
@@ -613,16 +656,16 @@ attn_bwd_dq_kernel(AttnArgs a) {
       vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[buf][j], a.T - row);
     }
   };
-  const int ns = last / NT + 1;
-  for (int j = 0; j < NB - 1 && j < ns; ++j) stage(j, j);
-  for (int st = 0; st < ns; ++st) {
+  const int ns = last / NT + 1, st0 = sw.kstart / NT;
+  for (int j = st0; j < st0 + NB - 1 && j < ns; ++j) stage(j, j % NB);
+  for (int st = st0; st < ns; ++st) {
     const int buf = st % NB;
     // super-tile st has landed once only the later ones' pieces (NT * 2 PPW each) are in flight
     vm_wait_n(min(ns - 1 - st, NB - 2) * NT * 2 * DmaTile<D>::PPW);
     __syncthreads();  // ... for every wave; and every wave is done with the buffer restaged next
     if (st + NB - 1 < ns) stage(st + NB - 1, (st + NB - 1) % NB);
     const int kt0 = st * NT;
-    if (blk.active && kt0 <= qtile) {
+    if (blk.active && kt0 <= qtile && kt0 + NT - 1 >= sw.wlo) {
       // NT independent S / dP chains: one tile's exp / hash VALU work can sit
       // beside the other's MFMAs
       f32x16 s[NT], dp[NT];
@@ -645,6 +688,7 @@ attn_bwd_dq_kernel(AttnArgs a) {
           for (int reg = 0; reg < 16; ++reg)
             if ((kt0 + j) * 32 + acc_row(reg, hf) > q) s[j][reg] = -INFINITY;
       }
+      if (sw.cut(kt0, qtile)) window_mask_qlane<NT>(s, kt0, q, win, hf);
 #pragma unroll
       for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -748,7 +792,11 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   const int par2 = 2 * (key & 1);
   const uint32_t kmix = (static_cast<uint32_t>(key & 31) >> 1) * kKeyMul;  // pair within the key tile
   const DmaTile<D> qd(a.q_st), dd(a.o_st);
-  const int nq = ntiles - first;   // query tiles per head
+  // query tiles per head: first .. qhi (a sliding window ends the block's range
+  // at the last query its highest key reaches)
+  const int win = window_of<D>(a);
+  const int qhi = win > 0 ? min(ntiles - 1, (first * 32 + 127 + win - 1) >> 5) : ntiles - 1;
+  const int nq = qhi - first + 1;
   const int total = group * nq;    // (head, query tile) steps, head-major
   // step i -> buffer i&1: Q and dO tiles by LDS-DMA; wave 0 also DMAs the 32
   // lse (lanes 0..31) and delta (lanes 32..63) values into ls_[buf][0..1];
@@ -778,7 +826,7 @@ attn_bwd_dkv_kernel(AttnArgs a) {
         ls_[buf][2 + tt][slot] = __uint_as_float(tile_base(ar, first + tt));
       }
     }
-    if (++sq == ntiles) {
+    if (++sq > qhi) {
       sq = first;
       ++sg;
     }
@@ -787,12 +835,12 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   // LDS-DMA pieces per stage: Q + dO tiles, and wave 0's lse / delta row values
   const int per_stage = 2 * DmaTile<D>::PPW + (w == 0 ? 1 : 0);
   int qt = first;  // query tile of step i
-  for (int i = 0; i < total; ++i, qt = (qt + 1 == ntiles ? first : qt + 1)) {
+  for (int i = 0; i < total; ++i, qt = (qt + 1 > qhi ? first : qt + 1)) {
     const int buf = i % NB;
     vm_wait_n(min(total - 1 - i, NB - 2) * per_stage);  // step i landed (later steps may be in flight)
     __syncthreads();  // for every wave; and every wave is done with the buffer restaged next
     if (i + NB - 1 < total) stage_next((i + NB - 1) % NB);
-    if (active && qt >= ktile) {  // wave-uniform
+    if (active && qt >= ktile && (win == 0 || qt * 32 <= kb + 30 + win)) {  // wave-uniform
       const int qb = qt * 32;
       f32x16 s = zero16(), dp = zero16();
       DLION_PRIO_ON(kDkvPrio, 1);
@@ -811,6 +859,11 @@ attn_bwd_dkv_kernel(AttnArgs a) {
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg)
           if (qb + acc_row(reg, hf) >= a.T) s[reg] = -INFINITY;
+      }
+      if (win > 0 && qb + 31 - kb >= win) {  // sliding window: queries at or past key + window
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+          if (qb + acc_row(reg, hf) - key >= win) s[reg] = -INFINITY;
       }
       // row statistics of the lane's 16 query rows: rows (reg&3) + 8(reg>>2) + 4hf
       // come in 4 runs of 4 consecutive rows -> 16-byte LDS reads (broadcast),

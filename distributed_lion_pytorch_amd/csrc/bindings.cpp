@@ -226,8 +226,16 @@ dlion::AttnArgs attn_args(const Tensor& q, const Tensor& k, const Tensor& v, dou
   return a;
 }
 
-std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, double p, int64_t seed) {
+void set_window(dlion::AttnArgs& a, int64_t window, int64_t D) {
+  TORCH_CHECK(window >= 0, "dlion attn: window must be >= 0 (0 = plain causal)");
+  a.window = window >= a.T ? 0 : static_cast<int>(window);  // a window covering T is plain causal
+  TORCH_CHECK(a.window == 0 || D == 128, "dlion attn: a sliding window needs head_dim 128");
+}
+
+std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, double p, int64_t seed,
+                                    int64_t window) {
   auto a = attn_args(q, k, v, p, seed);
+  set_window(a, window, q.size(3));
   const c10::DeviceGuard g(q.device());
   auto out = at::empty({q.size(0), q.size(1), q.size(2), q.size(3)}, q.options());
   auto lse = at::empty({q.size(0), q.size(2), q.size(1)}, q.options().dtype(at::kFloat));
@@ -241,8 +249,9 @@ std::tuple<Tensor, Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tens
 void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& out, const Tensor& dout,
               const Tensor& lse, double p, int64_t seed, const Tensor& dq, const Tensor& dk, const Tensor& dv,
               const std::optional<Tensor>& colsum, const std::optional<Tensor>& rope_cos,
-              const std::optional<Tensor>& rope_sin) {
+              const std::optional<Tensor>& rope_sin, int64_t window) {
   auto a = attn_args(q, k, v, p, seed);
+  set_window(a, window, q.size(3));
   check_bthd(out, "out");
   check_bthd(dout, "dout");
   check_bthd(dq, "dq");
@@ -1113,11 +1122,11 @@ TORCH_LIBRARY(dlion, m) {
   m.def("sum_partials_scaled_(Tensor part, Tensor s, Tensor(a!) out, bool accumulate) -> ()");
   m.def("sum_partials_multi_(Tensor[] parts, Tensor(a!) out, bool accumulate) -> ()");
   m.def("colsum_partials(Tensor x, int parts) -> Tensor");
-  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float p, int seed) -> (Tensor, Tensor)");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float p, int seed, int window=0) -> (Tensor, Tensor)");
   m.def(
       "attn_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor dout, Tensor lse, float p, int seed,"
       " Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor(d!)? colsum=None, Tensor? rope_cos=None,"
-      " Tensor? rope_sin=None) -> ()");
+      " Tensor? rope_sin=None, int window=0) -> ()");
   m.def("softmax_xent_(Tensor(a!) logits, Tensor labels, int v, int variant=0) -> Tensor");
   m.def(
       "lion_local(Tensor meta, int seg_off, int chunk_off, int n_chunks, int dtype, float decay, float neg_lr,"

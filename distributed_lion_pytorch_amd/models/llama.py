@@ -123,18 +123,26 @@ def _attention_biases(cfg) -> tuple:
     return b, b
 
 
-def _sliding_window(cfg) -> Optional[int]:
-    """The attention window a config asks for (None: full causal).  Mistral
-    sets ``sliding_window`` (4096 in v0.1); Qwen2 only with ``use_sliding_window``."""
-    if getattr(cfg, "model_type", "") == "qwen2" and not getattr(cfg, "use_sliding_window", False):
-        return None
+def _layer_window(cfg, i: int) -> int:
+    """Layer i's sliding attention window (0: full causal), as HF builds the
+    masks: Mistral applies ``sliding_window`` (4096 in v0.1) to every layer;
+    configs with ``layer_types`` (Qwen2 with ``use_sliding_window``: the layers
+    from ``max_window_layers`` on) only to the "sliding_attention" ones."""
     w = getattr(cfg, "sliding_window", None)
-    return int(w) if w else None
+    if not w:
+        return 0
+    types = getattr(cfg, "layer_types", None)
+    if types is not None:
+        return int(w) if types[i] == "sliding_attention" else 0
+    if getattr(cfg, "model_type", "") == "qwen2" and not getattr(cfg, "use_sliding_window", False):
+        return 0
+    return int(w)
 
 
 class LlamaAttention(nn.Module):
-    def __init__(self, cfg: LlamaConfig):
+    def __init__(self, cfg: LlamaConfig, layer_idx: int = 0):
         super().__init__()
+        self.window = _layer_window(cfg, layer_idx)  # 0: full causal
         self.n_head = cfg.num_attention_heads
         self.n_kv = cfg.num_key_value_heads
         self.head_dim = getattr(cfg, "head_dim", None) or cfg.hidden_size // cfg.num_attention_heads
@@ -151,7 +159,7 @@ class LlamaAttention(nn.Module):
         q = q.view(B, T, self.n_head, self.head_dim)
         k = k.view(B, T, self.n_kv, self.head_dim)
         v = v.view(B, T, self.n_kv, self.head_dim)
-        y = fused.rope_attention(q, k, v, cos, sin, self.attn_dropout if self.training else 0.0)
+        y = fused.rope_attention(q, k, v, cos, sin, self.attn_dropout if self.training else 0.0, self.window)
         return _lin(self.o_proj, y)
 
 
@@ -209,9 +217,9 @@ class LlamaMLP(nn.Module):
 
 
 class LlamaDecoderLayer(nn.Module):
-    def __init__(self, cfg: LlamaConfig):
+    def __init__(self, cfg: LlamaConfig, layer_idx: int = 0):
         super().__init__()
-        self.self_attn = LlamaAttention(cfg)
+        self.self_attn = LlamaAttention(cfg, layer_idx)
         self.mlp = LlamaMLP(cfg)
         self.input_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
@@ -225,22 +233,14 @@ class LlamaModel(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
         self.embed_tokens = nn.Embedding(cfg.vocab_size, cfg.hidden_size)
-        self.layers = nn.ModuleList([LlamaDecoderLayer(cfg) for _ in range(cfg.num_hidden_layers)])
+        self.layers = nn.ModuleList([LlamaDecoderLayer(cfg, i) for i in range(cfg.num_hidden_layers)])
         self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         head_dim = getattr(cfg, "head_dim", None) or cfg.hidden_size // cfg.num_attention_heads
         self.rotary = Rotary(head_dim, _rope_theta(cfg))
-        self.sliding_window = _sliding_window(cfg)
-        if getattr(cfg, "model_type", "") == "qwen2" and getattr(cfg, "use_sliding_window", False):
-            raise NotImplementedError("Qwen2 with use_sliding_window (per-layer windows): use the HF model")
         self.gradient_checkpointing = False
 
     def forward(self, input_ids):
         T = input_ids.shape[1]
-        w = self.sliding_window
-        if w is not None and T > w:
-            # within the window a sliding-window model attends like a full causal one
-            raise NotImplementedError(f"sequence length {T} exceeds the model's sliding attention window {w}: "
-                                      "the native attention is full causal (use native=False for the HF model)")
         x = self.embed_tokens(input_ids)
         cos, sin = self.rotary.tables(T, x.device, x.dtype)
         if self.gradient_checkpointing and self.training:
@@ -332,17 +332,18 @@ class LlamaForCausalLM(PreTrainedModel):
 
 class MistralForCausalLM(LlamaForCausalLM):
     """Mistral: the Llama architecture (GQA, RoPE, SwiGLU, RMSNorm) with HF's
-    Mistral parameter names (identical to Llama's); its sliding attention
-    window (4096 in v0.1) equals full causal attention for sequences up to the
-    window, longer ones are refused."""
+    Mistral parameter names (identical to Llama's) and sliding-window
+    attention (4096 in v0.1): the flash kernels skip the key tiles outside each
+    query tile's window and mask the boundary ones (csrc/attention.hip)."""
 
     config_class = MistralConfig
 
 
 class Qwen2ForCausalLM(LlamaForCausalLM):
-    """Qwen2: the Llama architecture with q/k/v projection biases (the fused
-    q/k/v GEMM then runs per projection) and, for the small sizes, tied input /
-    output embeddings; HF's Qwen2 parameter names."""
+    """Qwen2: the Llama architecture with q/k/v projection biases (added to the
+    fused q/k/v GEMM's outputs), tied input / output embeddings for the small
+    sizes, and (``use_sliding_window``) sliding-window layers from
+    ``max_window_layers`` on; HF's Qwen2 parameter names."""
 
     config_class = Qwen2Config
 

@@ -640,16 +640,23 @@ def embed(ids: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor, p: float) -> 
 
 
 # ------------------------------------------------------------------ attention
-def _attn_ok(x: torch.Tensor, T: int, D: int) -> bool:
+def _attn_ok(x: torch.Tensor, T: int, D: int, window: int = 0) -> bool:
     """The gfx950 flash kernels take any sequence length (tail tiles are
-    masked in-kernel) at head_dim 64 / 128 -- every GPT-2 and Llama-2/3 size."""
-    return x.dtype == torch.bfloat16 and D in (64, 128) and T >= 1 and _use_hip(x)
+    masked in-kernel) at head_dim 64 / 128 -- every GPT-2 and Llama-2/3 size;
+    a sliding window (< T) at head_dim 128 (csrc/attention.hip window_of)."""
+    return (x.dtype == torch.bfloat16 and D in (64, 128) and T >= 1 and _use_hip(x)
+            and (_eff_window(window, T) == 0 or D == 128))
+
+
+def _eff_window(window, T: int) -> int:
+    """A sliding window that covers the whole sequence is plain causal: 0."""
+    return int(window) if window and int(window) < T else 0
 
 
 _MATH_WARNED = set()
 
 
-def _sdpa_math(q, k, v, dropout_p: float) -> torch.Tensor:
+def _sdpa_math(q, k, v, dropout_p: float, window: int = 0) -> torch.Tensor:
     """Fallback for what the flash kernels do not cover (head_dim not in {64,
     128}, fp32/fp16 inputs, no extension): PyTorch's *math* SDPA backend only
     -- matmul + softmax ATen ops (hipBLASLt GEMMs) -- never the flash /
@@ -664,7 +671,13 @@ def _sdpa_math(q, k, v, dropout_p: float) -> torch.Tensor:
 
         warnings.warn(f"dlion attention: no gfx950 flash kernel for head_dim={q.shape[-1]} / {q.dtype}; "
                       "using the math SDPA backend (O(T^2) memory)")
+    T = q.shape[-2]
+    window = _eff_window(window, T)
     with sdpa_kernel([SDPBackend.MATH]):
+        if window:  # HF's sliding-window mask: key k visible to query q iff q - window < k <= q
+            i = torch.arange(T, device=q.device)
+            d = i[:, None] - i[None, :]
+            return F.scaled_dot_product_attention(q, k, v, attn_mask=(d >= 0) & (d < window), dropout_p=dropout_p)
         return F.scaled_dot_product_attention(q, k, v, dropout_p=dropout_p, is_causal=True)
 
 
@@ -698,10 +711,10 @@ class _FlashAttn(torch.autograd.Function):
     """Causal (GQA) attention on separate q [B,T,H,D], k/v [B,T,Hkv,D]."""
 
     @staticmethod
-    def forward(ctx, q, k, v, p, seed):
-        out, lse = hip.ops().attn_fwd(q, k, v, p, seed)
+    def forward(ctx, q, k, v, p, seed, window=0):
+        out, lse = hip.ops().attn_fwd(q, k, v, p, seed, window)
         ctx.save_for_backward(q, k, v, out, lse)
-        ctx.p, ctx.seed = p, seed
+        ctx.p, ctx.seed, ctx.window = p, seed, window
         return out
 
     @staticmethod
@@ -710,8 +723,9 @@ class _FlashAttn(torch.autograd.Function):
         dout = dout.contiguous()
         dq = torch.empty(q.shape, dtype=q.dtype, device=q.device)
         dkv = torch.empty((2,) + tuple(k.shape), dtype=k.dtype, device=k.device)
-        hip.ops().attn_bwd(q, k, v, out, dout, lse, ctx.p, ctx.seed, dq, dkv[0], dkv[1])
-        return dq, dkv[0], dkv[1], None, None
+        hip.ops().attn_bwd(q, k, v, out, dout, lse, ctx.p, ctx.seed, dq, dkv[0], dkv[1], None, None, None,
+                           ctx.window)
+        return dq, dkv[0], dkv[1], None, None, None
 
 
 def causal_attention(qkv: torch.Tensor, dropout_p: float) -> torch.Tensor:
@@ -802,22 +816,25 @@ def qkv_attention(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, n_head: int
     return causal_attention(qkv, dropout_p)
 
 
-def causal_attention_gqa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, dropout_p: float = 0.0) -> torch.Tensor:
-    """q [B,T,H,D], k/v [B,T,Hkv,D] -> [B,T,H*D] (grouped-query causal attention)."""
+def causal_attention_gqa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, dropout_p: float = 0.0,
+                         window: int = 0) -> torch.Tensor:
+    """q [B,T,H,D], k/v [B,T,Hkv,D] -> [B,T,H*D] (grouped-query causal attention;
+    ``window`` > 0: sliding window, query q sees keys q - window < k <= q)."""
     B, T, H, D = q.shape
+    window = _eff_window(window, T)
     if q.is_cuda:
         from .linear import autocast_inputs
 
         q, k, v = autocast_inputs(q, k, v)
-    if _attn_ok(q, T, D):
+    if _attn_ok(q, T, D, window):
         with torch.autocast("cuda", enabled=False):
-            return _FlashAttn.apply(q, k, v, float(dropout_p), _new_seed()).view(B, T, H * D)
+            return _FlashAttn.apply(q, k, v, float(dropout_p), _new_seed(), window).view(B, T, H * D)
     rep = H // k.shape[2]
     qh, kh, vh = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
     if rep > 1:
         kh = kh.repeat_interleave(rep, dim=1)
         vh = vh.repeat_interleave(rep, dim=1)
-    y = _sdpa_math(qh, kh, vh, dropout_p)
+    y = _sdpa_math(qh, kh, vh, dropout_p, window)
     return y.transpose(1, 2).reshape(B, T, H * D)
 
 
@@ -845,7 +862,7 @@ class _RopeAttention(torch.autograd.Function):
     Llama-2-7B LoRA SFT step)."""
 
     @staticmethod
-    def forward(ctx, q, k, v, cos, sin, p, seed):
+    def forward(ctx, q, k, v, cos, sin, p, seed, window=0):
         ops = hip.ops()
         H = q.shape[2]
         qk = _adjacent_heads(q, k) if _ROPE_MERGE else None
@@ -855,9 +872,9 @@ class _RopeAttention(torch.autograd.Function):
         else:
             qr = ops.rope(q, cos, sin, False)
             kr = ops.rope(k, cos, sin, False)
-        out, lse = ops.attn_fwd(qr, kr, v, p, seed)
+        out, lse = ops.attn_fwd(qr, kr, v, p, seed, window)
         ctx.save_for_backward(qr, kr, v, out, lse, cos, sin)
-        ctx.p, ctx.seed = p, seed
+        ctx.p, ctx.seed, ctx.window = p, seed, window
         return out
 
     @staticmethod
@@ -871,15 +888,16 @@ class _RopeAttention(torch.autograd.Function):
         if _ROPE_BWD_FUSED and cos.shape[-1] == D:
             # the kernels store dq / dk through the inverse rotation (no extra pass)
             ops.attn_bwd(qr, kr, v, out, dout.contiguous(), lse, ctx.p, ctx.seed, dq, dk, dv, None,
-                         cos.reshape(-1, D), sin.reshape(-1, D))
-            return dq, dk, dv, None, None, None, None
-        ops.attn_bwd(qr, kr, v, out, dout.contiguous(), lse, ctx.p, ctx.seed, dq, dk, dv)
+                         cos.reshape(-1, D), sin.reshape(-1, D), ctx.window)
+            return dq, dk, dv, None, None, None, None, None
+        ops.attn_bwd(qr, kr, v, out, dout.contiguous(), lse, ctx.p, ctx.seed, dq, dk, dv, None, None, None,
+                     ctx.window)
         if _ROPE_MERGE:
             ops.rope_(buf[:, :, :H + Hkv], cos, sin, True)  # dq | dk: one in-place inverse rotation
         else:
             ops.rope_(dq, cos, sin, True)
             ops.rope_(dk, cos, sin, True)
-        return dq, dk, dv, None, None, None, None
+        return dq, dk, dv, None, None, None, None, None
 
 
 _ROPE_ATTN = os.environ.get("DLION_ROPE_ATTN", "1") != "0"  # A/B switch for _RopeAttention
@@ -887,20 +905,22 @@ _ROPE_BWD_FUSED = os.environ.get("DLION_ROPE_BWD_FUSED", "1") != "0"  # inverse 
 
 
 def rope_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
-                   dropout_p: float = 0.0) -> torch.Tensor:
-    """causal_attention_gqa(rope(q), rope(k), v) -> [B, T, H*D]; q [B,T,H,D],
+                   dropout_p: float = 0.0, window: int = 0) -> torch.Tensor:
+    """causal_attention_gqa(rope(q), rope(k), v, window) -> [B, T, H*D]; q [B,T,H,D],
     k / v [B,T,Hkv,D] (views of a fused projection output are read in place)."""
     B, T, H, D = q.shape
+    window = _eff_window(window, T)
     if q.is_cuda:
         from .linear import autocast_inputs
 
         q, k, v = autocast_inputs(q, k, v)
-    if (_ROPE_ATTN and _attn_ok(q, T, D) and cos.dtype == sin.dtype == torch.bfloat16 and k.dtype == v.dtype == torch.bfloat16
-            and all(_token_strided_ok(t) for t in (q, k, v))):
+    if (_ROPE_ATTN and _attn_ok(q, T, D, window) and cos.dtype == sin.dtype == torch.bfloat16
+            and k.dtype == v.dtype == torch.bfloat16 and all(_token_strided_ok(t) for t in (q, k, v))):
         with torch.autocast("cuda", enabled=False):
-            out = _RopeAttention.apply(q, k, v, cos.contiguous(), sin.contiguous(), float(dropout_p), _new_seed())
+            out = _RopeAttention.apply(q, k, v, cos.contiguous(), sin.contiguous(), float(dropout_p), _new_seed(),
+                                       window)
         return out.view(B, T, H * D)
-    return causal_attention_gqa(rope(q, cos, sin), rope(k, cos, sin), v, dropout_p)
+    return causal_attention_gqa(rope(q, cos, sin), rope(k, cos, sin), v, dropout_p, window)
 
 
 # ------------------------------------------------------------------- LoRA
@@ -1028,8 +1048,9 @@ def attention_dropout_keep(B: int, H: int, T: int, p: float, seed: int, device=N
     return (s16 >= th - 32768).view(B, H, T, T)
 
 
-def reference_attention(q, k, v, dropout_p: float = 0.0, seed: int = 0) -> torch.Tensor:
-    """fp32 math reference with the kernels' dropout mask: q [B,T,H,D], k/v [B,T,Hkv,D]."""
+def reference_attention(q, k, v, dropout_p: float = 0.0, seed: int = 0, window: int = 0) -> torch.Tensor:
+    """fp32 math reference with the kernels' dropout mask: q [B,T,H,D], k/v [B,T,Hkv,D]
+    (``window`` > 0: keys q - window < k <= q only)."""
     B, T, H, D = q.shape
     rep = H // k.shape[2]
     qh = q.float().transpose(1, 2)
@@ -1037,6 +1058,8 @@ def reference_attention(q, k, v, dropout_p: float = 0.0, seed: int = 0) -> torch
     vh = v.float().transpose(1, 2).repeat_interleave(rep, dim=1)
     s = (qh @ kh.transpose(-1, -2)) / (D ** 0.5)
     causal = torch.ones(T, T, dtype=torch.bool, device=q.device).tril()
+    if window:
+        causal &= ~torch.ones(T, T, dtype=torch.bool, device=q.device).tril(-window)
     s = s.masked_fill(~causal, float("-inf"))
     pr = torch.softmax(s, dim=-1)
     if dropout_p > 0:

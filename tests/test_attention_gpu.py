@@ -145,6 +145,67 @@ def test_flash_attention_tail_tiles(T, B, H, Hkv, D, p, cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("T,window", [(100, 1), (100, 31), (100, 32), (100, 33), (300, 64), (1000, 200),
+                                      (1000, 999), (257, 100)])
+@pytest.mark.parametrize("B,H,Hkv,p", [(1, 4, 2, 0.0), (2, 2, 1, 0.1)])
+def test_flash_attention_sliding_window(T, window, B, H, Hkv, p, cuda):
+    """Mistral-style sliding window at head_dim 128 (key k visible to query q iff
+    q - window < k <= q): skipped and boundary-masked tiles, tail tiles, GQA and
+    dropout, fwd + bwd vs the fp32 reference with the same masks."""
+    hip.require()
+    D = 128
+    torch.manual_seed(T + window)
+    q = torch.randn(B, T, H, D, device=cuda, dtype=torch.bfloat16)
+    k = torch.randn(B, T, Hkv, D, device=cuda, dtype=torch.bfloat16)
+    v = torch.randn(B, T, Hkv, D, device=cuda, dtype=torch.bfloat16)
+    dout = torch.randn(B, T, H * D, device=cuda, dtype=torch.bfloat16)
+    assert fused._attn_ok(q, T, D, window)
+    qs, ks, vs = (t.clone().requires_grad_() for t in (q, k, v))
+    out = fused._FlashAttn.apply(qs, ks, vs, p, 77, window).view(B, T, H * D)
+    out.backward(dout)
+    qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
+    ref = fused.reference_attention(qr, kr, vr, p, 77, window)
+    ref.backward(dout.float())
+    # window 1: each query sees only itself -- dq, dk are exactly 0 in fp32
+    floor = vr.grad.abs().max().item() if window == 1 else 0.0
+    _close(out, ref, 2e-2)
+    _close(qs.grad, qr.grad, 3e-2, floor)
+    _close(ks.grad, kr.grad, 3e-2, floor)
+    _close(vs.grad, vr.grad, 3e-2)
+
+
+@pytest.mark.gpu
+def test_sliding_window_rope_attention_and_mistral_model(cuda):
+    """The Llama-path op with a window (RoPE fused into the backward stores) and
+    a small Mistral (head_dim 128, window < T) against HF's model on the GPU."""
+    import transformers
+
+    from distributed_lion_pytorch_amd.models.llama import MistralForCausalLM
+
+    hip.require()
+    torch.manual_seed(3)
+    cfg = transformers.MistralConfig(vocab_size=256, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                                     num_attention_heads=2, num_key_value_heads=1, max_position_embeddings=512,
+                                     sliding_window=96)
+    ours = MistralForCausalLM(cfg)
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        ours.save_pretrained(d)
+        hf = transformers.MistralForCausalLM.from_pretrained(d)
+    ours, hf = ours.to(cuda, torch.bfloat16), hf.to(cuda, torch.float32)
+    ids = torch.randint(0, 256, (2, 300), device=cuda)
+    la = ours(ids, labels=ids).loss
+    lb = hf(ids, labels=ids).loss
+    assert abs(la.item() - lb.item()) < 2e-2, (la.item(), lb.item())
+    la.backward()
+    lb.backward()
+    for (n, p_), (_, r) in zip(ours.named_parameters(), hf.named_parameters()):
+        if r.grad is not None and r.grad.abs().max() > 0:
+            err = (p_.grad.float() - r.grad).abs().max().item() / r.grad.abs().max().item()
+            assert err < 0.1, (n, err)
+
+
+@pytest.mark.gpu
 def test_packed_qkv_bias_grad_tail_tile(cuda):
     """GPT-2's fused c_attn + attention at T = 100: the kernels' per-tile bias
     partials cover ceil(T/32) tiles with the tail rows excluded."""

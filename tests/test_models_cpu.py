@@ -58,16 +58,25 @@ def _small(cls, **kw):
                num_key_value_heads=2, max_position_embeddings=128, **kw)
 
 
-@pytest.mark.parametrize("family", ["mistral", "qwen2"])
+@pytest.mark.parametrize("family", ["mistral", "qwen2", "qwen2-sliding"])
 def test_mistral_qwen2_match_hf(family):
+    """Loss / grads / checkpoint round trip against the HF classes.  The
+    sequence (40) is longer than the sliding windows (mistral: every layer 16;
+    qwen2-sliding: layer 1 of 2, window 12), so the windowed masks are covered."""
     from distributed_lion_pytorch_amd.models import llama as L
     from distributed_lion_pytorch_amd.models.registry import NATIVE
     if family == "mistral":
-        cfg, ours_cls, hf_cls = _small(transformers.MistralConfig, sliding_window=48), L.MistralForCausalLM, \
+        cfg, ours_cls, hf_cls = _small(transformers.MistralConfig, sliding_window=16), L.MistralForCausalLM, \
             transformers.MistralForCausalLM
-    else:
+    elif family == "qwen2":
         cfg, ours_cls, hf_cls = _small(transformers.Qwen2Config, tie_word_embeddings=True), L.Qwen2ForCausalLM, \
             transformers.Qwen2ForCausalLM
+    else:
+        cfg = _small(transformers.Qwen2Config, tie_word_embeddings=True, use_sliding_window=True, sliding_window=12,
+                     max_window_layers=1)
+        ours_cls, hf_cls = L.Qwen2ForCausalLM, transformers.Qwen2ForCausalLM
+    expect_windows = {"mistral": [16, 16], "qwen2": [0, 0], "qwen2-sliding": [0, 12]}[family]
+    family = family.split("-")[0]
     assert NATIVE[family] is ours_cls
     torch.manual_seed(0)
     ours = ours_cls(cfg)
@@ -90,9 +99,23 @@ def test_mistral_qwen2_match_hf(family):
     la.backward()
     lb.backward()
     _grads_close(ours, hf)
-    if family == "mistral":  # past the sliding window the native full-causal attention refuses
-        with pytest.raises(NotImplementedError, match="sliding"):
-            ours(torch.randint(0, cfg.vocab_size, (1, 49)))
+    assert [layer.self_attn.window for layer in ours.model.layers] == expect_windows
+
+
+def test_sliding_window_attention_reference():
+    """The masked SDPA path (CPU / head_dims without a kernel): query q sees
+    keys q - window < k <= q, and a window covering T is plain causal."""
+    torch.manual_seed(0)
+    q, k, v = (torch.randn(2, 37, 4, 16) for _ in range(3))
+    w = 8
+    out = fused.causal_attention_gqa(q, k, v, 0.0, window=w).view(2, 37, 4, 16)
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) / 4.0
+    i = torch.arange(37)
+    ok = (i[:, None] >= i[None, :]) & (i[:, None] - i[None, :] < w)
+    ref = torch.einsum("bhqk,bkhd->bqhd", s.masked_fill(~ok, float("-inf")).softmax(-1), v)
+    assert torch.allclose(out, ref, atol=1e-5)
+    full = fused.causal_attention_gqa(q, k, v, 0.0)
+    assert torch.equal(fused.causal_attention_gqa(q, k, v, 0.0, window=37), full)
 
 
 def test_fused_ce_matches_reference_and_normalizer():
