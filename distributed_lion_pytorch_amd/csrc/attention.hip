@@ -796,6 +796,10 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   // at the last query its highest key reaches)
   const int win = window_of<D>(a);
   const int qhi = win > 0 ? min(ntiles - 1, (first * 32 + 127 + win - 1) >> 5) : ntiles - 1;
+  // this wave's last in-window query tile, and the first query tile holding a
+  // query at or past (lowest key) + window: only those need the element mask
+  const int wq_last = win > 0 ? (kb + 30 + win) >> 5 : ntiles;
+  const int wq_cut = win > 0 ? kb + win - 31 : 1 << 30;
   const int nq = qhi - first + 1;
   const int total = group * nq;    // (head, query tile) steps, head-major
   // step i -> buffer i&1: Q and dO tiles by LDS-DMA; wave 0 also DMAs the 32
@@ -840,7 +844,7 @@ attn_bwd_dkv_kernel(AttnArgs a) {
     vm_wait_n(min(total - 1 - i, NB - 2) * per_stage);  // step i landed (later steps may be in flight)
     __syncthreads();  // for every wave; and every wave is done with the buffer restaged next
     if (i + NB - 1 < total) stage_next((i + NB - 1) % NB);
-    if (active && qt >= ktile && (win == 0 || qt * 32 <= kb + 30 + win)) {  // wave-uniform
+    if (active && qt >= ktile && (D != 128 || qt <= wq_last)) {  // wave-uniform
       const int qb = qt * 32;
       f32x16 s = zero16(), dp = zero16();
       DLION_PRIO_ON(kDkvPrio, 1);
@@ -860,10 +864,11 @@ attn_bwd_dkv_kernel(AttnArgs a) {
         for (int reg = 0; reg < 16; ++reg)
           if (qb + acc_row(reg, hf) >= a.T) s[reg] = -INFINITY;
       }
-      if (win > 0 && qb + 31 - kb >= win) {  // sliding window: queries at or past key + window
+      if (D == 128 && qb >= wq_cut) {  // sliding window: queries at or past key + window (window_of<D> reloaded here)
+        const int kw = key + window_of<D>(a);
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg)
-          if (qb + acc_row(reg, hf) - key >= win) s[reg] = -INFINITY;
+          if (qb + acc_row(reg, hf) >= kw) s[reg] = -INFINITY;
       }
       // row statistics of the lane's 16 query rows: rows (reg&3) + 8(reg>>2) + 4hf
       // come in 4 runs of 4 consecutive rows -> 16-byte LDS reads (broadcast),
