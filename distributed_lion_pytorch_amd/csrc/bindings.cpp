@@ -725,6 +725,20 @@ bool lt_gemm_nn(const Tensor& a, const Tensor& b, const Tensor& out) {
                         a.size(0), b.size(1), a.size(1), 0, a.device().index(), cur_stream(), dlion::Layout::NN, false);
 }
 
+// out [M, N] (+)= a [M, K] . b [N, K]^T, plain epilogue, beta = 1 when accumulating (a weight gradient from
+// token-contiguous operand copies).
+bool lt_gemm_nt_acc(const Tensor& a, const Tensor& b, const Tensor& out, bool accumulate) {
+  check_gemm_operand(a, "a");
+  check_gemm_operand(b, "b");
+  check_gemm_operand(out, "out");
+  TORCH_CHECK(a.size(1) == b.size(1) && out.size(0) == a.size(0) && out.size(1) == b.size(0),
+              "dlion lt_gemm_nt_acc: shape mismatch a=", a.sizes(), " b=", b.sizes(), " out=", out.sizes());
+  const c10::DeviceGuard g(a.device());
+  return dlion::lt_gemm(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0), nullptr,
+                        a.size(0), b.size(0), a.size(1), 0, a.device().index(), cur_stream(), dlion::Layout::NT,
+                        accumulate);
+}
+
 // out [M, N] (+)= a [K, M]^T . b [K, N] (a weight gradient over the token axis; accumulate: beta = 1).
 bool lt_gemm_tn(const Tensor& a, const Tensor& b, const Tensor& out, bool accumulate) {
   check_gemm_operand(a, "a");
@@ -1101,6 +1115,7 @@ TORCH_LIBRARY(dlion, m) {
   m.def("lt_gemm_nt(Tensor a, Tensor b, Tensor? bias, int epi, Tensor(a!) out) -> bool");
   m.def("lt_gemm_nn(Tensor a, Tensor b, Tensor(a!) out) -> bool");
   m.def("lt_gemm_tn(Tensor a, Tensor b, Tensor(a!) out, bool accumulate) -> bool");
+  m.def("lt_gemm_nt_acc(Tensor a, Tensor b, Tensor(a!) out, bool accumulate) -> bool");
   m.def("gemm_nt(Tensor a, Tensor b, Tensor? bias) -> Tensor");
   m.def("gemm_nt_out(Tensor a, Tensor b, Tensor? bias, Tensor(a!) out) -> ()");
   m.def("gemm_nt_gelu(Tensor a, Tensor b, Tensor bias, bool exact) -> (Tensor, Tensor)");
@@ -1184,6 +1199,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("lt_gemm_nt", &lt_gemm_nt);
   m.impl("lt_gemm_nn", &lt_gemm_nn);
   m.impl("lt_gemm_tn", &lt_gemm_tn);
+  m.impl("lt_gemm_nt_acc", &lt_gemm_nt_acc);
   m.impl("gemm_tn", &gemm_tn);
   m.impl("gemm_tn_", &gemm_tn_);
   m.impl("lora_rows", &lora_rows);

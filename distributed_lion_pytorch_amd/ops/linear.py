@@ -544,6 +544,20 @@ def split_k_factor(M: int, K: int, N: int) -> int:
     return s
 
 
+def _wgrad_via_transposes(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool) -> bool:
+    """out (+)= a^T b as hipBLASLt's NT form (both operands contraction-
+    contiguous, its fastest layout: 1.5-1.6 PF/s at Llama-3-8B shapes against
+    1.1-1.3 for the TN forms) on token-contiguous copies a^T, b^T made by the
+    LDS-tiled transpose kernel -- the copies cost ~1/8 of the GEMM at
+    gate_up / down_proj (tools/r5/bench_wgrad_lt.py)."""
+    from . import hip
+
+    at, bt = fast_transpose(a), fast_transpose(b)
+    ok = hip.ops().lt_gemm_nt_acc(at, bt, out, accumulate)
+    del at, bt
+    return ok
+
+
 def _direct_split_pick(a: torch.Tensor, b: torch.Tensor, s: int, own: bool) -> bool:
     """A split own-TN weight gradient outside a multi-micro-batch window goes
     through _unsplit_wgrad's per-shape timing instead (the split launch is one
@@ -577,15 +591,20 @@ def _unsplit_wgrad(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumula
                     [hip.ops().gemm_tn([a], [b], split).view(split, K * N)], scratch.view(-1), False)
             if _LT_TN and _lt_nn_ok(a, b):  # hipBLASLt's TN form with the searched algorithm
                 cands["lt"] = lambda: hip.ops().lt_gemm_tn(a, b, scratch, False) or torch.mm(a.t(), b, out=scratch)
+                if _LT_TT:
+                    cands["lt_tt"] = lambda: (_wgrad_via_transposes(a, b, scratch, False)
+                                              or torch.mm(a.t(), b, out=scratch))
             name = _pick(key, cands)
             del scratch
         if name == "lt" and hip.ops().lt_gemm_tn(a, b, out2, accumulate):
+            return
+        if name == "lt_tt" and _wgrad_via_transposes(a, b, out2, accumulate):
             return
         if name == "split":
             hip.ops().sum_partials_multi_([hip.ops().gemm_tn([a], [b], split).view(split, K * N)], out2.view(-1),
                                           accumulate)
             return
-        if name in ("blas", "lt"):
+        if name in ("blas", "lt", "lt_tt"):
             if accumulate:
                 out2.addmm_(a.t(), b)
             else:
@@ -833,6 +852,7 @@ def gemm_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
 
 _LT_NN = os.environ.get("DLION_LT_NN", "1") != "0"  # A/B switch: 0 drops the hipBLASLt NN candidate
 _LT_TN = os.environ.get("DLION_LT_TN", "1") != "0"  # A/B switch: 0 drops the hipBLASLt TN weight-gradient candidate
+_LT_TT = os.environ.get("DLION_LT_TT", "1") != "0"  # A/B switch: 0 drops the transposed-copies NT candidate
 
 
 def _lt_nn(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:

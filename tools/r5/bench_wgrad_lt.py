@@ -43,6 +43,7 @@ def main():
             cands[f"own_split{s}"] = lambda: ops.sum_partials_acc_(ops.gemm_tn([dy], [x], s).view(s, -1), out)
         if ops.lt_gemm_tn(dy, x, out, True):
             cands["lt_tn"] = lambda: ops.lt_gemm_tn(dy, x, out, True)
+        cands["lt_nt_transposed"] = lambda: linear._wgrad_via_transposes(dy, x, out, True)
         ref = (dy.float().t() @ x.float())
         chk = torch.empty_like(out)
         assert ops.lt_gemm_tn(dy, x, chk, False)
