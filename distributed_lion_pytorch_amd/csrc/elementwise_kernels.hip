@@ -385,12 +385,13 @@ __global__ void __launch_bounds__(kTallQ * kTallR) sum_partials_split_kernel(con
 // 256-thread block through LDS: 16-byte row loads, 2-byte LDS column reads (row pitch 66
 // elements = 33 dwords: the 8 rows a lane gathers fall in distinct banks), 16-byte stores.
 __global__ void __launch_bounds__(256) transpose_pad_kernel(const uint16_t* __restrict__ x, int64_t R, int64_t C,
-                                                            int64_t ldx, uint16_t* __restrict__ out, int64_t Rp) {
+                                                            int64_t ldx, uint16_t* __restrict__ out, int64_t Rp,
+                                                            int tr_path) {
   // rows padded to 72 elements (144 B): 16-byte aligned for the b128 stores,
   // and the 4 rows of a transposed read land on disjoint bank ranges
   __shared__ __attribute__((aligned(16))) uint16_t tile[64][72];
   const int64_t r0 = static_cast<int64_t>(blockIdx.y) * 64, c0 = static_cast<int64_t>(blockIdx.x) * 64;
-  if (r0 + 64 <= R && c0 + 64 <= C) {  // full tile (block-uniform): 16-byte LDS stores, hardware-transposed reads
+  if (tr_path && r0 + 64 <= R && c0 + 64 <= C) {  // full tile (block-uniform): b128 LDS stores, transposed reads
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int idx = threadIdx.x + h * 256, tr = idx >> 3, tc = (idx & 7) * 8;
@@ -581,7 +582,7 @@ hipError_t launch_sum_partials_multi(const float* const* ptrs, const int64_t* ro
 }
 
 hipError_t launch_transpose_pad(const void* x, int64_t R, int64_t C, int64_t ldx, void* out, int64_t Rp,
-                                hipStream_t st) {
+                                hipStream_t st, bool tr_path) {
   if (R <= 0 || C <= 0) return hipSuccess;
   if (Rp < R || Rp % 8 != 0 || ldx % 8 != 0 || ldx < C || reinterpret_cast<uintptr_t>(x) % 16 != 0 ||
       reinterpret_cast<uintptr_t>(out) % 16 != 0)
@@ -589,7 +590,7 @@ hipError_t launch_transpose_pad(const void* x, int64_t R, int64_t C, int64_t ldx
   const int64_t gx = (C + 63) / 64, gy = (Rp + 63) / 64;
   if (gx > 0x7fffffff || gy > 65535) return hipErrorInvalidValue;
   hipLaunchKernelGGL(transpose_pad_kernel, dim3(static_cast<unsigned>(gx), static_cast<unsigned>(gy)), dim3(256), 0, st,
-                     static_cast<const uint16_t*>(x), R, C, ldx, static_cast<uint16_t*>(out), Rp);
+                     static_cast<const uint16_t*>(x), R, C, ldx, static_cast<uint16_t*>(out), Rp, tr_path ? 1 : 0);
   return hipGetLastError();
 }
 
