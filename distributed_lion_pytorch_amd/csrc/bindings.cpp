@@ -1058,7 +1058,7 @@ void dequant4_(const Tensor& q, const Tensor& absmax, const Tensor& code, const 
 }
 
 // out [C, Rp] = x [R, C]^T zero-padded to Rp columns (16-bit dtypes; the per-step weight layouts)
-Tensor transpose_pad(const Tensor& x, int64_t rows_out, bool tr_path) {
+Tensor transpose_pad(const Tensor& x, int64_t rows_out) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1 && x.element_size() == 2,
               "dlion transpose_pad: x must be a 2-D 16-bit GPU tensor with unit column stride");
   const int64_t R = x.size(0), C = x.size(1);
@@ -1067,7 +1067,7 @@ Tensor transpose_pad(const Tensor& x, int64_t rows_out, bool tr_path) {
               "dlion transpose_pad: needs rows_out >= rows, rows_out % 8 == 0, row stride % 8 == 0, 16-byte alignment");
   const c10::DeviceGuard g(x.device());
   auto out = at::empty({C, Rp}, x.options());
-  check_hip(dlion::launch_transpose_pad(x.data_ptr(), R, C, x.stride(0), out.data_ptr(), Rp, cur_stream(), tr_path),
+  check_hip(dlion::launch_transpose_pad(x.data_ptr(), R, C, x.stride(0), out.data_ptr(), Rp, cur_stream()),
             "transpose_pad");
   return out;
 }
@@ -1094,7 +1094,7 @@ void dequant4_t_(const Tensor& q, const Tensor& absmax, const Tensor& code, cons
 
 TORCH_LIBRARY(dlion, m) {
   m.def("dequant4_t_(Tensor q, Tensor absmax, Tensor code, Tensor(a!) out) -> ()");
-  m.def("transpose_pad(Tensor x, int rows_out=-1, bool tr_path=True) -> Tensor");
+  m.def("transpose_pad(Tensor x, int rows_out=-1) -> Tensor");
   m.def("quant4(Tensor w, Tensor code) -> (Tensor, Tensor)");
   m.def("dequant4_(Tensor q, Tensor absmax, Tensor code, Tensor(a!) out) -> ()");
   m.def("gemm_tn(Tensor[] P, Tensor[] Q, int splits) -> Tensor");

@@ -385,40 +385,9 @@ __global__ void __launch_bounds__(kTallQ * kTallR) sum_partials_split_kernel(con
 // 256-thread block through LDS: 16-byte row loads, 2-byte LDS column reads (row pitch 66
 // elements = 33 dwords: the 8 rows a lane gathers fall in distinct banks), 16-byte stores.
 __global__ void __launch_bounds__(256) transpose_pad_kernel(const uint16_t* __restrict__ x, int64_t R, int64_t C,
-                                                            int64_t ldx, uint16_t* __restrict__ out, int64_t Rp,
-                                                            int tr_path) {
-  // rows padded to 72 elements (144 B): 16-byte aligned for the b128 stores,
-  // and the 4 rows of a transposed read land on disjoint bank ranges
-  __shared__ __attribute__((aligned(16))) uint16_t tile[64][72];
+                                                            int64_t ldx, uint16_t* __restrict__ out, int64_t Rp) {
+  __shared__ uint16_t tile[64][66];
   const int64_t r0 = static_cast<int64_t>(blockIdx.y) * 64, c0 = static_cast<int64_t>(blockIdx.x) * 64;
-  if (tr_path && r0 + 64 <= R && c0 + 64 <= C) {  // full tile (block-uniform): b128 LDS stores, transposed reads
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int idx = threadIdx.x + h * 256, tr = idx >> 3, tc = (idx & 7) * 8;
-      *reinterpret_cast<uint4*>(&tile[tr][tc]) = *reinterpret_cast<const uint4*>(x + (r0 + tr) * ldx + c0 + tc);
-    }
-    __syncthreads();
-    // wave w: tile columns 16w .. 16w+15; 16-lane group g, step u: tile rows 8(g + 4u) .. +7.  A
-    // ds_read_b64_tr_b16 gives lane i of a group column i of 4 rows (lane 4q+p addresses row q,
-    // columns 4p..4p+3), two of them one 8-row output chunk: 16 output rows x 64 contiguous bytes
-    // per store instruction
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
-    const int col = 16 * w + 4 * (i & 3);
-    typedef short tp_s16x4 __attribute__((ext_vector_type(4)));
-    typedef int tp_i32x2 __attribute__((ext_vector_type(2)));
-    typedef __attribute__((address_space(3))) tp_s16x4 lds_s16x4;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int rb = 8 * (g + 4 * u);
-      const tp_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&tile[rb + (i >> 2)][col]));
-      const tp_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&tile[rb + 4 + (i >> 2)][col]));
-      const tp_i32x2 l2 = __builtin_bit_cast(tp_i32x2, lo), h2 = __builtin_bit_cast(tp_i32x2, hi);
-      *reinterpret_cast<uint4*>(out + (c0 + 16 * w + i) * Rp + r0 + rb) =
-          make_uint4(static_cast<uint32_t>(l2[0]), static_cast<uint32_t>(l2[1]), static_cast<uint32_t>(h2[0]),
-                     static_cast<uint32_t>(h2[1]));
-    }
-    return;
-  }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int idx = threadIdx.x + h * 256;  // 512 chunks of 8 elements: 64 rows x 8 chunks
@@ -582,7 +551,7 @@ hipError_t launch_sum_partials_multi(const float* const* ptrs, const int64_t* ro
 }
 
 hipError_t launch_transpose_pad(const void* x, int64_t R, int64_t C, int64_t ldx, void* out, int64_t Rp,
-                                hipStream_t st, bool tr_path) {
+                                hipStream_t st) {
   if (R <= 0 || C <= 0) return hipSuccess;
   if (Rp < R || Rp % 8 != 0 || ldx % 8 != 0 || ldx < C || reinterpret_cast<uintptr_t>(x) % 16 != 0 ||
       reinterpret_cast<uintptr_t>(out) % 16 != 0)
@@ -590,7 +559,7 @@ hipError_t launch_transpose_pad(const void* x, int64_t R, int64_t C, int64_t ldx
   const int64_t gx = (C + 63) / 64, gy = (Rp + 63) / 64;
   if (gx > 0x7fffffff || gy > 65535) return hipErrorInvalidValue;
   hipLaunchKernelGGL(transpose_pad_kernel, dim3(static_cast<unsigned>(gx), static_cast<unsigned>(gy)), dim3(256), 0, st,
-                     static_cast<const uint16_t*>(x), R, C, ldx, static_cast<uint16_t*>(out), Rp, tr_path ? 1 : 0);
+                     static_cast<const uint16_t*>(x), R, C, ldx, static_cast<uint16_t*>(out), Rp);
   return hipGetLastError();
 }
 

@@ -62,8 +62,7 @@ hipError_t launch_sum_partials_multi(const float* const* ptrs, const int64_t* ro
 int sum_partials_split_factor(int64_t n, int64_t total_rows);
 // out [C, Rp] (16-bit elements) = x [R, C]^T (row stride ldx), output columns R..Rp-1 zero; Rp % 8 == 0
 hipError_t launch_transpose_pad(const void* x, int64_t R, int64_t C, int64_t ldx, void* out, int64_t Rp,
-                                hipStream_t st,
-                                bool tr_path = true);
+                                hipStream_t st);
 hipError_t launch_sum_partials_split(const float* const* ptrs, const int64_t* rows, const int64_t* lds, int nseg,
                                      int64_t n, int Y, float* scratch, void* out, bool accumulate, const float* scale,
                                      hipStream_t st);
