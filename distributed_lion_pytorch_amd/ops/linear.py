@@ -85,7 +85,6 @@ class _FusionState:
         self.pending: list = []  # keys written in the current window, in order
         self.wdefer: dict = {}  # key -> [params, cols, [a segments], [b segments], [versions]]
         self.wdefer_bytes = [0]
-        self.tt_pref = None  # (a, b, a^T, b^T, event): copies started by _tt_prefetch
 
 
 _ST = _FusionState()
@@ -550,57 +549,13 @@ def _wgrad_via_transposes(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, a
     contiguous, its fastest layout: 1.5-1.6 PF/s at Llama-3-8B shapes against
     1.1-1.3 for the TN forms) on token-contiguous copies a^T, b^T made by the
     LDS-tiled transpose kernel -- the copies cost ~1/8 of the GEMM at
-    gate_up / down_proj (tools/r5/bench_wgrad_lt.py).  Copies started earlier
-    on the side stream by _tt_prefetch (beside the input-gradient GEMM) are
-    used when they match."""
+    gate_up / down_proj (tools/r5/bench_wgrad_lt.py)."""
     from . import hip
 
-    pref, _ST.tt_pref = _ST.tt_pref, None
-    if pref is not None and _same_view(pref[0], a) and _same_view(pref[1], b):
-        main = torch.cuda.current_stream(a.device)
-        main.wait_event(pref[4])
-        at, bt = pref[2], pref[3]
-        at.record_stream(main)
-        bt.record_stream(main)
-    else:
-        at, bt = fast_transpose(a), fast_transpose(b)
+    at, bt = fast_transpose(a), fast_transpose(b)
     ok = hip.ops().lt_gemm_nt_acc(at, bt, out, accumulate)
     del at, bt
     return ok
-
-
-def _same_view(x: torch.Tensor, y: torch.Tensor) -> bool:
-    return x.data_ptr() == y.data_ptr() and x.shape == y.shape and x.stride() == y.stride()
-
-
-_TT_PREFETCH = os.environ.get("DLION_TT_PREFETCH", "1") != "0"  # A/B switch: copies beside the dgrad GEMM
-_SIDE: dict = {}  # device index -> side stream for the prefetched copies
-
-
-def _tt_prefetch(a: torch.Tensor, b: torch.Tensor) -> None:
-    """If this weight gradient's timed pick is the transposed-copy NT form,
-    start its two operand copies now on a side stream: they run beside the
-    input-gradient GEMM the backward issues next (compute-bound, while the
-    copies are HBM-bound) instead of in front of the weight-gradient GEMM."""
-    if not (_LT_TT and _TT_PREFETCH and a.is_cuda and a.dtype == torch.bfloat16) or (
-            _ST.fuse["on"] and _ST.fuse["multi"]) or torch.cuda.is_current_stream_capturing():
-        return
-    M, K = a.shape
-    s, own = wgrad_splits(a, b)
-    if _GEMM_PICK.get(("wgrad", M, K, b.shape[1], a.stride(0), b.stride(0), s)) != "lt_tt":
-        return
-    dev = a.device
-    side = _SIDE.get(dev.index)
-    if side is None:
-        side = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
-    side.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(side):
-        at, bt = fast_transpose(a), fast_transpose(b)
-        ev = torch.cuda.Event()
-        ev.record(side)
-    a.record_stream(side)
-    b.record_stream(side)
-    _ST.tt_pref = (a, b, at, bt, ev)
 
 
 def _direct_split_pick(a: torch.Tensor, b: torch.Tensor, s: int, own: bool) -> bool:
@@ -999,8 +954,6 @@ class _LinearNK(torch.autograd.Function):
     def backward(ctx, dy):
         x2d, w = ctx.saved_tensors
         dy = dy.contiguous()
-        if ctx.needs_input_grad[1] and ctx.fuse and ctx.needs_input_grad[0]:
-            _tt_prefetch(dy, x2d)
         dx = gemm_dgrad(dy, ctx.w, not ctx.w.requires_grad) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
@@ -1117,12 +1070,10 @@ class _LinearMultiNK(torch.autograd.Function):
             dy = torch.cat([g.reshape(-1, g.shape[-1]) for g in grads], -1)
         dy = dy.reshape(-1, dy.shape[-1])
         dx = None
-        want = [ctx.needs_input_grad[1 + i] for i in range(len(ws))]
         if ctx.needs_input_grad[0]:
-            if all(ctx.fuse) and all(want):
-                _tt_prefetch(dy, x2d)
             dx = gemm_dgrad(dy, cat_weights(ctx.ws), not any(w.requires_grad for w in ctx.ws))
         dws = [None] * len(ws)
+        want = [ctx.needs_input_grad[1 + i] for i in range(len(ws))]
         if any(want):
             if all(ctx.fuse) and all(want):
                 _multi_wgrad_into(dy, x2d, ctx.params, ctx.sizes)

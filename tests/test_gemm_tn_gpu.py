@@ -333,39 +333,3 @@ def test_direct_split_weight_gradient_goes_through_the_timed_pick(cuda, monkeypa
     ref = dy.float().t() @ x.float()
     got = torch.cat([p.grad.float() for p in ps], 0)
     assert (got - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
-
-
-def test_transposed_copy_weight_gradient_prefetched_beside_dgrad(cuda, monkeypatch):
-    """With the transposed-copy NT form picked for a weight gradient, its
-    operand copies start on a side stream before the input-gradient GEMM and
-    the weight-gradient GEMM consumes them; both gradients match fp32."""
-    from distributed_lion_pytorch_amd.ops import linear as L
-
-    hip.require()
-    torch.manual_seed(8)
-    M, K, sizes = 4096, 1024, [1536, 512]
-    x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16, requires_grad=True)
-    ws = [torch.nn.Parameter((torch.randn(n, K, device=cuda) / K ** 0.5).to(torch.bfloat16)) for n in sizes]
-    dys = [torch.randn(M, n, device=cuda, dtype=torch.bfloat16) for n in sizes]
-    monkeypatch.setattr(L, "_GEMM_PICK", {})
-    seen = []
-    orig = L._wgrad_via_transposes
-
-    def spy(a, b, out, acc):
-        seen.append(L._ST.tt_pref is not None)
-        return orig(a, b, out, acc)
-
-    monkeypatch.setattr(L, "_wgrad_via_transposes", spy)
-    s, _ = L.wgrad_splits(torch.empty(M, sum(sizes), device=cuda, dtype=torch.bfloat16), x.detach())
-    L._GEMM_PICK[("wgrad", M, sum(sizes), K, sum(sizes), K, s)] = "lt_tt"
-    with L.grad_accumulation_fusion(True, micro_batches=1):
-        outs = L.linear_multi_nk(x, ws)
-        torch.autograd.backward(outs, dys)
-    assert seen and seen[0], "the weight gradient did not use prefetched copies"
-    assert L._ST.tt_pref is None
-    dyc = torch.cat([d.float() for d in dys], 1)
-    ref_dw = dyc.t() @ x.detach().float()
-    got_dw = torch.cat([w.grad.float() for w in ws], 0)
-    assert (got_dw - ref_dw).abs().max().item() <= 1e-2 * ref_dw.abs().max().item()
-    ref_dx = dyc @ torch.cat([w.detach().float() for w in ws], 0)
-    assert (x.grad.float() - ref_dx).abs().max().item() <= 1e-2 * ref_dx.abs().max().item()
