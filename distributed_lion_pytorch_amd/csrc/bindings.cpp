@@ -17,7 +17,7 @@
 #include "kernels.h"
 
 namespace dlion {
-enum class Layout : int { NT = 0, NN = 1, TN = 2 };
+enum class Layout : int { NT = 0, NN = 1, TN = 2, TT = 3 };
 bool lt_gemm(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, const void* bias,
              int64_t M, int64_t N, int64_t K, int epi, int device, hipStream_t s, Layout lay, bool accumulate);
 }
@@ -739,6 +739,23 @@ bool lt_gemm_nt_acc(const Tensor& a, const Tensor& b, const Tensor& out, bool ac
                         accumulate);
 }
 
+// Any of the four layouts with beta = 1 when accumulating: out [M, N] (+)= op(a) . op(b) with
+// layout 0 NT: a [M, K], b [N, K];  1 NN: a [M, K], b [K, N];  2 TN: a [K, M], b [K, N];  3 TT: a [K, M], b [N, K].
+bool lt_gemm_layout(const Tensor& a, const Tensor& b, const Tensor& out, int64_t layout, bool accumulate) {
+  check_gemm_operand(a, "a");
+  check_gemm_operand(b, "b");
+  check_gemm_operand(out, "out");
+  TORCH_CHECK(layout >= 0 && layout <= 3, "dlion lt_gemm_layout: layout must be 0..3");
+  const bool at = layout >= 2, bt = layout == 0 || layout == 3;  // a stored [K, M]; b stored [N, K]
+  const int64_t M = at ? a.size(1) : a.size(0), K = at ? a.size(0) : a.size(1), N = bt ? b.size(0) : b.size(1);
+  TORCH_CHECK((bt ? b.size(1) : b.size(0)) == K && out.size(0) == M && out.size(1) == N,
+              "dlion lt_gemm_layout: shape mismatch a=", a.sizes(), " b=", b.sizes(), " out=", out.sizes(),
+              " layout ", layout);
+  const c10::DeviceGuard g(a.device());
+  return dlion::lt_gemm(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0), nullptr,
+                        M, N, K, 0, a.device().index(), cur_stream(), static_cast<dlion::Layout>(layout), accumulate);
+}
+
 // out [M, N] (+)= a [K, M]^T . b [K, N] (a weight gradient over the token axis; accumulate: beta = 1).
 bool lt_gemm_tn(const Tensor& a, const Tensor& b, const Tensor& out, bool accumulate) {
   check_gemm_operand(a, "a");
@@ -1116,6 +1133,7 @@ TORCH_LIBRARY(dlion, m) {
   m.def("lt_gemm_nn(Tensor a, Tensor b, Tensor(a!) out) -> bool");
   m.def("lt_gemm_tn(Tensor a, Tensor b, Tensor(a!) out, bool accumulate) -> bool");
   m.def("lt_gemm_nt_acc(Tensor a, Tensor b, Tensor(a!) out, bool accumulate) -> bool");
+  m.def("lt_gemm_layout(Tensor a, Tensor b, Tensor(a!) out, int layout, bool accumulate) -> bool");
   m.def("gemm_nt(Tensor a, Tensor b, Tensor? bias) -> Tensor");
   m.def("gemm_nt_out(Tensor a, Tensor b, Tensor? bias, Tensor(a!) out) -> ()");
   m.def("gemm_nt_gelu(Tensor a, Tensor b, Tensor bias, bool exact) -> (Tensor, Tensor)");
@@ -1200,6 +1218,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("lt_gemm_nn", &lt_gemm_nn);
   m.impl("lt_gemm_tn", &lt_gemm_tn);
   m.impl("lt_gemm_nt_acc", &lt_gemm_nt_acc);
+  m.impl("lt_gemm_layout", &lt_gemm_layout);
   m.impl("gemm_tn", &gemm_tn);
   m.impl("gemm_tn_", &gemm_tn_);
   m.impl("lora_rows", &lora_rows);

@@ -9,7 +9,9 @@
 // nn.Linear weight as stored, no W^T copy) is D^T = b_cm[N,K] . a^T (transA = N);
 // the TN form out[M,N] (+)= a[K,M]^T . b[K,N] (lt_gemm_tn: a weight gradient
 // dY^T X over the token axis) is D^T = b_cm[N,K] . op_T(a_cm[M,K]) (transB = T),
-// with beta = 1 to accumulate onto the gradient (tuned on a scratch output).  Epilogue 2 is
+// with beta = 1 to accumulate onto the gradient (tuned on a scratch output);
+// TT: out[M,N] (+)= a[K,M]^T . b[N,K]^T (a weight gradient with one operand
+// copied token-contiguous) is D^T = op_T(b_cm[K,N]) . op_T(a_cm[M,K]).  Epilogue 2 is
 // the GPT-2 MLP up-projection when no backward follows (evaluation, frozen
 // reference models): one GEMM instead of GEMM + a bias+GELU pass over the
 // [tokens, 4C] activation.  Training keeps the separate kernel because the
@@ -51,7 +53,7 @@
 
 namespace dlion {
 
-enum class Layout : int { NT = 0, NN = 1, TN = 2 };
+enum class Layout : int { NT = 0, NN = 1, TN = 2, TT = 3 };
 
 namespace {
 
@@ -132,11 +134,11 @@ Plan& get_plan(DevState& st, const Key& key, int64_t m, int64_t n, int64_t k, in
   if (it != g_plans.end()) return it->second;
   Plan& p = g_plans[key];
   p.beta = beta;
-  const bool nn = lay == Layout::NN, tn = lay == Layout::TN;
+  const bool nn = lay == Layout::NN, tn = lay == Layout::TN, tt = lay == Layout::TT;
   lt_check(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F), "hipblasLtMatmulDescCreate");
   const int32_t opT = HIPBLAS_OP_T, opN = HIPBLAS_OP_N;
   set_attr(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, nn || tn ? &opN : &opT, sizeof(opT));
-  set_attr(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, tn ? &opT : &opN, sizeof(opN));
+  set_attr(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, tn || tt ? &opT : &opN, sizeof(opN));
   const hipblasLtEpilogue_t e = epilogue_of(epi);
   set_attr(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e));
   if (epi == 1 || epi == 2) {
@@ -147,7 +149,7 @@ Plan& get_plan(DevState& st, const Key& key, int64_t m, int64_t n, int64_t k, in
   // A_cm: b viewed column-major [K, N] (NN / TN: [N, K]) (ld = ldb); B_cm: a as [K, M] (TN: [M, K])
   // (ld = lda); D: [N, M] (ld = ldc)
   lt_check(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, nn || tn ? n : k, nn || tn ? k : n, ldb), "layout A");
-  lt_check(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, tn ? m : k, tn ? k : m, lda), "layout B");
+  lt_check(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, tn || tt ? m : k, tn || tt ? k : m, lda), "layout B");
   lt_check(hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_16BF, n, m, ldc), "layout D");
   hipblasLtMatmulPreference_t pref;
   lt_check(hipblasLtMatmulPreferenceCreate(&pref), "preference");
@@ -171,7 +173,7 @@ Plan& get_plan(DevState& st, const Key& key, int64_t m, int64_t n, int64_t k, in
   if (exhaustive()) {
     std::vector<hipblasLtMatmulHeuristicResult_t> all;
     if (hipblaslt_ext::getAllAlgos(st.handle, hipblaslt_ext::GemmType::HIPBLASLT_GEMM,
-                                   nn || tn ? HIPBLAS_OP_N : HIPBLAS_OP_T, tn ? HIPBLAS_OP_T : HIPBLAS_OP_N,
+                                   nn || tn ? HIPBLAS_OP_N : HIPBLAS_OP_T, tn || tt ? HIPBLAS_OP_T : HIPBLAS_OP_N,
                                    HIP_R_16BF, HIP_R_16BF, HIP_R_16BF, HIP_R_16BF, HIPBLAS_COMPUTE_32F,
                                    all) == HIPBLAS_STATUS_SUCCESS) {
       const float alpha = 1.f;

@@ -93,3 +93,21 @@ def test_linear_gelu_no_grad_uses_epilogue(cuda):
     ref = F.gelu(x.float() @ w.float() + b.float(), approximate="tanh")
     assert _rel(train, ref) < 1.5e-2 and _rel(ev, ref) < 1.5e-2
     assert _rel(ev, train) < 1.5e-2
+
+
+@pytest.mark.parametrize("layout", [0, 1, 2, 3])
+def test_lt_gemm_layouts(layout, cuda):
+    """lt_gemm_layout: NT / NN / TN / TT operand layouts, with and without beta = 1."""
+    hip.require()
+    torch.manual_seed(10 + layout)
+    M, N, K = 384, 256, 512
+    A = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    B = (torch.randn(K, N, device=cuda) / 16).to(torch.bfloat16)
+    a = A.t().contiguous() if layout >= 2 else A          # stored [K, M] for TN / TT
+    b = B.t().contiguous() if layout in (0, 3) else B     # stored [N, K] for NT / TT
+    ref = A.float() @ B.float()
+    init = torch.randn(M, N, device=cuda).to(torch.bfloat16)
+    for acc in (False, True):
+        out = init.clone()
+        assert hip.ops().lt_gemm_layout(a, b, out, layout, acc)
+        assert _rel(out, ref + (init.float() if acc else 0)) < 1e-2, (layout, acc)

@@ -44,6 +44,8 @@ def main():
         if ops.lt_gemm_tn(dy, x, out, True):
             cands["lt_tn"] = lambda: ops.lt_gemm_tn(dy, x, out, True)
         cands["lt_nt_transposed"] = lambda: linear._wgrad_via_transposes(dy, x, out, True)
+        cands["lt_copy_dy_nn"] = lambda: linear._wgrad_one_copy(dy, x, out, True, "a")
+        cands["lt_copy_x_tt"] = lambda: linear._wgrad_one_copy(dy, x, out, True, "b")
         ref = (dy.float().t() @ x.float())
         chk = torch.empty_like(out)
         assert ops.lt_gemm_tn(dy, x, chk, False)
