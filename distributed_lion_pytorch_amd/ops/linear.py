@@ -558,17 +558,6 @@ def _wgrad_via_transposes(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, a
     return ok
 
 
-def _wgrad_one_copy(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool, which: str) -> bool:
-    """out (+)= a^T b with ONE operand copied token-contiguous: a^T (then
-    hipBLASLt's NN form a^T . b) or b^T (TT form a^T . (b^T)^T) -- the copy of
-    the smaller operand is cheap (Llama-3-8B gate_up: X is 1/7 of dY)."""
-    from . import hip
-
-    if which == "a":
-        return hip.ops().lt_gemm_layout(fast_transpose(a), b, out, 1, accumulate)
-    return hip.ops().lt_gemm_layout(a, fast_transpose(b), out, 3, accumulate)
-
-
 def _direct_split_pick(a: torch.Tensor, b: torch.Tensor, s: int, own: bool) -> bool:
     """A split own-TN weight gradient outside a multi-micro-batch window goes
     through _unsplit_wgrad's per-shape timing instead (the split launch is one
@@ -605,24 +594,17 @@ def _unsplit_wgrad(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumula
                 if _LT_TT:
                     cands["lt_tt"] = lambda: (_wgrad_via_transposes(a, b, scratch, False)
                                               or torch.mm(a.t(), b, out=scratch))
-                    # one token-contiguous copy (of the smaller operand's side): a^T -> NN, b^T -> TT
-                    cands["lt_ca"] = lambda: (_wgrad_one_copy(a, b, scratch, False, "a")
-                                              or torch.mm(a.t(), b, out=scratch))
-                    cands["lt_cb"] = lambda: (_wgrad_one_copy(a, b, scratch, False, "b")
-                                              or torch.mm(a.t(), b, out=scratch))
             name = _pick(key, cands)
             del scratch
         if name == "lt" and hip.ops().lt_gemm_tn(a, b, out2, accumulate):
             return
         if name == "lt_tt" and _wgrad_via_transposes(a, b, out2, accumulate):
             return
-        if name in ("lt_ca", "lt_cb") and _wgrad_one_copy(a, b, out2, accumulate, name[-1]):
-            return
         if name == "split":
             hip.ops().sum_partials_multi_([hip.ops().gemm_tn([a], [b], split).view(split, K * N)], out2.view(-1),
                                           accumulate)
             return
-        if name in ("blas", "lt", "lt_tt", "lt_ca", "lt_cb"):
+        if name in ("blas", "lt", "lt_tt"):
             if accumulate:
                 out2.addmm_(a.t(), b)
             else:

@@ -288,7 +288,7 @@ def test_gemm_autotune_candidates_agree(cuda):
     assert (d1.float() - dref).abs().max().item() <= 2e-2 * dref.abs().max().item()
 
 
-@pytest.mark.parametrize("choice", ["tn", "blas", "lt", "lt_tt", "lt_ca", "lt_cb", "split"])
+@pytest.mark.parametrize("choice", ["tn", "blas", "lt", "lt_tt", "split"])
 def test_unsplit_wgrad_choices(cuda, choice):
     """Every candidate of the timed weight gradient (own TN bf16 epilogue,
     ATen's hipBLASLt TN, hipBLASLt TN with the searched algorithm and beta = 1,

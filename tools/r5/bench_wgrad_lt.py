@@ -44,8 +44,9 @@ def main():
         if ops.lt_gemm_tn(dy, x, out, True):
             cands["lt_tn"] = lambda: ops.lt_gemm_tn(dy, x, out, True)
         cands["lt_nt_transposed"] = lambda: linear._wgrad_via_transposes(dy, x, out, True)
-        cands["lt_copy_dy_nn"] = lambda: linear._wgrad_one_copy(dy, x, out, True, "a")
-        cands["lt_copy_x_tt"] = lambda: linear._wgrad_one_copy(dy, x, out, True, "b")
+        # one-copy forms (c31, profiles/r5/wgrad_onecopy_c31.txt): never faster, not in the pick
+        cands["lt_copy_dy_nn"] = lambda: ops.lt_gemm_layout(linear.fast_transpose(dy), x, out, 1, True)
+        cands["lt_copy_x_tt"] = lambda: ops.lt_gemm_layout(dy, linear.fast_transpose(x), out, 3, True)
         ref = (dy.float().t() @ x.float())
         chk = torch.empty_like(out)
         assert ops.lt_gemm_tn(dy, x, chk, False)
