@@ -548,8 +548,9 @@ def _wgrad_via_transposes(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, a
     """out (+)= a^T b as hipBLASLt's NT form (both operands contraction-
     contiguous, its fastest layout: 1.5-1.6 PF/s at Llama-3-8B shapes against
     1.1-1.3 for the TN forms) on token-contiguous copies a^T, b^T made by the
-    LDS-tiled transpose kernel -- the copies cost ~1/8 of the GEMM at
-    gate_up / down_proj (tools/r5/bench_wgrad_lt.py)."""
+    LDS-tiled transpose kernel -- the copies cost about a fifth of the GEMM
+    at gate_up / down_proj and the sum still wins there
+    (tools/r5/bench_wgrad_lt.py, profiles/r5/wgrad_tt_c27.txt)."""
     from . import hip
 
     at, bt = fast_transpose(a), fast_transpose(b)
