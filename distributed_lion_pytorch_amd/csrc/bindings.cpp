@@ -584,6 +584,26 @@ Tensor swiglu_bwd_fused(const Tensor& dh, const Tensor& g, const Tensor& u) {
   return dgu;
 }
 
+// swiglu_bwd_fused plus the token-contiguous copy dguT [2F, rows] of its result
+// (rows % 64 == 0, F % 64 == 0)
+std::tuple<Tensor, Tensor> swiglu_bwd_fused_t(const Tensor& dh, const Tensor& g, const Tensor& u) {
+  int64_t rows, ld;
+  check_pair(g, u, rows, ld);
+  TORCH_CHECK(dh.is_contiguous() && dh.sizes() == g.sizes() && dh.scalar_type() == at::kBFloat16,
+              "dlion swiglu: dh must be contiguous bf16 of the gate's shape");
+  const int64_t F = g.size(-1);
+  TORCH_CHECK(rows % 64 == 0 && F % 64 == 0, "dlion swiglu_bwd_fused_t: rows and F must be multiples of 64");
+  const c10::DeviceGuard dg(g.device());
+  auto shape = g.sizes().vec();
+  shape.back() = 2 * F;
+  auto dgu = at::empty(shape, g.options());
+  auto dgut = at::empty({2 * F, rows}, g.options());
+  check_hip(dlion::launch_swiglu_bwd_t(dh.data_ptr(), g.data_ptr(), u.data_ptr(), dgu.data_ptr(), dgut.data_ptr(),
+                                       rows, F, ld, cur_stream()),
+            "swiglu_bwd_fused_t");
+  return {dgu, dgut};
+}
+
 // x [B, T, H, D] with unit-stride heads (stride(2) == D) and any token stride
 // (a q or k slice of a fused projection output), cos / sin [>= T, D] bf16
 // (row t = position t); y contiguous.
@@ -1140,6 +1160,7 @@ TORCH_LIBRARY(dlion, m) {
   m.def("swiglu_fwd(Tensor g, Tensor u) -> Tensor");
   m.def("swiglu_bwd(Tensor dh, Tensor g, Tensor u) -> (Tensor, Tensor)");
   m.def("swiglu_bwd_fused(Tensor dh, Tensor g, Tensor u) -> Tensor");
+  m.def("swiglu_bwd_fused_t(Tensor dh, Tensor g, Tensor u) -> (Tensor, Tensor)");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, bool inverse) -> Tensor");
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, bool inverse) -> ()");
   m.def(
@@ -1201,6 +1222,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("swiglu_bwd_fused", &swiglu_bwd_fused);
+  m.impl("swiglu_bwd_fused_t", &swiglu_bwd_fused_t);
   m.impl("rope", &rope);
   m.impl("rope_", &rope_);
   m.impl("gemm_nt", &gemm_nt);

@@ -191,6 +191,53 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restr
   }
 }
 
+// The same backward on 64-token x 64-feature tiles that also writes the
+// token-contiguous copy dguT [2F, rows] of dgu = [dg | du] (the operand the
+// gate/up weight gradient's NT form wants, ops/linear.py _wgrad_via_transposes):
+// the tile's results go out row-major as above and, staged through LDS,
+// transposed -- one extra write of dgu instead of a transpose pass that reads
+// and writes it again.  rows % 64 == 0, F % 64 == 0 (the launcher checks).
+__global__ void __launch_bounds__(256) swiglu_bwd_t_kernel(const uint16_t* __restrict__ dh,
+                                                          const uint16_t* __restrict__ g,
+                                                          const uint16_t* __restrict__ u,
+                                                          uint16_t* __restrict__ dgu, uint16_t* __restrict__ dgut,
+                                                          int64_t F, int64_t ld_in, int64_t rows) {
+  __shared__ uint16_t tg[64][66], tu[64][66];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * 64, c0 = static_cast<int64_t>(blockIdx.x) * 64;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = threadIdx.x + h * 256, tr = idx >> 3, tc = (idx & 7) * 8;
+    const int64_t row = r0 + tr, c = c0 + tc;
+    float dv[8], gv[8], uv[8], og[8], ou[8];
+    Elem<kBF16>::load8(dh + row * F + c, dv);
+    Elem<kBF16>::load8(g + row * ld_in + c, gv);
+    Elem<kBF16>::load8(u + row * ld_in + c, uv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float sg = sigmoid_f(gv[j]);
+      ou[j] = dv[j] * gv[j] * sg;
+      og[j] = dv[j] * uv[j] * sg * (1.f + gv[j] * (1.f - sg));
+      tg[tr][tc + j] = f32_to_bf16(og[j]);
+      tu[tr][tc + j] = f32_to_bf16(ou[j]);
+    }
+    Elem<kBF16>::store8(dgu + row * 2 * F + c, og);
+    Elem<kBF16>::store8(dgu + row * 2 * F + F + c, ou);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = threadIdx.x + h * 256, oc = idx >> 3, orr = (idx & 7) * 8;
+    uint32_t wg[4], wu[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      wg[j] = static_cast<uint32_t>(tg[orr + 2 * j][oc]) | (static_cast<uint32_t>(tg[orr + 2 * j + 1][oc]) << 16);
+      wu[j] = static_cast<uint32_t>(tu[orr + 2 * j][oc]) | (static_cast<uint32_t>(tu[orr + 2 * j + 1][oc]) << 16);
+    }
+    *reinterpret_cast<uint4*>(dgut + (c0 + oc) * rows + r0 + orr) = make_uint4(wg[0], wg[1], wg[2], wg[3]);
+    *reinterpret_cast<uint4*>(dgut + (F + c0 + oc) * rows + r0 + orr) = make_uint4(wu[0], wu[1], wu[2], wu[3]);
+  }
+}
+
 // 4 bf16 <-> fp32 (one 8-byte access)
 __device__ __forceinline__ void load4(const uint16_t* p, float (&o)[4]) {
   const uint2 v = *reinterpret_cast<const uint2*>(p);
@@ -488,6 +535,16 @@ hipError_t launch_swiglu_fwd(const void* g, const void* u, void* h, int64_t rows
   const int64_t n8 = rows * F / 8;
   hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(n8, 256)), dim3(256), 0, st, static_cast<const uint16_t*>(g),
                      static_cast<const uint16_t*>(u), static_cast<uint16_t*>(h), n8, F / 8, ld_in);
+  return hipGetLastError();
+}
+
+hipError_t launch_swiglu_bwd_t(const void* dh, const void* g, const void* u, void* dgu, void* dgut, int64_t rows,
+                               int64_t F, int64_t ld_in, hipStream_t st) {
+  if (rows % 64 != 0 || F % 64 != 0 || ld_in % 8 != 0 || rows / 64 > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(swiglu_bwd_t_kernel, dim3(static_cast<unsigned>(F / 64), static_cast<unsigned>(rows / 64)),
+                     dim3(256), 0, st, static_cast<const uint16_t*>(dh), static_cast<const uint16_t*>(g),
+                     static_cast<const uint16_t*>(u), static_cast<uint16_t*>(dgu), static_cast<uint16_t*>(dgut), F,
+                     ld_in, rows);
   return hipGetLastError();
 }
 

@@ -117,7 +117,15 @@ class _SwiGLU(torch.autograd.Function):
         F_ = gate.shape[-1]
         if (gate.stride(-2) == 2 * F_ and up.data_ptr() == gate.data_ptr() + F_ * gate.element_size()
                 and up.stride() == gate.stride()):
-            dgu = hip.ops().swiglu_bwd_fused(dh.contiguous(), gate, up)
+            from . import linear
+
+            rows = gate.numel() // F_
+            if rows % 64 == 0 and F_ % 64 == 0 and linear.want_transposed_copy(rows, 2 * F_):
+                # the gate/up weight gradient runs on token-contiguous copies: write dgu^T here
+                dgu, dgut = hip.ops().swiglu_bwd_fused_t(dh.contiguous(), gate, up)
+                linear.register_transposed(dgu.view(rows, 2 * F_), dgut)
+            else:
+                dgu = hip.ops().swiglu_bwd_fused(dh.contiguous(), gate, up)
             return dgu[..., :F_], dgu[..., F_:]
         dg, du = hip.ops().swiglu_bwd(dh.contiguous(), gate, up)
         return dg, du

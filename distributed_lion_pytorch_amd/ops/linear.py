@@ -141,6 +141,7 @@ def end_fusion_window(flush: bool = True) -> None:
     _ST.pending.clear()
     _clear_deferred()
     _drop_deferred()
+    _TCOPY.clear()
     _ST.fuse["nodefer"] = False
 
 
@@ -553,10 +554,42 @@ def _wgrad_via_transposes(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, a
     (tools/r5/bench_wgrad_lt.py, profiles/r5/wgrad_tt_c27.txt)."""
     from . import hip
 
-    at, bt = fast_transpose(a), fast_transpose(b)
+    at, bt = _transposed(a), _transposed(b)
     ok = hip.ops().lt_gemm_nt_acc(at, bt, out, accumulate)
     del at, bt
     return ok
+
+
+# Token-contiguous copies written by the producing kernel itself (the SwiGLU
+# backward's dgu^T: one extra write instead of a transpose pass that reads dgu
+# again), offered to the next transposed-copy weight gradient.  One entry at a
+# time; it holds the original too, so its address cannot be reused meanwhile.
+_TCOPY: dict = {}  # data_ptr -> (tensor, its transposed copy)
+_TT_A: set = set()  # (rows, cols) of a-operands whose weight gradient picked "lt_tt"
+
+
+_TT_PRODUCER = os.environ.get("DLION_TT_PRODUCER", "1") != "0"  # A/B switch for producer-written copies
+
+
+def want_transposed_copy(rows: int, cols: int) -> bool:
+    """Should a producer of a [rows, cols] weight-gradient operand also write its transpose?"""
+    return _LT_TT and _TT_PRODUCER and (int(rows), int(cols)) in _TT_A
+
+
+def register_transposed(t: torch.Tensor, tt: torch.Tensor) -> None:
+    _TCOPY.clear()
+    _TCOPY[t.data_ptr()] = (t, tt)
+
+
+def _transposed(t: torch.Tensor) -> torch.Tensor:
+    ent = _TCOPY.pop(t.data_ptr(), None)
+    if ent is not None and _same_view(ent[0], t):
+        return ent[1]
+    return fast_transpose(t)
+
+
+def _same_view(x: torch.Tensor, y: torch.Tensor) -> bool:
+    return x.data_ptr() == y.data_ptr() and x.shape == y.shape and x.stride() == y.stride()
 
 
 def _direct_split_pick(a: torch.Tensor, b: torch.Tensor, s: int, own: bool) -> bool:
@@ -596,6 +629,8 @@ def _unsplit_wgrad(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumula
                     cands["lt_tt"] = lambda: (_wgrad_via_transposes(a, b, scratch, False)
                                               or torch.mm(a.t(), b, out=scratch))
             name = _pick(key, cands)
+            if name == "lt_tt":
+                _TT_A.add((M, K))
             del scratch
         if name == "lt" and hip.ops().lt_gemm_tn(a, b, out2, accumulate):
             return

@@ -194,3 +194,48 @@ def test_rope_attention_packed_grads(H, Hkv, T, fused_bwd, cuda, monkeypatch):
     assert rel(y, yr) < 2e-2
     for got, ref in ((gq, rq), (gk, rk), (gv, rv)):
         assert rel(got, ref) < 3e-2, rel(got, ref)
+
+
+def test_swiglu_bwd_transposed_copy(cuda):
+    """swiglu_bwd_fused_t: the same dgu as swiglu_bwd_fused, plus dgu^T bit for bit."""
+    hip.require()
+    torch.manual_seed(11)
+    rows, F = 256, 192
+    gu = torch.randn(rows, 2 * F, device=cuda).to(torch.bfloat16)
+    g, u = gu[:, :F], gu[:, F:]
+    dh = torch.randn(rows, F, device=cuda).to(torch.bfloat16)
+    ref = hip.ops().swiglu_bwd_fused(dh, g, u)
+    dgu, dgut = hip.ops().swiglu_bwd_fused_t(dh, g, u)
+    assert torch.equal(dgu, ref)
+    assert torch.equal(dgut, dgu.t())
+
+
+def test_gate_up_weight_gradient_uses_the_swiglu_transposed_copy(cuda, monkeypatch):
+    """With the transposed-copy NT form picked for the gate/up weight
+    gradient, the SwiGLU backward writes dgu^T itself and the weight gradient
+    takes it instead of transposing dgu; all gradients match fp32."""
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    torch.manual_seed(12)
+    M, C, F = 4096, 2048, 1024
+    x = torch.randn(M, C, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    wg = torch.nn.Parameter((torch.randn(F, C, device=cuda) / C ** 0.5).to(torch.bfloat16))
+    wu = torch.nn.Parameter((torch.randn(F, C, device=cuda) / C ** 0.5).to(torch.bfloat16))
+    dh = torch.randn(M, F, device=cuda, dtype=torch.bfloat16)
+    monkeypatch.setattr(L, "_GEMM_PICK", {})
+    monkeypatch.setattr(L, "_TT_A", {(M, 2 * F)})
+    s, _ = L.wgrad_splits(torch.empty(M, 2 * F, device=cuda, dtype=torch.bfloat16), x.detach())
+    L._GEMM_PICK[("wgrad", M, 2 * F, C, 2 * F, C, s)] = "lt_tt"
+    shapes = []
+    orig = L.fast_transpose
+    monkeypatch.setattr(L, "fast_transpose", lambda t, *a: shapes.append(tuple(t.shape)) or orig(t, *a))
+    with L.grad_accumulation_fusion(True, micro_batches=1):
+        gate, up = L.linear_multi_nk(x, [wg, wu])
+        fused.swiglu(gate, up).backward(dh)
+    assert (M, 2 * F) not in shapes and (M, C) in shapes, shapes  # dgu^T came from the SwiGLU kernel
+    assert not L._TCOPY
+    xr, gr, ur = (t.detach().float().requires_grad_() for t in (x, wg, wu))
+    (torch.nn.functional.silu(xr @ gr.t()) * (xr @ ur.t())).backward(dh.float())
+    for got, ref in ((wg.grad, gr.grad), (wu.grad, ur.grad), (x.grad, xr.grad)):
+        assert (got.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
