@@ -218,7 +218,7 @@ def test_gate_up_weight_gradient_uses_the_swiglu_transposed_copy(cuda, monkeypat
 
     hip.require()
     torch.manual_seed(12)
-    M, C, F = 4096, 2048, 1024
+    M, C, F = 4096, 1536, 1024  # C != 2F: the two operands' shapes differ
     x = torch.randn(M, C, device=cuda, dtype=torch.bfloat16, requires_grad=True)
     wg = torch.nn.Parameter((torch.randn(F, C, device=cuda) / C ** 0.5).to(torch.bfloat16))
     wu = torch.nn.Parameter((torch.randn(F, C, device=cuda) / C ** 0.5).to(torch.bfloat16))
