@@ -584,6 +584,21 @@ Tensor swiglu_bwd_fused(const Tensor& dh, const Tensor& g, const Tensor& u) {
   return dgu;
 }
 
+// swiglu_fwd plus the token-contiguous copy hT [F, rows] (rows % 64 == 0, F % 64 == 0)
+std::tuple<Tensor, Tensor> swiglu_fwd_t(const Tensor& g, const Tensor& u) {
+  int64_t rows, ld;
+  check_pair(g, u, rows, ld);
+  const int64_t F = g.size(-1);
+  TORCH_CHECK(rows % 64 == 0 && F % 64 == 0, "dlion swiglu_fwd_t: rows and F must be multiples of 64");
+  const c10::DeviceGuard dg(g.device());
+  auto h = at::empty(g.sizes(), g.options());
+  auto ht = at::empty({F, rows}, g.options());
+  check_hip(dlion::launch_swiglu_fwd_t(g.data_ptr(), u.data_ptr(), h.data_ptr(), ht.data_ptr(), rows, F, ld,
+                                       cur_stream()),
+            "swiglu_fwd_t");
+  return {h, ht};
+}
+
 // swiglu_bwd_fused plus the token-contiguous copy dguT [2F, rows] of its result
 // (rows % 64 == 0, F % 64 == 0)
 std::tuple<Tensor, Tensor> swiglu_bwd_fused_t(const Tensor& dh, const Tensor& g, const Tensor& u) {
@@ -1161,6 +1176,7 @@ TORCH_LIBRARY(dlion, m) {
   m.def("swiglu_bwd(Tensor dh, Tensor g, Tensor u) -> (Tensor, Tensor)");
   m.def("swiglu_bwd_fused(Tensor dh, Tensor g, Tensor u) -> Tensor");
   m.def("swiglu_bwd_fused_t(Tensor dh, Tensor g, Tensor u) -> (Tensor, Tensor)");
+  m.def("swiglu_fwd_t(Tensor g, Tensor u) -> (Tensor, Tensor)");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, bool inverse) -> Tensor");
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, bool inverse) -> ()");
   m.def(
@@ -1223,6 +1239,7 @@ TORCH_LIBRARY_IMPL(dlion, CUDA, m) {
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("swiglu_bwd_fused", &swiglu_bwd_fused);
   m.impl("swiglu_bwd_fused_t", &swiglu_bwd_fused_t);
+  m.impl("swiglu_fwd_t", &swiglu_fwd_t);
   m.impl("rope", &rope);
   m.impl("rope_", &rope_);
   m.impl("gemm_nt", &gemm_nt);

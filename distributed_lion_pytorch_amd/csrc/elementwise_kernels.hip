@@ -191,6 +191,41 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restr
   }
 }
 
+// The forward on 64-token x 64-feature tiles that also writes hT [F, rows],
+// the token-contiguous copy of h the down projection's weight gradient uses
+// in its NT form (written once here instead of transposed in the backward).
+__global__ void __launch_bounds__(256) swiglu_fwd_t_kernel(const uint16_t* __restrict__ g,
+                                                          const uint16_t* __restrict__ u, uint16_t* __restrict__ h,
+                                                          uint16_t* __restrict__ ht, int64_t F, int64_t ld_in,
+                                                          int64_t rows) {
+  __shared__ uint16_t th[64][66];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * 64, c0 = static_cast<int64_t>(blockIdx.x) * 64;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = threadIdx.x + k * 256, tr = idx >> 3, tc = (idx & 7) * 8;
+    const int64_t row = r0 + tr, c = c0 + tc;
+    float gv[8], uv[8], o[8];
+    Elem<kBF16>::load8(g + row * ld_in + c, gv);
+    Elem<kBF16>::load8(u + row * ld_in + c, uv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = gv[j] * sigmoid_f(gv[j]) * uv[j];
+      th[tr][tc + j] = f32_to_bf16(o[j]);
+    }
+    Elem<kBF16>::store8(h + row * F + c, o);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = threadIdx.x + k * 256, oc = idx >> 3, orr = (idx & 7) * 8;
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = static_cast<uint32_t>(th[orr + 2 * j][oc]) | (static_cast<uint32_t>(th[orr + 2 * j + 1][oc]) << 16);
+    *reinterpret_cast<uint4*>(ht + (c0 + oc) * rows + r0 + orr) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 // The same backward on 64-token x 64-feature tiles that also writes the
 // token-contiguous copy dguT [2F, rows] of dgu = [dg | du] (the operand the
 // gate/up weight gradient's NT form wants, ops/linear.py _wgrad_via_transposes):
@@ -535,6 +570,15 @@ hipError_t launch_swiglu_fwd(const void* g, const void* u, void* h, int64_t rows
   const int64_t n8 = rows * F / 8;
   hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(n8, 256)), dim3(256), 0, st, static_cast<const uint16_t*>(g),
                      static_cast<const uint16_t*>(u), static_cast<uint16_t*>(h), n8, F / 8, ld_in);
+  return hipGetLastError();
+}
+
+hipError_t launch_swiglu_fwd_t(const void* g, const void* u, void* h, void* ht, int64_t rows, int64_t F,
+                               int64_t ld_in, hipStream_t st) {
+  if (rows % 64 != 0 || F % 64 != 0 || ld_in % 8 != 0 || rows / 64 > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(swiglu_fwd_t_kernel, dim3(static_cast<unsigned>(F / 64), static_cast<unsigned>(rows / 64)),
+                     dim3(256), 0, st, static_cast<const uint16_t*>(g), static_cast<const uint16_t*>(u),
+                     static_cast<uint16_t*>(h), static_cast<uint16_t*>(ht), F, ld_in, rows);
   return hipGetLastError();
 }
 

@@ -46,6 +46,8 @@ hipError_t launch_bias_gelu_bwd(const void* dh, const void* z, const void* b, vo
                                 int64_t rows, int N, bool exact, hipStream_t st);
 hipError_t launch_swiglu_fwd(const void* g, const void* u, void* h, int64_t rows, int64_t F, int64_t ld_in,
                              hipStream_t st);
+hipError_t launch_swiglu_fwd_t(const void* g, const void* u, void* h, void* ht, int64_t rows, int64_t F,
+                               int64_t ld_in, hipStream_t st);
 hipError_t launch_swiglu_bwd_t(const void* dh, const void* g, const void* u, void* dgu, void* dgut, int64_t rows,
                                int64_t F, int64_t ld_in, hipStream_t st);
 hipError_t launch_swiglu_bwd(const void* dh, const void* g, const void* u, void* dg, void* du, int64_t rows,

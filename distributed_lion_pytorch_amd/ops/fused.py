@@ -108,7 +108,16 @@ class _SwiGLU(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, gate, up):
+        from . import linear
+
         ctx.save_for_backward(gate, up)
+        F_ = gate.shape[-1]
+        rows = gate.numel() // F_
+        if rows % 64 == 0 and F_ % 64 == 0 and linear.want_transposed_copy(rows, F_, "b"):
+            # the down projection's weight gradient runs on token-contiguous copies: write h^T now
+            h, ht = hip.ops().swiglu_fwd_t(gate, up)
+            linear.register_transposed(h.view(rows, F_), ht)
+            return h
         return hip.ops().swiglu_fwd(gate, up)
 
     @staticmethod

@@ -560,24 +560,34 @@ def _wgrad_via_transposes(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, a
     return ok
 
 
-# Token-contiguous copies written by the producing kernel itself (the SwiGLU
-# backward's dgu^T: one extra write instead of a transpose pass that reads dgu
-# again), offered to the next transposed-copy weight gradient.  One entry at a
-# time; it holds the original too, so its address cannot be reused meanwhile.
+# Token-contiguous copies written by the producing kernels themselves (the
+# SwiGLU backward's dgu^T, the SwiGLU forward's h^T: one extra write instead of
+# a transpose pass that reads the operand again), offered to the
+# transposed-copy weight gradients.  An entry holds the original too, so its
+# address cannot be reused while the entry lives; entries die when consumed,
+# at the window's end, or past _TCOPY_MAX (oldest first).
 _TCOPY: dict = {}  # data_ptr -> (tensor, its transposed copy)
-_TT_A: set = set()  # (rows, cols) of a-operands whose weight gradient picked "lt_tt"
+_TCOPY_MAX = 160
+_TT_A: set = set()  # (rows, cols) of a-operands (dY) whose weight gradient picked "lt_tt"
+_TT_B: set = set()  # (rows, cols) of b-operands (X)
 
 
 _TT_PRODUCER = os.environ.get("DLION_TT_PRODUCER", "1") != "0"  # A/B switch for producer-written copies
 
 
-def want_transposed_copy(rows: int, cols: int) -> bool:
-    """Should a producer of a [rows, cols] weight-gradient operand also write its transpose?"""
-    return _LT_TT and _TT_PRODUCER and (int(rows), int(cols)) in _TT_A
+def want_transposed_copy(rows: int, cols: int, operand: str = "a") -> bool:
+    """Should a producer of a [rows, cols] weight-gradient operand (a = the
+    output gradient, b = the layer input) also write its transpose?  Never
+    inside an activation-checkpointed window: an input's copy would be kept
+    from the forward to the backward."""
+    if not (_LT_TT and _TT_PRODUCER) or (operand == "b" and (_ST.fuse["nodefer"] or not _ST.fuse["on"])):
+        return False
+    return (int(rows), int(cols)) in (_TT_A if operand == "a" else _TT_B)
 
 
 def register_transposed(t: torch.Tensor, tt: torch.Tensor) -> None:
-    _TCOPY.clear()
+    while len(_TCOPY) >= _TCOPY_MAX:
+        _TCOPY.pop(next(iter(_TCOPY)))
     _TCOPY[t.data_ptr()] = (t, tt)
 
 
@@ -631,6 +641,7 @@ def _unsplit_wgrad(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumula
             name = _pick(key, cands)
             if name == "lt_tt":
                 _TT_A.add((M, K))
+                _TT_B.add((M, N))
             del scratch
         if name == "lt" and hip.ops().lt_gemm_tn(a, b, out2, accumulate):
             return

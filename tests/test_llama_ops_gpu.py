@@ -239,3 +239,45 @@ def test_gate_up_weight_gradient_uses_the_swiglu_transposed_copy(cuda, monkeypat
     (torch.nn.functional.silu(xr @ gr.t()) * (xr @ ur.t())).backward(dh.float())
     for got, ref in ((wg.grad, gr.grad), (wu.grad, ur.grad), (x.grad, xr.grad)):
         assert (got.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+
+
+def test_swiglu_fwd_transposed_copy(cuda):
+    """swiglu_fwd_t: the same h as swiglu_fwd, plus h^T bit for bit."""
+    hip.require()
+    torch.manual_seed(13)
+    rows, F = 320, 128
+    gu = torch.randn(rows, 2 * F, device=cuda).to(torch.bfloat16)
+    g, u = gu[:, :F], gu[:, F:]
+    h, ht = hip.ops().swiglu_fwd_t(g, u)
+    assert torch.equal(h, hip.ops().swiglu_fwd(g, u))
+    assert torch.equal(ht, h.t())
+
+
+def test_down_proj_weight_gradient_uses_the_swiglu_forward_copy(cuda, monkeypatch):
+    """The SwiGLU forward writes h^T when the down projection's weight
+    gradient runs on token-contiguous copies; that gradient takes it."""
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    torch.manual_seed(14)
+    M, F, C = 4096, 1536, 1024  # h [M, F] feeds down_proj [C, F]
+    gu = torch.randn(M, 2 * F, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    wd = torch.nn.Parameter((torch.randn(C, F, device=cuda) / F ** 0.5).to(torch.bfloat16))
+    dy = torch.randn(M, C, device=cuda, dtype=torch.bfloat16)
+    monkeypatch.setattr(L, "_GEMM_PICK", {})
+    monkeypatch.setattr(L, "_TT_B", {(M, F)})
+    s, _ = L.wgrad_splits(dy, torch.empty(M, F, device=cuda, dtype=torch.bfloat16))
+    L._GEMM_PICK[("wgrad", M, C, F, C, F, s)] = "lt_tt"
+    shapes = []
+    orig = L.fast_transpose
+    monkeypatch.setattr(L, "fast_transpose", lambda t, *a: shapes.append(tuple(t.shape)) or orig(t, *a))
+    with L.grad_accumulation_fusion(True, micro_batches=1):
+        h = fused.swiglu(gu[:, :F], gu[:, F:])
+        assert len(L._TCOPY) == 1
+        L.linear_nk(h, wd).backward(dy)
+    assert (M, F) not in shapes and (M, C) in shapes, shapes  # h^T came from the forward kernel
+    assert not L._TCOPY
+    gr = gu.detach().float()
+    hr = torch.nn.functional.silu(gr[:, :F]) * gr[:, F:]
+    ref = dy.float().t() @ hr
+    assert (wd.grad.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
