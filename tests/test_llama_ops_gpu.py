@@ -260,7 +260,7 @@ def test_down_proj_weight_gradient_uses_the_swiglu_forward_copy(cuda, monkeypatc
 
     hip.require()
     torch.manual_seed(14)
-    M, F, C = 4096, 1536, 1024  # h [M, F] feeds down_proj [C, F]
+    M, F, C = 8192, 1536, 1024  # h [M, F] feeds down_proj [C, F]; 2 M F C >= 2^34: a timed shape
     gu = torch.randn(M, 2 * F, device=cuda, dtype=torch.bfloat16, requires_grad=True)
     wd = torch.nn.Parameter((torch.randn(C, F, device=cuda) / F ** 0.5).to(torch.bfloat16))
     dy = torch.randn(M, C, device=cuda, dtype=torch.bfloat16)
