@@ -23,14 +23,16 @@ HEADROOM = 0.6
 def activation_bytes(config, tokens: int, dtype_bytes: int = 2) -> int:
     """Upper estimate of the tensors a decoder layer keeps for its backward,
     summed over layers, for ``tokens`` tokens of one micro-batch: norm
-    outputs, q/k/v, attention output, residual, MLP up/gate/activation
-    (~6 x hidden + 3 x intermediate elements per token per layer), plus the
-    LM-head logits of the loss (fp32 worst case)."""
+    outputs, q/k/v, attention output, residual, MLP up/gate/activation and
+    the activation's token-contiguous copy the down projection's weight
+    gradient may keep (ops/linear.py want_transposed_copy) -- ~6 x hidden + 4 x
+    intermediate elements per token per layer -- plus the LM-head logits of
+    the loss (fp32 worst case)."""
     h = getattr(config, "hidden_size", None) or getattr(config, "n_embd")
     ff = getattr(config, "intermediate_size", None) or getattr(config, "n_inner", None) or 4 * h
     layers = getattr(config, "num_hidden_layers", None) or getattr(config, "n_layer")
     vocab = getattr(config, "vocab_size", 0)
-    per_layer = (6 * h + 3 * ff) * dtype_bytes
+    per_layer = (6 * h + 4 * ff) * dtype_bytes
     return tokens * (layers * per_layer + 4 * vocab)
 
 
