@@ -212,3 +212,24 @@ def test_rope_frequencies_stay_fp32_under_bf16_cast():
     hf = LlamaRotaryEmbedding(config=cfg)
     hc, hs = hf(torch.zeros(1, dtype=torch.float32), torch.arange(2048)[None])
     assert torch.equal(cos, hc[0]) and torch.equal(sin, hs[0])
+
+
+def test_registry_builds_native_families_from_local_dirs(tmp_path):
+    """A local HF config directory of each Llama-architecture family builds the
+    native class (registry.NATIVE); an unknown type falls back to the HF class."""
+    from distributed_lion_pytorch_amd.models import llama as L
+    from distributed_lion_pytorch_amd.models.registry import build_model, load_config
+
+    for name, cfg, cls in (("mistral", _small(transformers.MistralConfig, sliding_window=16), L.MistralForCausalLM),
+                           ("qwen2", _small(transformers.Qwen2Config), L.Qwen2ForCausalLM),
+                           ("llama", _small(transformers.LlamaConfig), L.LlamaForCausalLM)):
+        d = tmp_path / name
+        cfg.save_pretrained(d)
+        m = build_model(load_config(str(d)))
+        assert type(m) is cls, (name, type(m))
+    gpt_neox = transformers.GPTNeoXConfig(vocab_size=97, hidden_size=64, num_hidden_layers=1, num_attention_heads=4,
+                                          intermediate_size=128)
+    gpt_neox.save_pretrained(tmp_path / "neox")
+    assert type(build_model(load_config(str(tmp_path / "neox")))).__name__ == "GPTNeoXForCausalLM"
+    for key in ("mistral-7b", "qwen2-0.5b", "qwen2-7b"):
+        assert load_config(key).model_type == key.split("-")[0]
