@@ -29,6 +29,13 @@ def load_config(name_or_path: str, overrides: Optional[str] = None) -> Pretraine
                            f"{sorted(GPT2_SIZES) + sorted(LLAMA_SIZES)}")
     if overrides:
         cfg.update_from_string(overrides)
+        types = getattr(cfg, "layer_types", None)
+        if types is not None and len(types) != cfg.num_hidden_layers:
+            # per-layer attention types (Qwen2) are derived at construction: rebuild them for the
+            # overridden depth instead of saving a config HF's validator rejects
+            d = cfg.to_dict()
+            d.pop("layer_types")
+            cfg = type(cfg)(**d)
     return cfg
 
 

@@ -233,3 +233,13 @@ def test_registry_builds_native_families_from_local_dirs(tmp_path):
     assert type(build_model(load_config(str(tmp_path / "neox")))).__name__ == "GPTNeoXForCausalLM"
     for key in ("mistral-7b", "qwen2-0.5b", "qwen2-7b"):
         assert load_config(key).model_type == key.split("-")[0]
+
+
+def test_config_overrides_rebuild_per_layer_types(tmp_path):
+    """--config_overrides on a Qwen2 size: the derived per-layer attention
+    types follow the overridden depth (HF refuses to save a mismatch)."""
+    from distributed_lion_pytorch_amd.models.registry import load_config
+
+    cfg = load_config("qwen2-0.5b", "num_hidden_layers=3,hidden_size=64")
+    assert cfg.layer_types == ["full_attention"] * 3 and cfg.hidden_size == 64
+    cfg.save_pretrained(tmp_path)
