@@ -50,6 +50,12 @@
 #ifndef DLION_DKV_WAVES128
 #define DLION_DKV_WAVES128 1
 #endif
+// dK/dV at D = 128 without dropout: the wave's K tile in registers (32 VGPRs)
+// instead of LDS, which takes the block's LDS from 97.5 to 65.5 KiB -- two
+// blocks per CU, two waves per SIMD (the kernel fits 256 VGPRs there).
+#ifndef DLION_DKV_KREG128
+#define DLION_DKV_KREG128 1
+#endif
 // LDS ring depth of the 4-wave backward kernels' streamed tiles: tile i+NB-1
 // is staged while tile i is consumed (NB = 2: classic double buffering).
 // NB = 3 spills 34 dwords in dK/dV under the 3-wave floor (168 VGPRs) and
@@ -742,12 +748,14 @@ attn_bwd_dq_kernel(AttnArgs a) {
 // 3's software-pipelined variant measured -1 % and was removed.)
 template <int D, bool DROP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    D == 64 ? DLION_DKV_WAVES64 : DLION_DKV_WAVES128)))
+    D == 64 ? DLION_DKV_WAVES64 : (!DROP && DLION_DKV_KREG128 ? 2 : DLION_DKV_WAVES128))))
 attn_bwd_dkv_kernel(AttnArgs a) {
   constexpr int NB = DLION_ATTN_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> qs_[NB];
   __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[NB];
-  __shared__ __attribute__((aligned(16))) LdsTile<D> kvs_[2][4];  // [K | V][wave's key tile]
+  constexpr bool KREG = D == 128 && !DROP && DLION_DKV_KREG128;  // K fragments in registers (see above)
+  constexpr int KV = KREG ? 0 : 1;  // V's slot in kvs_
+  __shared__ __attribute__((aligned(16))) LdsTile<D> kvs_[KREG ? 1 : 2][4];  // [K | V][wave's key tile]
   __shared__ __attribute__((aligned(16))) float ls_[NB][6][32];  // [buf][lse | delta | hash base of key tile 0..3][row]
   const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntiles = ntiles32(a.T), nbhk = a.B * a.Hkv;
@@ -770,10 +778,19 @@ attn_bwd_dkv_kernel(AttnArgs a) {
     for (int j = 0; j < 4; ++j) {
       const int row = __builtin_amdgcn_readfirstlane((first + j) * 32);
       if (row < a.T) {  // block-uniform
-        kd.issue(a.k + b * a.k_sb + hk * a.k_sh + static_cast<int64_t>(row) * a.k_st, kvs_[0][j], a.T - row);
-        vd.issue(a.v + b * a.v_sb + hk * a.v_sh + static_cast<int64_t>(row) * a.v_st, kvs_[1][j], a.T - row);
+        if constexpr (!KREG)
+          kd.issue(a.k + b * a.k_sb + hk * a.k_sh + static_cast<int64_t>(row) * a.k_st, kvs_[0][j], a.T - row);
+        vd.issue(a.v + b * a.v_sb + hk * a.v_sh + static_cast<int64_t>(row) * a.v_st, kvs_[KV][j], a.T - row);
       }
     }
+  }
+  // KREG: row r of the wave's K tile, columns 16 ks + 8 hf .. +7 (row_frag's layout);
+  // rows past T read row T-1 (their keys are masked out of every product)
+  bf16x8 kf[KREG ? D / 16 : 1];
+  if constexpr (KREG) {
+    const __bf16* kp = a.k + b * a.k_sb + hk * a.k_sh + static_cast<int64_t>(min(key, a.T - 1)) * a.k_st + 8 * hf;
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) kf[ks] = ld8(kp + 16 * ks);
   }
   f32x16 dk[D / 32], dv[D / 32];
 #pragma unroll
@@ -850,8 +867,11 @@ attn_bwd_dkv_kernel(AttnArgs a) {
       DLION_PRIO_ON(kDkvPrio, 1);
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
-        s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), row_frag<D>(kvs_[0][w], r, ks, hf), s);   // S = Q K^T
-        dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), row_frag<D>(kvs_[1][w], r, ks, hf), dp);  // dP = dO V^T
+        if constexpr (KREG)
+          s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), kf[ks], s);                            // S = Q K^T
+        else
+          s = mfma32(row_frag<D>(qs_[buf], r, ks, hf), row_frag<D>(kvs_[0][w], r, ks, hf), s);   // S = Q K^T
+        dp = mfma32(row_frag<D>(ds_[buf], r, ks, hf), row_frag<D>(kvs_[KV][w], r, ks, hf), dp);  // dP = dO V^T
       }
       DLION_PRIO_OFF(kDkvPrio, 1);
       if (qt == ktile) {  // causal mask on the diagonal tile only (scalar branch): exp2(-inf) = 0
