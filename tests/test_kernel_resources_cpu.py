@@ -16,12 +16,14 @@ import pytest
 CSRC = Path(__file__).resolve().parent.parent / "distributed_lion_pytorch_amd" / "csrc"
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
-# (source, kernel-name regex, extra flags) -- the flags mirror _build.EXTRA_FLAGS
+# (source, kernel-name regex, extra flags) -- the flags ARE the build's (_build.EXTRA_FLAGS)
+from distributed_lion_pytorch_amd._build import EXTRA_FLAGS  # noqa: E402
+
 HOT = [
-    ("attention.hip", r"attn_(fwd|bwd_dq|bwd_dkv)_kernel", ["-mllvm", "-amdgpu-mfma-vgpr-form"]),
+    ("attention.hip", r"attn_(fwd|bwd_dq|bwd_dkv)_kernel", EXTRA_FLAGS.get("attention.hip", [])),
     # EPI 5 (erf-GELU derivative recomputed in the drain) is not on a training path
-    ("gemm.hip", r"gemm_nt_kernelILi[0-4678]E", []),
-    ("gemm_tn.hip", r"gemm_tn_kernel", []),
+    ("gemm.hip", r"gemm_nt_kernelILi[0-4678]E", EXTRA_FLAGS.get("gemm.hip", [])),
+    ("gemm_tn.hip", r"gemm_tn_kernel", EXTRA_FLAGS.get("gemm_tn.hip", [])),
 ]
 
 
