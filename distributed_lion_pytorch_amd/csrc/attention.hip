@@ -30,6 +30,8 @@
 #include "common.h"
 #include "attention.h"
 
+#include <cstdlib>
+
 // Occupancy floors (waves per SIMD), A/B-measured (profiles/r3/attn_occupancy_ab.txt):
 // dK/dV D=64 at 3 waves fits 168 VGPRs without spills and is ~4 % faster over
 // fwd+bwd; dK/dV D=128 at 2 waves (~30 dwords of spill) does not pay.  dQ D=64
@@ -746,14 +748,14 @@ attn_bwd_dq_kernel(AttnArgs a) {
 // every head in the GQA group is staged once per block (Q, dO and the 32
 // lse / delta values).  Low key groups (most query tiles) go first.  (Round
 // 3's software-pipelined variant measured -1 % and was removed.)
-template <int D, bool DROP>
+template <int D, bool DROP, bool KREG = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    D == 64 ? DLION_DKV_WAVES64 : (!DROP && DLION_DKV_KREG128 ? 2 : DLION_DKV_WAVES128))))
+    D == 64 ? DLION_DKV_WAVES64 : (KREG ? 2 : DLION_DKV_WAVES128))))
 attn_bwd_dkv_kernel(AttnArgs a) {
   constexpr int NB = DLION_ATTN_STAGES;
   __shared__ __attribute__((aligned(16))) LdsTile<D> qs_[NB];
   __shared__ __attribute__((aligned(16))) LdsTile<D> ds_[NB];
-  constexpr bool KREG = D == 128 && !DROP && DLION_DKV_KREG128;  // K fragments in registers (see above)
+  static_assert(!KREG || (D == 128 && !DROP), "K in registers: D = 128 without dropout");  // (see above)
   constexpr int KV = KREG ? 0 : 1;  // V's slot in kvs_
   __shared__ __attribute__((aligned(16))) LdsTile<D> kvs_[KREG ? 1 : 2][4];  // [K | V][wave's key tile]
   __shared__ __attribute__((aligned(16))) float ls_[NB][6][32];  // [buf][lse | delta | hash base of key tile 0..3][row]
@@ -1011,6 +1013,13 @@ hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
   return hipGetLastError();
 }
 
+// A/B switch for the D = 128 K-in-registers dK/dV variant (read per launch):
+// DLION_DKV_KREG128=0 takes the K-in-LDS kernel
+static bool dkv_kreg() {
+  const char* v = std::getenv("DLION_DKV_KREG128");
+  return DLION_DKV_KREG128 && (v == nullptr || v[0] != '0');
+}
+
 hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) {
   const dim3 bq(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T)));
   const dim3 bkv(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.Hkv, a.T)));
@@ -1021,7 +1030,10 @@ hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), bkv, dim3(256), 0, st, a);     \
   } else {                                                                              \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, false, 1>), bq, dim3(256), 0, st, a);   \
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), bkv, dim3(256), 0, st, a);    \
+    if (DD == 128 && dkv_kreg())                                                        \
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<128, false, true>), bkv, dim3(256), 0, st, a); \
+    else                                                                                \
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), bkv, dim3(256), 0, st, a);  \
   }
   if (D == 64) {
     BWD(64)
