@@ -55,6 +55,10 @@
 // dK/dV at D = 128 without dropout: the wave's K tile in registers (32 VGPRs)
 // instead of LDS, which takes the block's LDS from 97.5 to 65.5 KiB -- two
 // blocks per CU, two waves per SIMD (the kernel fits 256 VGPRs there).
+// Interleaved (tools/r5/bench_dkv_kreg.py, profiles/r5/dkv_kreg_c38.txt):
+// Llama-2-7B SFT shape (no GQA) fwd + bwd 0.309 -> 0.283 ms, SFT preset
+// +0.5-1.4 %; at Llama-3-8B's GQA shape (4 heads per K/V head) 0.777 ->
+// 0.806 ms, so the launcher takes it only when H == Hkv.
 #ifndef DLION_DKV_KREG128
 #define DLION_DKV_KREG128 1
 #endif
@@ -1030,7 +1034,7 @@ hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
     hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, true>), bkv, dim3(256), 0, st, a);     \
   } else {                                                                              \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, false, 1>), bq, dim3(256), 0, st, a);   \
-    if (DD == 128 && dkv_kreg())                                                        \
+    if (DD == 128 && a.H == a.Hkv && dkv_kreg())                                        \
       hipLaunchKernelGGL((attn_bwd_dkv_kernel<128, false, true>), bkv, dim3(256), 0, st, a); \
     else                                                                                \
       hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, false>), bkv, dim3(256), 0, st, a);  \
