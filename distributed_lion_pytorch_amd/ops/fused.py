@@ -107,13 +107,13 @@ class _SwiGLU(torch.autograd.Function):
     as one buffer, which the fused projection's backward takes without a copy."""
 
     @staticmethod
-    def forward(ctx, gate, up):
+    def forward(ctx, gate, up, want_t):
         from . import linear
 
         ctx.save_for_backward(gate, up)
         F_ = gate.shape[-1]
         rows = gate.numel() // F_
-        if rows % 64 == 0 and F_ % 64 == 0 and linear.want_transposed_copy(rows, F_, "b"):
+        if want_t and rows % 64 == 0 and F_ % 64 == 0 and linear.want_transposed_copy(rows, F_, "b"):
             # the down projection's weight gradient runs on token-contiguous copies: write h^T now
             h, ht = hip.ops().swiglu_fwd_t(gate, up)
             linear.register_transposed(h.view(rows, F_), ht)
@@ -135,9 +135,9 @@ class _SwiGLU(torch.autograd.Function):
                 linear.register_transposed(dgu.view(rows, 2 * F_), dgut)
             else:
                 dgu = hip.ops().swiglu_bwd_fused(dh.contiguous(), gate, up)
-            return dgu[..., :F_], dgu[..., F_:]
+            return dgu[..., :F_], dgu[..., F_:], None
         dg, du = hip.ops().swiglu_bwd(dh.contiguous(), gate, up)
-        return dg, du
+        return dg, du, None
 
 
 def swiglu(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
@@ -150,8 +150,11 @@ def swiglu(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
             and gate.shape[-1] % 8 == 0 and _use_hip(gate)):
         if not (_rows_ok(gate) and up.stride() == gate.stride()):
             gate, up = gate.contiguous(), up.contiguous()
+        # h^T is written only when a backward will consume it: never under
+        # no_grad (a frozen reference model's forward) or for frozen inputs
+        want_t = torch.is_grad_enabled() and (gate.requires_grad or up.requires_grad)
         with torch.autocast("cuda", enabled=False):
-            return _SwiGLU.apply(gate, up)
+            return _SwiGLU.apply(gate, up, want_t)
     return F.silu(gate) * up
 
 

@@ -114,6 +114,7 @@ def grad_accumulation_fusion(enabled: bool = True, micro_batches: int | None = N
             _ST.pending.clear()
             _clear_deferred()
             _drop_deferred()
+            _TCOPY.clear()
             _ST.fuse["nodefer"] = False
 
 
@@ -579,8 +580,13 @@ def want_transposed_copy(rows: int, cols: int, operand: str = "a") -> bool:
     """Should a producer of a [rows, cols] weight-gradient operand (a = the
     output gradient, b = the layer input) also write its transpose?  Never
     inside an activation-checkpointed window: an input's copy would be kept
-    from the forward to the backward."""
-    if not (_LT_TT and _TT_PRODUCER) or (operand == "b" and (_ST.fuse["nodefer"] or not _ST.fuse["on"])):
+    from the forward to the backward; and never in a multi-micro-batch window,
+    whose weight gradients are deferred to its exit or summed in the split-K
+    accumulators (the transposed-copy form only runs outside one: a copy
+    would only pin memory and cost a write)."""
+    if not (_LT_TT and _TT_PRODUCER) or (_ST.fuse["on"] and _ST.fuse["multi"]):
+        return False
+    if operand == "b" and (_ST.fuse["nodefer"] or not _ST.fuse["on"]):
         return False
     return (int(rows), int(cols)) in (_TT_A if operand == "a" else _TT_B)
 

@@ -319,22 +319,20 @@ class ElasticGroup:
         the deadline; then decide "fail" (first write wins)."""
         deadline = time.monotonic() + self.timeout + self.grace
         first = True
-        old = self.store.timeout
-        try:
-            while True:
-                left = deadline - time.monotonic()
-                if left <= 0 or (not first and self.dead_members()):
-                    break
-                first = False
-                # the timeout is the client's (shared with the process group's
-                # store ops): set for this get only, restored below
-                self.store.set_timeout(datetime.timedelta(seconds=min(left, DECISION_WAIT_S)))
-                try:
-                    return self.store.get(dec)
-                except RuntimeError:  # DistStoreError: not decided yet
-                    continue
-        finally:
-            self.store.set_timeout(old)
+        while True:
+            left = deadline - time.monotonic()
+            if left <= 0 or (not first and self.dead_members()):
+                break
+            first = False
+            # a per-call deadline (Store.wait): the client-wide timeout, shared
+            # with the process groups' store operations on other threads, stays
+            # as it is (ADVICE r5: set_timeout on the PrefixStore changed the
+            # root TCPStore client's)
+            try:
+                self.store.wait([dec], datetime.timedelta(seconds=min(left, DECISION_WAIT_S)))
+            except RuntimeError:  # DistStoreError: not decided yet
+                continue
+            return self.store.get(dec)
         return self.store.compare_set(dec, "", "fail")
 
     def _delete_keys(self, key: str) -> None:

@@ -14,7 +14,14 @@ Re-designed for the installed transformers 5.x:
 * ``--lion`` builds the distributed Lion over the *trainable* parameters
   (LoRA-safe, D12) unless an optimizer is passed explicitly;
 * every rank checkpoints its own momentum (``rank{r}-of-{W}-optimizer.pt``)
-  next to HF's rank-0 ``optimizer.pt`` and reloads it on resume (D20).
+  next to HF's rank-0 ``optimizer.pt`` and reloads it on resume (D20);
+* no DDP wrap at all: the reference wraps only to switch DDP off
+  (/root/reference/async_trainer.py:15), but DDP's reducer still allocates a
+  flat copy of every trainable gradient at wrap time (~16 GB of HBM per rank
+  at Llama-3-8B full-parameter) and broadcasts the model; here the model is
+  prepared without the wrap and the replicas are initialised by one coalesced
+  broadcast (engine.broadcast_parameters).  ``--lion_ddp_wrap`` restores the
+  reference's wrap.
 """
 from __future__ import annotations
 
@@ -57,6 +64,9 @@ class LionArguments:
     lion_elastic_timeout: Optional[float] = field(default=None, metadata={
         "help": "real worker dropout: collective deadline (s); survivors regroup and continue "
                 "(launch with python -m distributed_lion_pytorch_amd.launch for death notices)"})
+    lion_ddp_wrap: bool = field(default=False, metadata={
+        "help": "async trainers: let accelerate wrap the model in DDP as the reference does (its gradient "
+                "buckets are never used under no_sync; default: no wrap, replicas initialised by one broadcast)"})
 
 
 def apply_lion_args(training_args, lion_args: LionArguments):
@@ -216,8 +226,32 @@ class AsyncMixin:
                 t.register_hook(lambda g, n=n: inject("backward", n))
         return loss
 
+    def _prepare_without_ddp(self) -> None:
+        """Route accelerate's model preparation through its ``evaluation_mode``
+        (device placement, mixed-precision forward, no DDP wrap) and replace
+        DDP's constructor broadcast by ``broadcast_parameters``."""
+        if getattr(self.args, "lion_ddp_wrap", False) or getattr(self, "_dlion_noddp", False):
+            return
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return
+        acc = self.accelerator
+        orig = acc.prepare_model
+
+        def prepare_model(model, device_placement=None, evaluation_mode=False):
+            out = orig(model, device_placement=device_placement, evaluation_mode=True)
+            if not evaluation_mode and not getattr(out, "_dlion_broadcast", False):
+                from .engine import broadcast_parameters
+
+                broadcast_parameters(out)
+                out._dlion_broadcast = True
+            return out
+
+        acc.prepare_model = prepare_model
+        self._dlion_noddp = True
+
     def train(self, *a, **kw):
         _share_gpus_if_oversubscribed(self.args)
+        self._prepare_without_ddp()
         if getattr(self.args, "lion_elastic_timeout", None) is not None:
             # no forward-time buffer broadcast on DDP's (possibly stale) group;
             # buffers are deterministic and every rank builds them identically
@@ -228,7 +262,12 @@ class AsyncMixin:
         # also when a regroup left a single survivor: world_end records the shrink
         if dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or elastic is not None):
             same = replicas_identical(self.model, self._elastic())
-            self.log({"replicas_identical": float(same), "world_end": float(dist.get_world_size())})
+            rec = {"replicas_identical": float(same), "world_end": float(dist.get_world_size()),
+                   "ddp_wrapped": float(isinstance(self.model_wrapped, torch.nn.parallel.DistributedDataParallel))}
+            rec["trainable_params"] = float(sum(p.numel() for p in self.model.parameters() if p.requires_grad))
+            if self.args.device.type == "cuda":
+                rec["max_memory_allocated_mb"] = torch.cuda.max_memory_allocated(self.args.device) / 2**20
+            self.log(rec)
         return out
 
     def _phase_timer(self):

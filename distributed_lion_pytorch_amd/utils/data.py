@@ -300,6 +300,86 @@ def load_local_splits(train_file: Optional[str], validation_file: Optional[str],
     return tr, va, text_column((tr if tr is not None else va).column_names)
 
 
+# ------------------------------------------------- named SFT / DPO datasets
+# The reference reads ``load_dataset(dataset_name, data_dir=subset,
+# split=split, streaming=..., num_proc=...)`` (sft_llama2.py:99-107,
+# dpo_llama2.py:102-107).  Offline the name is a local file or a local copy of
+# the dataset repository (e.g. a mirror of lvwerra/stack-exchange-paired with
+# its data/finetune, data/rl, data/evaluation parquet shards); a hub name is
+# tried too (it resolves when the dataset sits in the HF cache).  Anything
+# else is an error: training on the synthetic corpus must be asked for
+# (``--synthetic_data``), never a silent fallback.
+class DatasetUnavailable(FileNotFoundError):
+    pass
+
+
+def load_named_rows(name: str, data_dir: Optional[str] = None, split: str = "train", streaming: bool = False,
+                    num_workers: Optional[int] = None, cache_dir: Optional[str] = None):
+    """Re-iterable dict rows of ``name``:
+
+    * a json-lines / json file: read lazily by :class:`Rows` (``data_dir``
+      does not apply to a single file);
+    * another data file (parquet, csv, txt): ``datasets`` by extension;
+    * a directory saved by ``Dataset.save_to_disk``: ``load_from_disk`` (its
+      ``split`` when it is a DatasetDict);
+    * any other directory, or a hub name: ``datasets.load_dataset(name,
+      data_dir=data_dir, split=split, streaming=streaming)`` with
+      ``num_proc=num_workers`` when not streaming, like the reference.
+
+    Raises :class:`DatasetUnavailable` when none of these resolves."""
+    if not name:
+        raise DatasetUnavailable("no dataset name given")
+    if os.path.isfile(name):
+        builder = file_builder(name)
+        if builder == "json":
+            return Rows(name)
+        import datasets
+
+        kw = {"keep_linebreaks": True} if builder == "text" else {}
+        return datasets.load_dataset(builder, data_files={"train": name}, split="train", streaming=streaming,
+                                     cache_dir=cache_dir, **kw)
+    try:
+        import datasets
+    except ImportError as e:  # pragma: no cover - datasets is installed in this image
+        raise DatasetUnavailable(f"dataset {name!r} needs the `datasets` package ({e})") from e
+    if os.path.isdir(name):
+        if os.path.isfile(os.path.join(name, "dataset_dict.json")) or \
+                os.path.isfile(os.path.join(name, "state.json")):
+            ds = datasets.load_from_disk(name)
+            if isinstance(ds, datasets.DatasetDict):
+                ds = ds[split]
+            return ds.to_iterable_dataset() if streaming else ds
+        if data_dir and not os.path.isdir(os.path.join(name, data_dir)):
+            raise DatasetUnavailable(f"dataset directory {name!r} has no {data_dir!r} subdirectory")
+    try:
+        return datasets.load_dataset(name, data_dir=data_dir, split=split, streaming=streaming,
+                                     num_proc=None if streaming else num_workers, cache_dir=cache_dir)
+    except Exception as e:  # offline hub name, empty directory, unknown split
+        raise DatasetUnavailable(
+            f"dataset {name!r} (data_dir={data_dir!r}, split={split!r}) could not be loaded: "
+            f"{type(e).__name__}: {e}. Point --dataset_name at a local file or dataset directory, "
+            "or pass --synthetic_data to train on the synthetic corpus") from e
+
+
+def stack_exchange_pairs(rows):
+    """DPO rows in trl's prompt / chosen / rejected form.  Rows of the
+    stack-exchange-paired layout are mapped like the reference
+    (dpo_llama2.py:113-118): prompt = "Question: " + question + "\\n\\nAnswer: ",
+    chosen = response_j, rejected = response_k; rows that already carry
+    prompt / chosen / rejected pass through."""
+    out = []
+    for r in rows:
+        if "prompt" in r and "chosen" in r and "rejected" in r:
+            out.append({"prompt": r["prompt"], "chosen": r["chosen"], "rejected": r["rejected"]})
+        elif "question" in r and "response_j" in r and "response_k" in r:
+            out.append({"prompt": "Question: " + r["question"] + "\n\nAnswer: ",
+                        "chosen": r["response_j"], "rejected": r["response_k"]})
+        else:
+            raise KeyError("a DPO row needs prompt/chosen/rejected or question/response_j/response_k, "
+                           f"got columns {sorted(r)}")
+    return out
+
+
 def column_texts(rows, col: str) -> List[str]:
     """A column of a Dataset / list of row dicts as a list of strings."""
     if rows is None:

@@ -18,12 +18,18 @@ Same ScriptArguments (beta, lr, schedule, LoRA, lengths, steps, ``--lion``,
   default) is actually forwarded to it (D10, D12);
 * every Lion knob of run_clm (``--lion_*``, incl. ``--lion_elastic_timeout``
   for real worker dropout and ``--ddp_backend`` for the process group).
-Offline: prompt/chosen/rejected triples are synthetic unless
-``--dataset_name`` is a local json/jsonl file with those fields.
+Data: ``--dataset_name`` (default lvwerra/stack-exchange-paired) is read like
+the reference's ``get_stack_exchange_paired`` (dpo_llama2.py:84-125): a local
+dataset directory (its ``--subset``, default data/rl, for training and
+``--eval_subset``, default data/evaluation, capped at 1000 rows like the
+reference's ``sanity_check=True`` eval load, :164), a data file, or a hub name
+in the HF cache; question/response_j/response_k rows are mapped to
+prompt/chosen/rejected, rows already in that form pass through.  A name that
+resolves to nothing is an error; ``--synthetic_data`` trains on synthetic
+triples of the same format.
 """
 from __future__ import annotations
 
-import json
 import logging
 import os
 import sys
@@ -41,7 +47,8 @@ from distributed_lion_pytorch_amd.models.registry import build_model, load_confi
 from distributed_lion_pytorch_amd.trainer.async_trainer import (LionArguments, apply_lion_args,  # noqa: E402
                                                                 build_lion, warn_unsynced)
 from distributed_lion_pytorch_amd.trainer.dpo import AsyncDPOTrainer, DPOTrainer  # noqa: E402
-from distributed_lion_pytorch_amd.utils.data import load_tokenizer, synthetic_paired  # noqa: E402
+from distributed_lion_pytorch_amd.utils.data import (DatasetUnavailable, load_named_rows,  # noqa: E402
+                                                     load_tokenizer, stack_exchange_pairs, synthetic_paired)
 from distributed_lion_pytorch_amd.utils.metrics import JsonlMetricsCallback  # noqa: E402
 
 logger = logging.getLogger(__name__)
@@ -81,7 +88,16 @@ class ScriptArguments:
     ignore_bias_buffers: Optional[bool] = field(default=False)
     lion: Optional[bool] = field(default=False, metadata={"help": "whether to use lion optimizer"})
     async_grad: Optional[bool] = field(default=False, metadata={"help": "do not sync gradients between workers"})
-    dataset_name: Optional[str] = field(default=None, metadata={"help": "local json/jsonl of prompt/chosen/rejected"})
+    dataset_name: Optional[str] = field(default="lvwerra/stack-exchange-paired", metadata={
+        "help": "local dataset directory or data file (question/response_j/response_k or prompt/chosen/rejected "
+                "rows), or a hub name in the HF cache"})
+    subset: Optional[str] = field(default="data/rl", metadata={"help": "training data_dir inside --dataset_name"})
+    eval_subset: Optional[str] = field(default="data/evaluation", metadata={
+        "help": "evaluation data_dir inside --dataset_name (a single file: its first 5 %% is held out instead)"})
+    split: Optional[str] = field(default="train")
+    num_workers: Optional[int] = field(default=None, metadata={"help": "num_proc of the dataset load"})
+    synthetic_data: Optional[bool] = field(default=False, metadata={
+        "help": "train on synthetic prompt/chosen/rejected triples instead of --dataset_name"})
     synthetic_samples: Optional[int] = field(default=10000)
     synthetic_chars: Optional[int] = field(default=None, metadata={
         "help": "pad every synthetic prompt + response to about this many characters (throughput runs)"})
@@ -97,17 +113,48 @@ class ScriptArguments:
     ddp_backend: Optional[str] = field(default=None, metadata={"help": "nccl (RCCL) | gloo; default: HF's choice"})
 
 
-def load_pairs(args):
-    if args.dataset_name and os.path.isfile(args.dataset_name):
-        with open(args.dataset_name) as f:
-            rows = [json.loads(line) for line in f] if args.dataset_name.endswith(".jsonl") else json.load(f)
-    else:
+def _length_filter(rows, max_length):
+    """dpo_llama2.py:157-161 / :165-168 (characters, like the reference)."""
+    return [r for r in rows if len(r["prompt"]) + len(r["chosen"]) <= max_length
+            and len(r["prompt"]) + len(r["rejected"]) <= max_length]
+
+
+def load_pairs(args, data_dir=None, sanity_check=None):
+    """prompt / chosen / rejected rows of ``data_dir`` (default ``--subset``)
+    in ``--dataset_name``, mapped and length-filtered like the reference
+    (dpo_llama2.py:84-125, :157-161); synthetic triples with
+    ``--synthetic_data``.  ``sanity_check`` keeps the first 1000 rows."""
+    import itertools
+
+    sanity_check = args.sanity_check if sanity_check is None else sanity_check
+    if args.synthetic_data:
         rows = synthetic_paired(args.synthetic_samples, seed=args.seed, target_chars=args.synthetic_chars)
-    if args.sanity_check:
+    else:
+        src = load_named_rows(args.dataset_name, data_dir=args.subset if data_dir is None else data_dir,
+                              split=args.split, num_workers=args.num_workers)
+        rows = itertools.islice(iter(src), 1000) if sanity_check else src
+        rows = stack_exchange_pairs(rows)
+        logger.info("DPO rows from %s (data_dir=%s): %d", args.dataset_name,
+                    args.subset if data_dir is None else data_dir, len(rows))
+    if sanity_check:
         rows = rows[:1000]
-    # length filter (dpo_llama2.py:157-168)
-    return [r for r in rows if len(r["prompt"]) + len(r["chosen"]) <= args.max_length
-            and len(r["prompt"]) + len(r["rejected"]) <= args.max_length]
+    return _length_filter(rows, args.max_length)
+
+
+def train_eval_pairs(args):
+    """(train, eval) rows: eval from ``--eval_subset`` of a dataset directory
+    (first 1000 rows, the reference's ``sanity_check=True`` eval load,
+    dpo_llama2.py:164), else the front 5 % of the training rows (a single
+    file or synthetic data has no evaluation subset)."""
+    rows = load_pairs(args)
+    name = args.dataset_name
+    if not args.synthetic_data and args.eval_subset and name and not os.path.isfile(name):
+        try:
+            return rows, load_pairs(args, data_dir=args.eval_subset, sanity_check=True)
+        except DatasetUnavailable as e:
+            logger.warning("no evaluation subset (%s); holding out the front of the training rows", e)
+    n_eval = max(1, min(len(rows) // 20, 1000))
+    return rows[n_eval:], rows[:n_eval]
 
 
 def main(argv=None):
@@ -131,9 +178,7 @@ def main(argv=None):
                          bnb_4bit_compute_dtype=getattr(torch, script_args.torch_dtype))
         quantize_model(model, qc)
         quantize_model(model_ref, qc)
-    rows = load_pairs(script_args)
-    n_eval = max(1, min(len(rows) // 20, 1000))
-    train_rows, eval_rows = rows[n_eval:], rows[:n_eval]
+    train_rows, eval_rows = train_eval_pairs(script_args)
 
     training_args = TrainingArguments(
         per_device_train_batch_size=script_args.per_device_train_batch_size,

@@ -115,23 +115,26 @@ def _cap(ds, n: Optional[int]):
 def build_datasets(data_args, train_args, tokenizer, vocab_size, block_size, cache_dir=None):
     pct = data_args.validation_split_percentage if data_args.validation_split_percentage is not None else 5
     if data_args.dataset_name and not train_args.synthetic_data:
-        try:
-            import datasets
+        import datasets
 
-            if os.path.isdir(data_args.dataset_name):
-                raw = datasets.load_from_disk(data_args.dataset_name)
-            else:
-                raw = datasets.load_dataset(data_args.dataset_name, data_args.dataset_config_name)
-            col = "text" if "text" in raw["train"].column_names else raw["train"].column_names[0]
-            if "validation" in raw:  # the dataset's own validation split
-                tr, va = list(raw["train"][col]), list(raw["validation"][col])
-            else:
-                tr, va = split_train_validation(list(raw["train"][col]), pct)
-            return (_cap(_blocks(tr, tokenizer, block_size, data_args, train_args), data_args.max_train_samples),
-                    _cap(_blocks(va, tokenizer, block_size, data_args, train_args), data_args.max_eval_samples))
-        except Exception as e:  # offline: no hub datasets
-            logger.warning("dataset %s unavailable offline (%s); falling back to synthetic data",
-                           data_args.dataset_name, e)
+        name = data_args.dataset_name
+        try:
+            if os.path.isdir(name) and (os.path.isfile(os.path.join(name, "dataset_dict.json"))
+                                        or os.path.isfile(os.path.join(name, "state.json"))):
+                raw = datasets.load_from_disk(name)  # a save_to_disk directory
+            else:  # a local dataset repository (data files) or a hub name in the HF cache
+                raw = datasets.load_dataset(name, data_args.dataset_config_name)
+        except Exception as e:  # a name that resolves to nothing is an error, never random words
+            raise FileNotFoundError(
+                f"dataset {name!r} could not be loaded ({type(e).__name__}: {e}); point --dataset_name at a local "
+                "dataset directory, use --train_file, or pass --synthetic_data") from e
+        col = "text" if "text" in raw["train"].column_names else raw["train"].column_names[0]
+        if "validation" in raw:  # the dataset's own validation split
+            tr, va = list(raw["train"][col]), list(raw["validation"][col])
+        else:
+            tr, va = split_train_validation(list(raw["train"][col]), pct)
+        return (_cap(_blocks(tr, tokenizer, block_size, data_args, train_args), data_args.max_train_samples),
+                _cap(_blocks(va, tokenizer, block_size, data_args, train_args), data_args.max_eval_samples))
     if (data_args.train_file or data_args.validation_file) and not train_args.synthetic_data:
         # by extension through datasets.load_dataset (reference run_clm.py:343-381)
         tr, va, col = load_local_splits(data_args.train_file, data_args.validation_file, data_args.keep_linebreaks,

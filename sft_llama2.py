@@ -15,8 +15,12 @@
 * packed "Question: ...\\n\\nAnswer: ..." samples, the reference's data
   semantics (take / skip + seeded shuffle buffer, or a seeded random split;
   an infinite packed training stream read lazily and sharded per rank);
-  offline: the stack-exchange-paired data is replaced by a synthetic corpus of
-  the same format unless ``--dataset_name`` points at a local json/jsonl file;
+  ``--dataset_name`` is read like the reference's ``load_dataset(name,
+  data_dir=subset, split=split, streaming=...)`` (sft_llama2.py:99-107):
+  a local dataset directory (e.g. a stack-exchange-paired mirror with
+  data/finetune parquet shards), a json/jsonl/parquet/csv file, or a hub name
+  present in the HF cache; a name that resolves to nothing is an error, and
+  ``--synthetic_data`` trains on a synthetic corpus of the same format;
 * every Lion knob of run_clm (``--lion_beta1/2``, ``--lion_vote``,
   ``--lion_tie_break``, ``--lion_wire``, ``--lion_bucket_mb``,
   ``--lion_stochastic_max_norm``, ``--lion_dropout_schedule`` and
@@ -26,7 +30,6 @@
 """
 from __future__ import annotations
 
-import json
 import logging
 import os
 import sys
@@ -46,8 +49,9 @@ from distributed_lion_pytorch_amd.trainer.async_trainer import (LionArguments, a
                                                                 build_lion, warn_unsynced)
 from distributed_lion_pytorch_amd.trainer.sft import AsyncSFTTrainer, SFTTrainer  # noqa: E402
 from distributed_lion_pytorch_amd.utils.data import (ConstantLengthDataset, PackedStream, RowSlice,  # noqa: E402
-                                                     Rows, ShuffledRows, chars_token_ratio, load_tokenizer,
-                                                     prepare_sample_text, random_split, synthetic_qa)
+                                                     Rows, ShuffledRows, chars_token_ratio, load_named_rows,
+                                                     load_tokenizer, prepare_sample_text, random_split,
+                                                     synthetic_qa)
 from distributed_lion_pytorch_amd.utils.metrics import JsonlMetricsCallback  # noqa: E402
 
 logger = logging.getLogger(__name__)
@@ -56,9 +60,9 @@ logger = logging.getLogger(__name__)
 @dataclass
 class ScriptArguments:
     model_name: Optional[str] = field(default="meta-llama/Llama-2-7b-hf", metadata={"help": "size name or local dir"})
-    dataset_name: Optional[str] = field(default="lvwerra/stack-exchange-paired",
-                                        metadata={"help": "local json/jsonl file (else synthetic, offline)"})
-    subset: Optional[str] = field(default="data/finetune")
+    dataset_name: Optional[str] = field(default="lvwerra/stack-exchange-paired", metadata={
+        "help": "local dataset directory or data file, or a hub name in the HF cache"})
+    subset: Optional[str] = field(default="data/finetune", metadata={"help": "data_dir inside --dataset_name"})
     split: Optional[str] = field(default="train")
     size_valid_set: Optional[int] = field(default=4000)
     streaming: Optional[bool] = field(default=True)
@@ -72,6 +76,8 @@ class ScriptArguments:
     use_lora: Optional[bool] = field(default=True, metadata={"help": "False: full fine-tune"})
     lion: Optional[bool] = field(default=False, metadata={"help": "whether to use lion optimizer"})
     async_grad: Optional[bool] = field(default=False, metadata={"help": "do not sync gradients between workers"})
+    synthetic_data: Optional[bool] = field(default=False, metadata={
+        "help": "train on a synthetic corpus of the stack-exchange format instead of --dataset_name"})
     synthetic_samples: Optional[int] = field(default=20000)
     model_overrides: Optional[str] = field(default=None, metadata={"help": "config overrides, e.g. num_hidden_layers=4"})
     torch_dtype: Optional[str] = field(default="bfloat16")
@@ -92,17 +98,33 @@ def build_base(script_args, seed):
     return build_model(config, model_name_or_path=script_args.model_name, torch_dtype=script_args.torch_dtype)
 
 
-def load_samples(script_args, seed) -> Rows:
-    """Row source: a local json-lines file (read lazily) or json array, else
-    the synthetic corpus of the reference's format (offline)."""
-    path = script_args.dataset_name
-    if path and os.path.isfile(path):
-        return Rows(path)
-    return Rows(synthetic_qa(script_args.synthetic_samples, seed=seed))
+def load_samples(script_args, seed):
+    """Row source (re-iterable dict rows): ``--dataset_name`` through
+    ``load_named_rows`` (data_dir = ``--subset``, ``--split``, ``--streaming``,
+    ``--num_workers``; a json-lines file is read lazily), or the synthetic
+    corpus of the reference's format with ``--synthetic_data``.  A name that
+    resolves to nothing raises (utils/data.DatasetUnavailable)."""
+    if script_args.synthetic_data:
+        logger.info("--synthetic_data: training on %d synthetic stack-exchange-format rows",
+                    script_args.synthetic_samples)
+        return Rows(synthetic_qa(script_args.synthetic_samples, seed=seed))
+    rows = load_named_rows(script_args.dataset_name, data_dir=script_args.subset, split=script_args.split,
+                           streaming=script_args.streaming, num_workers=script_args.num_workers)
+    logger.info("SFT rows from %s (data_dir=%s, split=%s, streaming=%s)", script_args.dataset_name,
+                script_args.subset, script_args.split, script_args.streaming)
+    return rows
 
 
-def _count_rows(rows: Rows) -> int:
-    return len(rows.source) if isinstance(rows.source, list) else sum(1 for _ in rows)
+def _count_rows(rows, cap: int) -> int:
+    """Rows in the source, counting at most ``cap`` (a stream is not read to its end)."""
+    import itertools
+
+    if isinstance(rows, Rows) and isinstance(rows.source, list):
+        return min(len(rows.source), cap)
+    try:
+        return min(len(rows), cap)  # a map-style datasets.Dataset
+    except TypeError:  # a stream or a lazily read file
+        return sum(1 for _ in itertools.islice(iter(rows), cap))
 
 
 def create_datasets(tokenizer, script_args, seed):
@@ -117,7 +139,8 @@ def create_datasets(tokenizer, script_args, seed):
     rows = load_samples(script_args, seed)
     if script_args.streaming:
         # a corpus smaller than size_valid_set would leave nothing to train on: keep 95 % for training
-        n_valid = min(script_args.size_valid_set, max(1, _count_rows(rows) // 20))
+        n_rows = _count_rows(rows, 20 * script_args.size_valid_set)
+        n_valid = min(script_args.size_valid_set, max(1, n_rows // 20))
         valid_rows = list(RowSlice(rows, 0, n_valid))
         train_rows = ShuffledRows(RowSlice(rows, n_valid), script_args.shuffle_buffer, seed)
     else:

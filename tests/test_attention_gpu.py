@@ -147,11 +147,13 @@ def test_flash_attention_tail_tiles(T, B, H, Hkv, D, p, cuda):
 @pytest.mark.gpu
 @pytest.mark.parametrize("T,window", [(100, 1), (100, 31), (100, 32), (100, 33), (300, 64), (1000, 200),
                                       (1000, 999), (257, 100)])
-@pytest.mark.parametrize("B,H,Hkv,p", [(1, 4, 2, 0.0), (2, 2, 1, 0.1)])
+@pytest.mark.parametrize("B,H,Hkv,p", [(1, 4, 2, 0.0), (2, 2, 1, 0.1), (1, 2, 2, 0.0)])
 def test_flash_attention_sliding_window(T, window, B, H, Hkv, p, cuda):
     """Mistral-style sliding window at head_dim 128 (key k visible to query q iff
     q - window < k <= q): skipped and boundary-masked tiles, tail tiles, GQA and
-    dropout, fwd + bwd vs the fp32 reference with the same masks."""
+    dropout, fwd + bwd vs the fp32 reference with the same masks.  H == Hkv
+    without dropout runs the K-in-registers dK/dV kernel (its window bounds,
+    ADVICE r5), the other cases the LDS one."""
     hip.require()
     D = 128
     torch.manual_seed(T + window)

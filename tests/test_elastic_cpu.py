@@ -207,7 +207,7 @@ def test_sft_and_dpo_survive_a_dropout(tmp_path, script):
                 "--seq_length", "64", "--size_valid_set", "10", "--shuffle_buffer", "50",
                 "--save_strategy", "no", "--gradient_accumulation_steps", "1"] + common
     else:
-        args = ["dpo_llama2.py", "--model_name_or_path", "llama-tiny", "--synthetic_samples", "64",
+        args = ["dpo_llama2.py", "--model_name_or_path", "llama-tiny", "--synthetic_data", "--synthetic_samples", "64",
                 "--max_length", "400", "--max_prompt_length", "200", "--gradient_accumulation_steps", "1",
                 "--eval_steps", "0", "--save_steps", "100", "--warmup_steps", "1",
                 "--checkpointing_policy", "reference", "--gradient_checkpointing", "false"] + common

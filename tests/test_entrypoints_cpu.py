@@ -88,7 +88,7 @@ def test_sft_and_dpo_entrypoints(tmp_path):
     import sft_llama2
 
     sft_out = str(tmp_path / "sft")
-    sft_llama2.main(["--model_name", "llama-tiny", "--synthetic_samples", "100", "--seq_length", "64",
+    sft_llama2.main(["--model_name", "llama-tiny", "--synthetic_data", "--synthetic_samples", "100", "--seq_length", "64",
                      "--output_dir", sft_out, "--max_steps", "2", "--per_device_train_batch_size", "2",
                      "--learning_rate", "1e-3", "--lion", "--async_grad", "--report_to", "none", "--use_cpu",
                      "--torch_dtype", "float32"])
@@ -96,7 +96,7 @@ def test_sft_and_dpo_entrypoints(tmp_path):
     merged = os.path.join(sft_out, "final_merged_checkpoint")
     assert os.path.isfile(os.path.join(merged, "model.safetensors"))
     dpo_out = str(tmp_path / "dpo")
-    tr = dpo_llama2.main(["--model_name_or_path", merged, "--synthetic_samples", "60", "--max_length", "1024",
+    tr = dpo_llama2.main(["--model_name_or_path", merged, "--synthetic_data", "--synthetic_samples", "60", "--max_length", "1024",
                           "--max_prompt_length", "256", "--output_dir", dpo_out, "--max_steps", "2",
                           "--per_device_train_batch_size", "2", "--gradient_accumulation_steps", "1", "--lion",
                           "--async_grad", "--use_cpu", "--torch_dtype", "float32", "--eval_steps", "0",
@@ -115,7 +115,7 @@ def test_sft_4bit_merge_uses_original_weights(tmp_path):
     from distributed_lion_pytorch_amd.models.quant import QuantConfig, quantize_model
 
     out = str(tmp_path / "qsft")
-    args = ["--model_name", "llama-tiny", "--synthetic_samples", "60", "--seq_length", "64", "--output_dir", out,
+    args = ["--model_name", "llama-tiny", "--synthetic_data", "--synthetic_samples", "60", "--seq_length", "64", "--output_dir", out,
             "--max_steps", "2", "--per_device_train_batch_size", "2", "--learning_rate", "1e-2", "--lion",
             "--async_grad", "--report_to", "none", "--use_cpu", "--torch_dtype", "float32", "--load_in_4bit"]
     sft_llama2.main(args)
@@ -151,7 +151,7 @@ def test_dpo_checkpointing_decision_sees_lora_and_frozen_reference(tmp_path, mon
         return False
 
     monkeypatch.setattr(memory, "should_checkpoint", spy)
-    tr = dpo_llama2.main(["--model_name_or_path", "llama-tiny", "--synthetic_samples", "60", "--max_length", "1024",
+    tr = dpo_llama2.main(["--model_name_or_path", "llama-tiny", "--synthetic_data", "--synthetic_samples", "60", "--max_length", "1024",
                           "--max_prompt_length", "256", "--output_dir", str(tmp_path / "dpo"), "--max_steps", "1",
                           "--per_device_train_batch_size", "2", "--gradient_accumulation_steps", "1", "--lion",
                           "--async_grad", "--use_cpu", "--torch_dtype", "float32", "--eval_steps", "0",
@@ -167,7 +167,7 @@ def test_dpo_reward_stats_keep_train_and_eval_apart(tmp_path):
     log's rewards/* (trl logs them separately as eval_rewards/*)."""
     import dpo_llama2
 
-    tr = dpo_llama2.main(["--model_name_or_path", "llama-tiny", "--synthetic_samples", "60", "--max_length", "512",
+    tr = dpo_llama2.main(["--model_name_or_path", "llama-tiny", "--synthetic_data", "--synthetic_samples", "60", "--max_length", "512",
                           "--max_prompt_length", "256", "--output_dir", str(tmp_path / "dpo"), "--max_steps", "2",
                           "--per_device_train_batch_size", "2", "--gradient_accumulation_steps", "1", "--lion",
                           "--async_grad", "--use_cpu", "--torch_dtype", "float32", "--eval_steps", "1",

@@ -281,3 +281,31 @@ def test_down_proj_weight_gradient_uses_the_swiglu_forward_copy(cuda, monkeypatc
     hr = torch.nn.functional.silu(gr[:, :F]) * gr[:, F:]
     ref = dy.float().t() @ hr
     assert (wd.grad.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+
+
+def test_swiglu_forward_copy_only_when_a_backward_consumes_it(cuda, monkeypatch):
+    """the SwiGLU forward writes h^T only when the down projection's
+    weight gradient will take it -- not under no_grad (a frozen DPO reference
+    model), not for frozen inputs, not inside a multi-micro-batch window
+    (deferred / accumulated weight gradients read the row-major operand), and
+    grad_accumulation_fusion's exit drops any unconsumed copy."""
+    from distributed_lion_pytorch_amd.ops import linear as L
+
+    hip.require()
+    M, F = 256, 128
+    gu = torch.randn(M, 2 * F, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    monkeypatch.setattr(L, "_TT_B", {(M, F)})
+    with L.grad_accumulation_fusion(True, micro_batches=1):
+        with torch.no_grad():
+            fused.swiglu(gu[:, :F], gu[:, F:])
+        assert not L._TCOPY
+        frozen = gu.detach()
+        fused.swiglu(frozen[:, :F], frozen[:, F:])
+        assert not L._TCOPY
+        h = fused.swiglu(gu[:, :F], gu[:, F:])  # the one case that writes it
+        assert len(L._TCOPY) == 1
+    assert not L._TCOPY  # unconsumed: dropped at the window's exit
+    with L.grad_accumulation_fusion(True, micro_batches=4):
+        fused.swiglu(gu[:, :F], gu[:, F:])
+        assert not L._TCOPY
+    del h

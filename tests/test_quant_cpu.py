@@ -137,7 +137,7 @@ def test_sft_dpo_entrypoints_load_in_4bit(tmp_path):
     import sft_llama2
 
     sft_out = str(tmp_path / "sft")
-    sft_llama2.main(["--model_name", "llama-tiny", "--synthetic_samples", "100", "--seq_length", "64",
+    sft_llama2.main(["--model_name", "llama-tiny", "--synthetic_data", "--synthetic_samples", "100", "--seq_length", "64",
                      "--output_dir", sft_out, "--max_steps", "2", "--per_device_train_batch_size", "2",
                      "--learning_rate", "1e-3", "--lion", "--async_grad", "--report_to", "none", "--use_cpu",
                      "--torch_dtype", "float32", "--load_in_4bit", "--save_strategy", "no"])
@@ -147,7 +147,7 @@ def test_sft_dpo_entrypoints_load_in_4bit(tmp_path):
 
     sd = load_file(os.path.join(merged, "model.safetensors"))
     assert "model.layers.0.self_attn.q_proj.weight" in sd and not any("qweight" in k for k in sd)
-    tr = dpo_llama2.main(["--model_name_or_path", merged, "--synthetic_samples", "60", "--max_length", "1024",
+    tr = dpo_llama2.main(["--model_name_or_path", merged, "--synthetic_data", "--synthetic_samples", "60", "--max_length", "1024",
                           "--max_prompt_length", "256", "--output_dir", str(tmp_path / "dpo"), "--max_steps", "1",
                           "--per_device_train_batch_size", "2", "--gradient_accumulation_steps", "1", "--lion",
                           "--async_grad", "--use_cpu", "--torch_dtype", "float32", "--eval_steps", "0",
