@@ -114,7 +114,7 @@ def build(verbose: bool = False, force: bool = False, defines=(), out: Path | No
 
     ``defines`` (``NAME=VALUE`` strings), ``flags_extra`` (compiler flags)
     and ``out`` build a variant of the extension (tuning macros, e.g.
-    ``DLION_DKV_WAVES128=1``) into its own object directory and shared
+    ``DLION_DKV_KREG128=0``) into its own object directory and shared
     object, loadable with ``DLION_LIB=<out>``."""
     out = Path(out) if out else LIB_PATH
     bdir = BUILD_DIR

@@ -415,11 +415,6 @@ Partials partials(const Tensor& part) {
 bool sum_partials_split(const std::vector<const float*>& ptrs, const std::vector<int64_t>& rows,
                         const std::vector<int64_t>& lds, int64_t n, void* out, bool accumulate, const float* scale,
                         const at::TensorOptions& opt) {
-  static const bool enabled = [] {
-    const char* e = std::getenv("DLION_SPLIT_PARTIALS");  // A/B switch: 0 = one-pass kernels only
-    return e == nullptr || std::string(e) != "0";
-  }();
-  if (!enabled) return false;
   int64_t total = 0;
   for (auto r : rows) total += r;
   const int Y = dlion::sum_partials_split_factor(n, total);

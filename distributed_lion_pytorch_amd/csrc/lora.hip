@@ -337,19 +337,9 @@ hipError_t launch_lora_up(const void* o, int64_t ldo, const void* u, const void*
   const int rpt = 16;
   const int64_t threads = ((rows + rpt - 1) / rpt) * (N / 8);
   const dim3 grid(static_cast<unsigned>((threads + 255) / 256)), block(256);
-  static const bool shallow = [] {  // A/B switch: DLION_LORA_UP_RB=4 restores the 4-row load batches
-    const char* e = std::getenv("DLION_LORA_UP_RB");
-    return e != nullptr && e[0] == '4';
-  }();
-  if (shallow) {
-    LORA_R_DISPATCH(r, hipLaunchKernelGGL((lora_up_kernel<R, 4>), grid, block, 0, st, static_cast<const uint16_t*>(o),
-                                          ldo, static_cast<const uint16_t*>(u), static_cast<const uint16_t*>(b),
-                                          static_cast<uint16_t*>(out), rows, N, rpt, s));
-  } else {
-    LORA_R_DISPATCH(r, hipLaunchKernelGGL((lora_up_kernel<R, 8>), grid, block, 0, st, static_cast<const uint16_t*>(o),
-                                          ldo, static_cast<const uint16_t*>(u), static_cast<const uint16_t*>(b),
-                                          static_cast<uint16_t*>(out), rows, N, rpt, s));
-  }
+  LORA_R_DISPATCH(r, hipLaunchKernelGGL((lora_up_kernel<R, 8>), grid, block, 0, st, static_cast<const uint16_t*>(o),
+                                        ldo, static_cast<const uint16_t*>(u), static_cast<const uint16_t*>(b),
+                                        static_cast<uint16_t*>(out), rows, N, rpt, s));
   return hipGetLastError();
 }
 

@@ -262,23 +262,6 @@ softmax_xent_packed_kernel(uint16_t* __restrict__ logits, const int64_t* __restr
   if (tid == 0) row_loss[row] = lab >= 0 ? (mx + __logf(sum)) - tgt : 0.f;
 }
 
-// xent variant override for A/B runs: DLION_XENT = reg | stream | p256 | p512 | p1024 (default: auto)
-static int xent_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char* s = getenv("DLION_XENT");
-    v = 0;
-    if (s) {
-      if (!strcmp(s, "reg")) v = 1;
-      else if (!strcmp(s, "stream")) v = 2;
-      else if (!strcmp(s, "p256")) v = 3;
-      else if (!strcmp(s, "p512")) v = 4;
-      else if (!strcmp(s, "p1024")) v = 5;
-    }
-  }
-  return v;
-}
-
 template <int DT, int THREADS, int CH>
 static void launch_packed(uint16_t* lp, const int64_t* labels, int64_t n, int64_t vp, int v, float* loss,
                           hipStream_t st) {
@@ -319,7 +302,6 @@ static hipError_t launch_xent_dt(void* logits, const int64_t* labels, int64_t n,
   const int64_t per = kXentThreads * 8;
   const int vpt = static_cast<int>((vp + per - 1) / per);
   S* lp = static_cast<S*>(logits);
-  if (var == 0) var = xent_variant();
   if constexpr (DT != kF32) {
     if (var == 0) var = (vp + 8191) / 8192 <= 7 ? 5 : (vp + 4095) / 4096 <= 16 ? 4 : 0;
     if (var >= 3 && launch_packed_dt<DT>(var == 3 ? 256 : var == 4 ? 512 : 1024, logits, labels, n, vp, v, loss, st))

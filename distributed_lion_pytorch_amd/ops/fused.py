@@ -13,7 +13,6 @@ implementation is chosen per call:
 from __future__ import annotations
 
 
-import os
 
 import torch
 import torch.nn.functional as F
@@ -21,7 +20,7 @@ import torch.nn.functional as F
 from . import hip
 from .linear import gemm_fwd
 
-_IMPL = {"mode": os.environ.get("DLION_FUSED_IMPL", "auto")}  # auto | torch | hip
+_IMPL = {"mode": "auto"}  # auto | torch | hip (set_impl)
 
 
 def set_impl(mode: str) -> None:
@@ -174,9 +173,7 @@ def dropout_add(y: torch.Tensor, residual: torch.Tensor, p: float) -> torch.Tens
 
 # --------------------------------------- fused residual + dropout + LN / RMSNorm
 _NORM_BWD_ROWS = 4  # rows per backward block-iteration for C <= 1024 (csrc/norm_kernels.hip RowGroup)
-_NORM_PARTS_CAP = int(os.environ.get("DLION_NORM_PARTS", "512"))
-_JOINT = os.environ.get("DLION_JOINT_DEPOSIT", "1") != "0"  # A/B switch for _deposit_joint
-_LM_OWN_DGRAD = os.environ.get("DLION_LM_OWN_DGRAD", "1") != "0"  # A/B switch for _lm_dgrad
+_NORM_PARTS_CAP = 512
 
 
 def _norm_parts(rows: int, C: int) -> int:
@@ -217,7 +214,7 @@ def _param_grads(part2d, C, fused, present):
         for i in need:
             out[i] = _sum_rows(part2d[:, i * C:(i + 1) * C])
     dep = [i for i in range(3) if present[i] and fused[i] is not None]
-    if len(dep) > 1 and _JOINT and dep == list(range(dep[0], dep[0] + len(dep))):
+    if len(dep) > 1 and dep == list(range(dep[0], dep[0] + len(dep))):
         from .linear import defer_partials
 
         params = [fused[i] for i in dep]
@@ -424,9 +421,10 @@ def linear_gelu(x2d: torch.Tensor, w_in_out: torch.Tensor, bias: torch.Tensor, e
     return bias_gelu(linear_kn(x2d, w_in_out, None), bias, exact)
 
 
-_DGELU_FUSED = os.environ.get("DLION_DGELU_GEMM", "1") != "0"  # A/B switch: fused DGELU backward GEMM
-_GELU_FUSED = os.environ.get("DLION_GELU_GEMM", "1") != "0"  # A/B switch: fused GELU forward GEMM
-_GELU_DSTORE = os.environ.get("DLION_GELU_DSTORE", "1") != "0"  # A/B switch: store gelu' instead of z
+# unfused paths kept as test references (tests/test_dgelu_gpu.py toggles these)
+_DGELU_FUSED = True  # DGELU backward in the own NT GEMM's epilogue
+_GELU_FUSED = True  # bias + GELU forward in the own NT GEMM's epilogue
+_GELU_DSTORE = True  # store gelu'(z) instead of z
 
 
 def _own_gemm_ok(a: torch.Tensor, b_nk: torch.Tensor) -> bool:
@@ -644,14 +642,13 @@ class _Embed(torch.autograd.Function):
         return None, gw, gp, None, None
 
 
-_EMBED_FUSED = os.environ.get("DLION_FUSED_EMBED", "1") != "0"  # A/B switch for _Embed
 
 
 def embed(ids: torch.Tensor, wte: torch.Tensor, wpe: torch.Tensor, p: float) -> torch.Tensor:
     """dropout(wte[ids] + wpe[arange(T)]) for ids [B, T]: one kernel each way on
     the GPU (bf16), the ATen chain elsewhere."""
     T = ids.shape[1]
-    if (_EMBED_FUSED and ids.is_cuda and wte.dtype == torch.bfloat16 and wpe.dtype == torch.bfloat16 and wte.shape[1] % 8 == 0
+    if (ids.is_cuda and wte.dtype == torch.bfloat16 and wpe.dtype == torch.bfloat16 and wte.shape[1] % 8 == 0
             and wte.is_contiguous() and wpe.is_contiguous() and T <= wpe.shape[0] and _use_hip(wte)):
         with torch.autocast("cuda", enabled=False):
             return _Embed.apply(ids.contiguous(), wte, wpe, float(p), _new_seed() if p > 0 else 0)
@@ -814,7 +811,6 @@ class _QKVAttention(torch.autograd.Function):
         return dx, dw, db, None, None, None, None, None
 
 
-_QKV_FUSED = os.environ.get("DLION_QKV_FUSED", "1") != "0"  # A/B switch for _QKVAttention
 
 
 def qkv_attention(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, n_head: int, dropout_p: float) -> torch.Tensor:
@@ -826,7 +822,7 @@ def qkv_attention(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, n_head: int
     D = w.shape[1] // (3 * n_head)
     if x.is_cuda:
         x, w, b = autocast_inputs(x, w, b)
-    if (_QKV_FUSED and b is not None and x.is_cuda and x.dtype == w.dtype == b.dtype == torch.bfloat16
+    if (b is not None and x.is_cuda and x.dtype == w.dtype == b.dtype == torch.bfloat16
             and _attn_ok(x, T, D)
             and w.is_contiguous() and b.is_contiguous()):
         with torch.autocast("cuda", enabled=False):
@@ -858,7 +854,6 @@ def causal_attention_gqa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, drop
     return y.transpose(1, 2).reshape(B, T, H * D)
 
 
-_ROPE_MERGE = os.environ.get("DLION_ROPE_MERGE", "1") != "0"  # A/B switch: one rotation launch for q | k
 
 
 def _adjacent_heads(q: torch.Tensor, k: torch.Tensor):
@@ -885,7 +880,7 @@ class _RopeAttention(torch.autograd.Function):
     def forward(ctx, q, k, v, cos, sin, p, seed, window=0):
         ops = hip.ops()
         H = q.shape[2]
-        qk = _adjacent_heads(q, k) if _ROPE_MERGE else None
+        qk = _adjacent_heads(q, k)
         if qk is not None:  # q | k adjacent column blocks of the projection output: one rotation launch
             r = ops.rope(qk, cos, sin, False)
             qr, kr = r[:, :, :H], r[:, :, H:]
@@ -912,16 +907,11 @@ class _RopeAttention(torch.autograd.Function):
             return dq, dk, dv, None, None, None, None, None
         ops.attn_bwd(qr, kr, v, out, dout.contiguous(), lse, ctx.p, ctx.seed, dq, dk, dv, None, None, None,
                      ctx.window)
-        if _ROPE_MERGE:
-            ops.rope_(buf[:, :, :H + Hkv], cos, sin, True)  # dq | dk: one in-place inverse rotation
-        else:
-            ops.rope_(dq, cos, sin, True)
-            ops.rope_(dk, cos, sin, True)
+        ops.rope_(buf[:, :, :H + Hkv], cos, sin, True)  # dq | dk: one in-place inverse rotation
         return dq, dk, dv, None, None, None, None, None
 
 
-_ROPE_ATTN = os.environ.get("DLION_ROPE_ATTN", "1") != "0"  # A/B switch for _RopeAttention
-_ROPE_BWD_FUSED = os.environ.get("DLION_ROPE_BWD_FUSED", "1") != "0"  # inverse rotation in the bwd kernels' stores
+_ROPE_BWD_FUSED = True  # inverse rotation in the bwd kernels' stores (tests compare the separate pass)
 
 
 def rope_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
@@ -934,7 +924,7 @@ def rope_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cos: torch
         from .linear import autocast_inputs
 
         q, k, v = autocast_inputs(q, k, v)
-    if (_ROPE_ATTN and _attn_ok(q, T, D, window) and cos.dtype == sin.dtype == torch.bfloat16
+    if (_attn_ok(q, T, D, window) and cos.dtype == sin.dtype == torch.bfloat16
             and k.dtype == v.dtype == torch.bfloat16 and all(_token_strided_ok(t) for t in (q, k, v))):
         with torch.autocast("cuda", enabled=False):
             out = _RopeAttention.apply(q, k, v, cos.contiguous(), sin.contiguous(), float(dropout_p), _new_seed(),
@@ -997,7 +987,7 @@ class _LoraAdd(torch.autograd.Function):
         return dout if ctx.needs_input_grad[0] else None, dx, ga, gb, None, None, None
 
 
-_LORA_FUSED = os.environ.get("DLION_LORA_FUSED", "1") != "0"  # A/B switch for _LoraAdd
+_LORA_FUSED = True  # fused LoRA kernels (tests compare the unfused chain)
 
 
 def lora_add(o: torch.Tensor, x: torch.Tensor, a: torch.Tensor, b: torch.Tensor, scaling: float,
@@ -1114,7 +1104,7 @@ def _lm_dgrad(g: torch.Tensor, weight: torch.Tensor, wp: torch.Tensor) -> torch.
     22.1k tok/s with the own kernel), so larger outputs keep it."""
     vp = wp.shape[0]
     tiles = -(-g.shape[0] // 256) * -(-wp.shape[1] // 256)
-    if (_LM_OWN_DGRAD and tiles < 256 and isinstance(weight, torch.nn.Parameter) and g.is_cuda
+    if (tiles < 256 and isinstance(weight, torch.nn.Parameter) and g.is_cuda
             and g.dtype == torch.bfloat16 and vp % 128 == 0 and vp >= 8192 and g.is_contiguous()
             and g.numel() < 2**31 and hip.available()):
         from .linear import cached_derived
@@ -1126,10 +1116,7 @@ def _lm_dgrad(g: torch.Tensor, weight: torch.Tensor, wp: torch.Tensor) -> torch.
     return g @ wp
 
 
-_LM_TN = os.environ.get("DLION_LM_TN", "1") != "0"  # A/B switch for _lm_wgrad_partials
-_LM_FWD_OWN = os.environ.get("DLION_LM_FWD_OWN", "0") == "1"  # A/B switch: LM-head logits on the own NT GEMM
-_LM_DEFER = os.environ.get("DLION_LM_DEFER", "1") != "0"  # LM-head weight gradient in the window-level TN GEMM
-_LM_LATE = os.environ.get("DLION_LM_LATE", "1") != "0"  # unsplit LM-head weight gradient in the backward (bf16)
+_LM_DEFER = True  # LM-head weight gradient in the window-level TN GEMM (tests compare per micro-batch)
 
 
 def _lm_wgrad_partials(g: torch.Tensor, h2d: torch.Tensor, v: int):
@@ -1141,7 +1128,7 @@ def _lm_wgrad_partials(g: torch.Tensor, h2d: torch.Tensor, v: int):
     ~1.3 ms + 0.15 ms of partial traffic (tools/bench_wgrad.py)."""
     from .linear import _tn_eligible, tn_split_factor
 
-    if not (_LM_TN and g.shape[1] % 8 == 0 and _tn_eligible(g, h2d) and hip.available()):
+    if not (g.shape[1] % 8 == 0 and _tn_eligible(g, h2d) and hip.available()):
         return None
     s = tn_split_factor(g.shape[0], g.shape[1], h2d.shape[1])
     part = hip.ops().gemm_tn([g], [h2d], s)  # [S, Vp, C]
@@ -1160,10 +1147,7 @@ class _LMHeadCE(torch.autograd.Function):
         v = weight.shape[0]
         need_grad = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         wp = _pad_rows(weight)
-        if _LM_FWD_OWN and h2d.is_cuda and hip.available() and h2d.dtype == torch.bfloat16 and h2d.shape[1] % 128 == 0:
-            logits = hip.ops().gemm_nt(h2d.contiguous(), wp, None)  # own NT GEMM, non-temporal C stores
-        else:
-            logits = gemm_fwd(h2d, wp)  # [N, Vp] in the compute dtype
+        logits = gemm_fwd(h2d, wp)  # [N, Vp] in the compute dtype
         if normalizer is None:
             n_valid = (labels1d != -100).sum().clamp_min(1).to(torch.float32)
         else:
@@ -1315,7 +1299,7 @@ def _lm_late_ok(weight, logits, h2d, v) -> bool:
     7.4 ms GEMM + 0.6 ms partial reduction before)."""
     from . import linear
 
-    if not (_LM_TN and _LM_LATE and logits.is_cuda and weight.dtype == torch.bfloat16 and v % 8 == 0
+    if not (logits.is_cuda and weight.dtype == torch.bfloat16 and v % 8 == 0
             and hip.available()):
         return False
     lv = logits[:, :v]
@@ -1328,7 +1312,7 @@ def _lm_defer_ok(weight, logits, h2d) -> bool:
     multi-micro-batch fusion window, a fusable bf16 weight, TN-eligible operands."""
     from . import linear
 
-    return (_LM_DEFER and _LM_TN and logits.is_cuda and linear._WDEFER_ON and linear._ST.fuse["on"]
+    return (_LM_DEFER and logits.is_cuda and linear._WDEFER_ON and linear._ST.fuse["on"]
             and linear._ST.fuse["multi"] and not linear._ST.fuse["nodefer"] and linear._fuse_target(weight)
             and logits.shape[1] % 8 == 0 and linear._tn_eligible(logits, h2d) and hip.available())
 
@@ -1428,13 +1412,8 @@ def shift_labels(labels: torch.Tensor) -> torch.Tensor:
     return out
 
 
-_SHIFT_LABELS = os.environ.get("DLION_SHIFT_LABELS", "1") != "0"  # A/B switch: shift labels, not h
-
-
 def causal_lm_loss(h: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor, normalizer=None) -> torch.Tensor:
     """Shifted next-token cross-entropy of the LM head on h [B, T, C]."""
-    if not _SHIFT_LABELS:
-        return lm_head_cross_entropy(h[:, :-1], weight, labels[:, 1:], normalizer=normalizer)
     return lm_head_cross_entropy(h, weight, shift_labels(labels), normalizer=normalizer)
 
 

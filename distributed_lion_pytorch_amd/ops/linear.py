@@ -35,8 +35,7 @@ Memory cost: the buffers hold S x (weight numel) fp32 per split-K weight (about
 2 GB at GPT-2-124M) and stay allocated between steps so that the next window
 reuses them.  They are only used when the window is known to span more than
 one micro-batch (``grad_accumulation_fusion(micro_batches=n)`` with n > 1, or
-n unknown); ``release_split_k_accumulators()`` frees them, and
-``DLION_SPLITK_ACC=0`` disables them.  A change of split factor inside a window
+n unknown); ``release_split_k_accumulators()`` frees them.  A change of split factor inside a window
 (micro-batches with different token counts) first flushes the running
 partials into ``param.grad``, then starts a fresh buffer.
 
@@ -52,8 +51,7 @@ c_fc / mlp c_proj 103 -> 80 us, c_attn 86 -> 62 us, attn c_proj 43 -> 29 us
 per micro-batch.  The kept operands cost memory (~500 MB per GPT-2 layer per
 micro-batch at 20480 tokens), capped by ``DLION_WGRAD_DEFER_GB`` (default:
 a quarter of the device memory); past the cap, or at 16 segments, a weight's
-segments are reduced early into its accumulator.  ``DLION_WGRAD_DEFER=0``
-disables the deferral.
+segments are reduced early into its accumulator.
 """
 from __future__ import annotations
 
@@ -64,8 +62,8 @@ import weakref
 
 import torch
 
-_ACC_BUDGET = (8 << 30) if os.environ.get("DLION_SPLITK_ACC", "1") != "0" else 0  # bytes of fp32 accumulators
-_WDEFER_ON = os.environ.get("DLION_WGRAD_DEFER", "1") != "0"
+_ACC_BUDGET = 8 << 30  # bytes of fp32 accumulators
+_WDEFER_ON = True  # window-level deferred weight gradients (tests compare the per-micro-batch form)
 _WDEFER_MAX_SEG = 16  # csrc/gemm_tn.hip kMaxSeg
 
 
@@ -311,11 +309,8 @@ def _acc_gemm(params, cols, a, b, s) -> bool:
 # the GPT-2 shapes against torch.bmm / baddbmm (hipBLASLt) with each side's
 # best split (tools/bench_wgrad.py, 20480 tokens): c_attn 69 vs 94 us, c_fc
 # 86 vs 110, mlp c_proj 86 vs 107, attn c_proj 40 vs 38.
-_TN_ON = os.environ.get("DLION_TN_GEMM", "1") != "0"  # A/B switch for the own TN kernel
-
-
 def _tn_eligible(a: torch.Tensor, b: torch.Tensor) -> bool:
-    return (_TN_ON and a.is_cuda and a.dtype == b.dtype == torch.bfloat16 and a.dim() == b.dim() == 2
+    return (a.is_cuda and a.dtype == b.dtype == torch.bfloat16 and a.dim() == b.dim() == 2
             and a.shape[0] == b.shape[0] and a.shape[0] % 128 == 0 and a.shape[1] % 8 == 0 and b.shape[1] % 8 == 0
             and a.stride(1) == 1 and b.stride(1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
             and a.stride(0) >= a.shape[1] and b.stride(0) >= b.shape[1]
@@ -323,8 +318,7 @@ def _tn_eligible(a: torch.Tensor, b: torch.Tensor) -> bool:
             and a.shape[0] * max(a.stride(0), b.stride(0)) < 2 ** 31)
 
 
-_TN_WAVE = int(os.environ.get("DLION_TN_WAVE", "256"))  # grid-size target of tn_split_factor
-_TN_WINDOW_SPLIT = os.environ.get("DLION_TN_WINDOW_SPLIT", "1") != "0"  # deferred splits sized for the window
+_TN_WAVE = 256  # grid-size target of tn_split_factor: one block per CU
 _TN_MIN_TILES = 16  # below: hipBLASLt (attn c_proj 768x768, 9 tiles: 43 us vs 55 us in the step)
 
 
@@ -367,7 +361,7 @@ def wgrad_splits(a: torch.Tensor, b: torch.Tensor) -> tuple:
     deferred = _WDEFER_ON and _ST.fuse["on"] and _ST.fuse["multi"] and not _ST.fuse["nodefer"]
     if ((deferred or math.ceil(R / 256) * math.ceil(C / 256) >= _TN_MIN_TILES) and _tn_eligible(a, b)
             and hip.available()):
-        if deferred and _TN_WINDOW_SPLIT:
+        if deferred:
             # the window's GEMM reduces over every micro-batch's tokens: size the
             # split for that K (GPT-2 attn c_proj, 9 tiles: 28 splits = 252 blocks
             # instead of the per-micro-batch choice of 16 = 144 blocks, 0.77 PF/s)
@@ -419,7 +413,6 @@ def _fuse_target(w) -> bool:
 # optimizer step (one launch over the concatenated stacks), i.e. 1/GA of the
 # launches.  Only small stacks are deferred (<= _DEFER_MAX_PART bytes each,
 # _DEFER_CAP in total; GPT-2 keeps ~1.7 GB across 8 micro-batches).
-_DEFER_ON = os.environ.get("DLION_DEFER_PARTIALS", "1") != "0"
 _DEFER_MAX_PART = 64 << 20
 _DEFER_CAP = 8 << 30
 _DEFER: dict = {}  # key -> [deposit fn, [part stacks]]
@@ -430,7 +423,7 @@ def defer_partials(key, part2d: torch.Tensor, fn) -> bool:
     """Keep ``part2d`` for ``fn(concatenated stacks)`` at the window's end.
     False (nothing kept) outside a multi-micro-batch window or over budget:
     the caller then deposits now."""
-    if not (_DEFER_ON and _ST.fuse["on"] and _ST.fuse["multi"]):
+    if not (_ST.fuse["on"] and _ST.fuse["multi"]):
         return False
     nb = part2d.numel() * part2d.element_size()
     if nb > _DEFER_MAX_PART or _DEFER_BYTES[0] + nb > _DEFER_CAP:
@@ -573,8 +566,6 @@ _TT_A: set = set()  # (rows, cols) of a-operands (dY) whose weight gradient pick
 _TT_B: set = set()  # (rows, cols) of b-operands (X)
 
 
-_TT_PRODUCER = os.environ.get("DLION_TT_PRODUCER", "1") != "0"  # A/B switch for producer-written copies
-
 
 def want_transposed_copy(rows: int, cols: int, operand: str = "a") -> bool:
     """Should a producer of a [rows, cols] weight-gradient operand (a = the
@@ -584,7 +575,7 @@ def want_transposed_copy(rows: int, cols: int, operand: str = "a") -> bool:
     whose weight gradients are deferred to its exit or summed in the split-K
     accumulators (the transposed-copy form only runs outside one: a copy
     would only pin memory and cost a write)."""
-    if not (_LT_TT and _TT_PRODUCER) or (_ST.fuse["on"] and _ST.fuse["multi"]):
+    if _ST.fuse["on"] and _ST.fuse["multi"]:
         return False
     if operand == "b" and (_ST.fuse["nodefer"] or not _ST.fuse["on"]):
         return False
@@ -614,7 +605,7 @@ def _direct_split_pick(a: torch.Tensor, b: torch.Tensor, s: int, own: bool) -> b
     of its candidates): hipBLASLt's TN form is faster at some shapes
     (Llama-3-8B q/k/v: 352 vs 399 us, profiles/r5/wgrad_lt_c20.txt)."""
     M, K = a.shape
-    return (_LT_TN and own and s > 1 and not (_ST.fuse["on"] and _ST.fuse["multi"]) and a.dtype == torch.bfloat16
+    return (own and s > 1 and not (_ST.fuse["on"] and _ST.fuse["multi"]) and a.dtype == torch.bfloat16
             and _tunable(a, M, b.shape[1], K))
 
 
@@ -639,11 +630,10 @@ def _unsplit_wgrad(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumula
             if split > 1:
                 cands["split"] = lambda: hip.ops().sum_partials_multi_(
                     [hip.ops().gemm_tn([a], [b], split).view(split, K * N)], scratch.view(-1), False)
-            if _LT_TN and _lt_nn_ok(a, b):  # hipBLASLt's TN form with the searched algorithm
+            if _lt_nn_ok(a, b):  # hipBLASLt's TN form with the searched algorithm
                 cands["lt"] = lambda: hip.ops().lt_gemm_tn(a, b, scratch, False) or torch.mm(a.t(), b, out=scratch)
-                if _LT_TT:
-                    cands["lt_tt"] = lambda: (_wgrad_via_transposes(a, b, scratch, False)
-                                              or torch.mm(a.t(), b, out=scratch))
+                cands["lt_tt"] = lambda: (_wgrad_via_transposes(a, b, scratch, False)
+                                          or torch.mm(a.t(), b, out=scratch))
             name = _pick(key, cands)
             if name == "lt_tt":
                 _TT_A.add((M, K))
@@ -764,7 +754,6 @@ def cached_derived(w: torch.Tensor, tag: str, fn) -> torch.Tensor:
     return out
 
 
-_FAST_T = os.environ.get("DLION_FAST_TRANSPOSE", "1") != "0"  # A/B switch
 
 
 def fast_transpose(t: torch.Tensor, rows_out: int | None = None) -> torch.Tensor:
@@ -774,7 +763,7 @@ def fast_transpose(t: torch.Tensor, rows_out: int | None = None) -> torch.Tensor
     from . import hip
 
     rp = t.shape[0] if rows_out is None else rows_out
-    if (_FAST_T and t.is_cuda and t.dim() == 2 and t.element_size() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0
+    if (t.is_cuda and t.dim() == 2 and t.element_size() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0
             and rp % 8 == 0 and t.data_ptr() % 16 == 0 and hip.available()):
         return hip.ops().transpose_pad(t, rp)
     out = t.t().contiguous()
@@ -805,8 +794,7 @@ def transposed_weight(w: torch.Tensor) -> torch.Tensor:
 _AUTOTUNE = os.environ.get("DLION_GEMM_AUTOTUNE", "1") != "0"
 _TUNE_MIN_FLOP = float(2 ** 34)
 _GEMM_PICK: dict = {}  # key -> candidate name
-_GEMM_FORCE = os.environ.get("DLION_GEMM_FORCE", "")
-_OWN_MARGIN = float(os.environ.get("DLION_GEMM_OWN_MARGIN", "0.05"))
+_OWN_MARGIN = 0.05
 
 
 def _own_nt_ok(a: torch.Tensor, b_nk: torch.Tensor) -> bool:
@@ -844,10 +832,6 @@ def _pick(key, cands: dict, rounds: int = 3, reps: int = 3) -> str:
     name = _GEMM_PICK.get(key)
     if name is not None and name in cands:
         return name
-    forced = [n for n in cands if _GEMM_FORCE and n.endswith(_GEMM_FORCE)]
-    if forced:  # A/B switch: DLION_GEMM_FORCE=own | lt | aten pins that candidate wherever it exists
-        _GEMM_PICK[key] = forced[0]
-        return forced[0]
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     live = {}
     for n, fn in cands.items():
@@ -903,10 +887,6 @@ def gemm_fwd(x2d: torch.Tensor, w: torch.Tensor, bias=None) -> torch.Tensor:
     return cands[_pick(key, cands)]()
 
 
-_LT_NN = os.environ.get("DLION_LT_NN", "1") != "0"  # A/B switch: 0 drops the hipBLASLt NN candidate
-_LT_TN = os.environ.get("DLION_LT_TN", "1") != "0"  # A/B switch: 0 drops the hipBLASLt TN weight-gradient candidate
-_LT_TT = os.environ.get("DLION_LT_TT", "1") != "0"  # A/B switch: 0 drops the transposed-copies NT candidate
-
 
 def _lt_nn(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dy @ w (w [N, K] row-major) through hipBLASLt's NN form with the tuned
@@ -942,7 +922,7 @@ def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, frozen: bool) -> torch.Tensor:
         # time the NT forms with the transpose included for a trainable weight (its W^T is
         # rebuilt once per optimizer step, i.e. at most once per micro-batch)
         timed = {"nn": lambda: dy @ w}
-        if _LT_NN and _lt_nn_ok(dy, w):
+        if _lt_nn_ok(dy, w):
             timed["lt_nn"] = lambda: _lt_nn(dy, w)
         wt_t = cached_derived(w, "t", lambda t: fast_transpose(t)) if frozen else None
         probe = _nt_candidates(dy, wt_t if frozen else fast_transpose(w), "nt_")

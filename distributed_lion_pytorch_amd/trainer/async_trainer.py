@@ -323,9 +323,9 @@ class AsyncMixin:
         # uploads are issued here back to back (pinned, non-blocking) instead of
         # one per micro-batch between the previous backward and the next forward,
         # where each copy waited on the stream with the GPU idle (~0.25 ms per
-        # micro-batch in the run_clm trace).  DLION_HF_PREFETCH=0 turns it off.
+        # micro-batch in the run_clm trace).
         batch_samples, n = super().get_batch_samples(epoch_iterator, num_batches, device)
-        if (os.environ.get("DLION_HF_PREFETCH", "1") != "0" and getattr(self.args.device, "type", None) == "cuda"):
+        if getattr(self.args.device, "type", None) == "cuda":
             for b in batch_samples:
                 if isinstance(b, dict):
                     for k, v in b.items():

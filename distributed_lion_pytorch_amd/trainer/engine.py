@@ -11,7 +11,6 @@ majority vote.
 """
 from __future__ import annotations
 
-import os
 import time
 from typing import Callable, Iterable, Optional
 
@@ -70,7 +69,7 @@ class TrainStep:
     def _fused_clip(self) -> bool:
         """Lion's fused clip covers exactly its own parameters: use it only when
         those are the parameters being trained (else the norm would differ)."""
-        if not hasattr(self.optimizer, "clip_grad_norm_") or os.environ.get("DLION_FUSED_CLIP", "1") == "0":
+        if not hasattr(self.optimizer, "clip_grad_norm_"):
             return False
         if not hasattr(self, "_fused_ok"):
             mine = {id(p) for g in self.optimizer.param_groups for p in g["params"]}
