@@ -319,6 +319,18 @@ __device__ __forceinline__ void glds16s(const __bf16* base, uint32_t boff, const
 __device__ __forceinline__ void glds4(const float* src, const void* dst) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(lds_addr(dst)));
 }
+// the same three with the destination as a 32-bit LDS byte address computed
+// once per kernel (lds_addr of the generic pointer costs a shared-aperture
+// null check -- s_mov src_shared_base, s_cmp, s_cselect -- per piece)
+__device__ __forceinline__ void glds16_a(const __bf16* src, uint32_t dst) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(dst));
+}
+__device__ __forceinline__ void glds16s_a(const __bf16* base, uint32_t boff, uint32_t dst) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(boff), "s"(base), "s"(dst));
+}
+__device__ __forceinline__ void glds4_a(const float* src, uint32_t dst) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(dst));
+}
 // vmcnt(0) through the builtin (gfx9 encoding: lgkmcnt 15, expcnt 7, vmcnt 0),
 // not asm: the waitcnt pass then knows the Q/K/V register loads issued
 // before it are complete, instead of re-waiting for them with counted vmcnt
@@ -375,6 +387,18 @@ struct DmaTile {
     } else {
       glds16(tile + min(r0, valid - 1) * st + c0, dst);
       if constexpr (PPW == 2) glds16(tile + min(r1, valid - 1) * st + c1, dst + 1024);
+    }
+  }
+  // issue() into the tile at LDS byte address `ldsb` (lds_addr of the tile,
+  // hoisted out of the loop by the caller)
+  __device__ __forceinline__ void issue_at(const __bf16* tile, uint32_t ldsb, int valid = 32) const {
+    const uint32_t dst = ldsb + static_cast<uint32_t>(lds);
+    if (valid >= 32) {  // block-uniform
+      glds16s_a(tile, boff0, dst);
+      if constexpr (PPW == 2) glds16s_a(tile, boff1, dst + 1024);
+    } else {
+      glds16_a(tile + min(r0, valid - 1) * st + c0, dst);
+      if constexpr (PPW == 2) glds16_a(tile + min(r1, valid - 1) * st + c1, dst + 1024);
     }
   }
 };
@@ -473,15 +497,28 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const uint32_t arow = drop_row(a.seed, bh, q), hoff = static_cast<uint32_t>(2 * hf) * kKeyMul;
   const uint32_t tm1 = drop_tm1(a.thresh16);
   const DmaTile<D> kd(a.k_st), vd(a.v_st);
+  const uint32_t ks_lds = lds_addr(&ks_[0][0]), vs_lds = lds_addr(&vs_[0][0]);
+  constexpr uint32_t kTileB = sizeof(LdsTile<D>);
   // tiles past `last` re-read tile `last` (valid memory); the causal mask
-  // zeroes them, since they lie beyond every query of the block
+  // zeroes them, since they lie beyond every query of the block.  stage() is
+  // called for kstart, kstart + NT, ... in order: the tile pointers advance by
+  // adds (the dQ / dK/dV kernels' strength reduction)
+  const int64_t kstep = 32 * a.k_st, vstep = 32 * a.v_st;
+  const __bf16* kn = kg + static_cast<int64_t>(sw.kstart) * kstep;
+  const __bf16* vn = vg + static_cast<int64_t>(sw.kstart) * vstep;
+  const __bf16* kl = kg + static_cast<int64_t>(last) * kstep;
+  const __bf16* vl = vg + static_cast<int64_t>(last) * vstep;
   auto stage = [&](int first, int buf) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const int row = __builtin_amdgcn_readfirstlane(min(first + j, last) * 32);
-      kd.issue(kg + static_cast<int64_t>(row) * a.k_st, ks_[buf][j], a.T - row);
-      vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[buf][j], a.T - row);
+      const bool in = NT == 1 || first + j <= last;
+      const uint32_t slot = static_cast<uint32_t>(buf * NT + j) * kTileB;
+      kd.issue_at(in ? kn + j * kstep : kl, ks_lds + slot, a.T - row);
+      vd.issue_at(in ? vn + j * vstep : vl, vs_lds + slot, a.T - row);
     }
+    kn += NT * kstep;
+    vn += NT * vstep;
   };
   stage(sw.kstart, (sw.kstart / NT) & 1);
   vm_wait0();
@@ -658,17 +695,32 @@ attn_bwd_dq_kernel(AttnArgs a) {
   const __bf16* kg = a.k + b * a.k_sb + hk * a.k_sh;
   const __bf16* vg = a.v + b * a.v_sb + hk * a.v_sh;
   const DmaTile<D> kd(a.k_st), vd(a.v_st);
+  const uint32_t ks_lds = lds_addr(&ks_[0][0]), vs_lds = lds_addr(&vs_[0][0]);
+  constexpr uint32_t kTileB = sizeof(LdsTile<D>);
+  const int ns = last / NT + 1, st0 = sw.kstart / NT;
   // super-tile st = key tiles st*NT .. st*NT+NT-1, one LDS slot each; tiles
-  // past `last` re-read tile `last` (valid memory) and are masked below
+  // past `last` re-read tile `last` (valid memory) and are masked below.
+  // stage() is called for st0, st0+1, ... in order: the K / V tile pointers
+  // run one super-tile ahead by an add, not a 64-bit row * stride product
+  const int64_t kstep = 32 * a.k_st, vstep = 32 * a.v_st;
+  const __bf16* kn = kg + static_cast<int64_t>(st0 * NT) * kstep;
+  const __bf16* vn = vg + static_cast<int64_t>(st0 * NT) * vstep;
   auto stage = [&](int st, int buf) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const int row = __builtin_amdgcn_readfirstlane(min(st * NT + j, last) * 32);
-      kd.issue(kg + static_cast<int64_t>(row) * a.k_st, ks_[buf][j], a.T - row);
-      vd.issue(vg + static_cast<int64_t>(row) * a.v_st, vs_[buf][j], a.T - row);
+      const uint32_t slot = static_cast<uint32_t>(buf * NT + j) * kTileB;
+      if (NT == 1 || st * NT + j <= last) {
+        kd.issue_at(kn + j * kstep, ks_lds + slot, a.T - row);
+        vd.issue_at(vn + j * vstep, vs_lds + slot, a.T - row);
+      } else {
+        kd.issue_at(kg + static_cast<int64_t>(row) * a.k_st, ks_lds + slot, a.T - row);
+        vd.issue_at(vg + static_cast<int64_t>(row) * a.v_st, vs_lds + slot, a.T - row);
+      }
     }
+    kn += NT * kstep;
+    vn += NT * vstep;
   };
-  const int ns = last / NT + 1, st0 = sw.kstart / NT;
   for (int j = st0; j < st0 + NB - 1 && j < ns; ++j) stage(j, j % NB);
   for (int st = st0; st < ns; ++st) {
     const int buf = st % NB;
@@ -830,16 +882,28 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   // with dropout, wave 1 writes the 32 per-row hash keys into ls_[buf][2]
   // (head in the group, query tile) of the next step to stage: advanced by
   // counters, not i / nq and i % nq (a runtime division is ~40 SALU per step)
-  int sg = 0, sq = first;
+  // The stage pointers run with the steps (block-uniform, SGPRs): the next
+  // step's Q / dO tile and lse / delta row advance by one query tile, and move
+  // to the next head of the GQA group when the tile index wraps -- adds, not
+  // the 64-bit (head, row) x stride products per step (~40 SALU).  The LDS
+  // destinations are byte addresses computed once.
+  int sq = first;
+  const int64_t qstep = 32 * a.q_st, ostep = 32 * a.o_st;
+  const __bf16* qh = a.q + b * a.q_sb + static_cast<int64_t>(hk * group) * a.q_sh + first * qstep;
+  const __bf16* oh = a.dout + b * a.o_sb + static_cast<int64_t>(hk * group) * a.o_sh + first * ostep;
+  const __bf16* qn = qh;
+  const __bf16* on = oh;
+  int bh_n = b * a.H + hk * group;  // the staged step's (batch, head) row of lse / delta
+  const float* ld_src = (lane < 32 ? a.lse : a.delta) + static_cast<int64_t>(bh_n) * a.T;
+  const uint32_t qs_lds = lds_addr(&qs_[0]), ds_lds = lds_addr(&ds_[0]), ls_lds = lds_addr(&ls_[0][0][0]);
+  constexpr uint32_t kTileB = sizeof(LdsTile<D>), kLsB = sizeof(ls_[0]);
   auto stage_next = [&](int buf) {
-    const int h = hk * group + sg, bh = b * a.H + h;
+    const int bh = bh_n;
     const int qrow = __builtin_amdgcn_readfirstlane(sq * 32);
-    qd.issue(a.q + b * a.q_sb + h * a.q_sh + static_cast<int64_t>(qrow) * a.q_st, qs_[buf], a.T - qrow);
-    dd.issue(a.dout + b * a.o_sb + h * a.o_sh + static_cast<int64_t>(qrow) * a.o_st, ds_[buf], a.T - qrow);
+    qd.issue_at(qn, qs_lds + buf * kTileB, a.T - qrow);
+    dd.issue_at(on, ds_lds + buf * kTileB, a.T - qrow);
     if (w == 0) {
-      const float* src = (lane < 32 ? a.lse : a.delta) + static_cast<int64_t>(bh) * a.T +
-                         min(qrow + (lane & 31), a.T - 1);
-      glds4(src, &ls_[buf][0][0]);
+      glds4_a(ld_src + min(qrow + (lane & 31), a.T - 1), ls_lds + buf * kLsB);
     } else if (DROP && w == 1) {
       // the hash bases of the 32 rows for the block's 4 key tiles (lane: row
       // lane & 31, tiles 2 (lane >> 5) + {0, 1}); rows 4i..4i+3 stored as
@@ -855,7 +919,15 @@ attn_bwd_dkv_kernel(AttnArgs a) {
     }
     if (++sq > qhi) {
       sq = first;
-      ++sg;
+      ++bh_n;
+      qh += a.q_sh;
+      oh += a.o_sh;
+      qn = qh;
+      on = oh;
+      ld_src += a.T;
+    } else {
+      qn += qstep;
+      on += ostep;
     }
   };
   for (int j = 0; j < NB - 1 && j < total; ++j) stage_next(j);
@@ -1017,12 +1089,8 @@ hipError_t launch_attn_fwd(const AttnArgs& a, int D, bool drop, hipStream_t st) 
   return hipGetLastError();
 }
 
-// A/B switch for the D = 128 K-in-registers dK/dV variant (read per launch):
-// DLION_DKV_KREG128=0 takes the K-in-LDS kernel
-static bool dkv_kreg() {
-  const char* v = std::getenv("DLION_DKV_KREG128");
-  return DLION_DKV_KREG128 && (v == nullptr || v[0] != '0');
-}
+// the D = 128 K-in-registers dK/dV variant (build macro DLION_DKV_KREG128=0 takes the K-in-LDS kernel)
+static constexpr bool dkv_kreg() { return DLION_DKV_KREG128 != 0; }
 
 hipError_t launch_attn_bwd(const AttnArgs& a, int D, bool drop, hipStream_t st) {
   const dim3 bq(static_cast<unsigned>(tile_blocks(static_cast<int64_t>(a.B) * a.H, a.T)));
