@@ -13,7 +13,7 @@ Rows (random uniform [-1, 1) bf16 operands, guide §5.4 rule 25):
     copies would enable; copy cost NOT included);
   * the same at one micro-batch (K = 20480).
 
-  python tools/gemm_anchor.py [--quick]
+  python tools/gemm_anchor.py [--quick | --square]
 """
 import statistics
 import sys
@@ -86,7 +86,7 @@ def wgrad_rows(T):
         s = linear.tn_split_factor(T, R, Cc, max_split=min(32, T // 128))
         cands = {
             f"own TN ({s} splits, partials)": lambda dy=dy, x=x, s=s: ops.gemm_tn([dy], [x], s),
-            "own TN -> bf16 (sum incl.)": lambda dy=dy, x=x, out=out: ops.gemm_tn_([dy], [x], out, False),
+            "own TN unsplit -> bf16": lambda dy=dy, x=x, out=out: ops.gemm_tn_([dy], [x], out, False),
             "hipblaslt TN": lambda dy=dy, x=x, out=out: ops.lt_gemm_tn(dy, x, out, False),
             "hipblaslt NT on copies": lambda dyt=dyt, xt=xt, out=out: ops.lt_gemm_nt_acc(dyt, xt, out, False),
         }
@@ -104,6 +104,8 @@ def main():
     sq = square_rows()
     anchor = max(sq[(8192, 8192, 8192)].values())
     print(f"# ANCHOR (best at 8192^3) = {anchor:.3f} PF/s", flush=True)
+    if "--square" in sys.argv:
+        return
     for T in ((20480,) if quick else (163840, 20480)):
         wgrad_rows(T)
 
