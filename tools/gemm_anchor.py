@@ -13,7 +13,7 @@ Rows (random uniform [-1, 1) bf16 operands, guide §5.4 rule 25):
     copies would enable; copy cost NOT included);
   * the same at one micro-batch (K = 20480).
 
-  python tools/gemm_anchor.py [--quick | --square]
+  python tools/gemm_anchor.py [--quick | --square | --tn]
 """
 import statistics
 import sys
@@ -96,6 +96,23 @@ def wgrad_rows(T):
     return rows
 
 
+def tn_rows():
+    """The weight-gradient (TN) layout at the anchor size and at the GPT-2 LM
+    head's window shape: own TN kernel (split partials, as the step runs it)
+    vs hipBLASLt's TN form with the searched algorithm."""
+    ops = hip.ops()
+    for role, T, R, Cc in (("TN 8192^3", 8192, 8192, 8192), ("LM head wgrad (window)", 163840, 50304, 768),
+                           ("LM head wgrad (1 micro-batch)", 20480, 50304, 768)):
+        dy, x = rand(T, R), rand(T, Cc)
+        out = torch.empty(R, Cc, dtype=torch.bfloat16, device="cuda")
+        s = linear.tn_split_factor(T, R, Cc, max_split=min(32, T // 128))
+        cands = {f"own TN ({s} splits, partials)": lambda dy=dy, x=x, s=s: ops.gemm_tn([dy], [x], s),
+                 "hipblaslt TN": lambda dy=dy, x=x, out=out: ops.lt_gemm_tn(dy, x, out, False)}
+        run_row(role, T, R, Cc, cands, rounds=3, reps=2)
+        del dy, x, out
+        torch.cuda.empty_cache()
+
+
 def main():
     hip.require()
     quick = "--quick" in sys.argv
@@ -105,6 +122,9 @@ def main():
     anchor = max(sq[(8192, 8192, 8192)].values())
     print(f"# ANCHOR (best at 8192^3) = {anchor:.3f} PF/s", flush=True)
     if "--square" in sys.argv:
+        return
+    if "--tn" in sys.argv:
+        tn_rows()
         return
     for T in ((20480,) if quick else (163840, 20480)):
         wgrad_rows(T)
