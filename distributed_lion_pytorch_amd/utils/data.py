@@ -361,6 +361,31 @@ def load_named_rows(name: str, data_dir: Optional[str] = None, split: str = "tra
             "or pass --synthetic_data to train on the synthetic corpus") from e
 
 
+def _pair_length_ok(r, max_length: int) -> bool:
+    return (len(r["prompt"]) + len(r["chosen"]) <= max_length
+            and len(r["prompt"]) + len(r["rejected"]) <= max_length)
+
+
+def stack_exchange_pairs_dataset(ds, max_length: int, num_proc: Optional[int] = None):
+    """:func:`stack_exchange_pairs` + the reference's length filter for a
+    ``datasets.Dataset``, as its batched ``map`` / ``filter`` (dpo_llama2.py:
+    120-125, :158-161): the rows stay in Arrow (memory-mapped) instead of a
+    Python list -- the stack-exchange-paired rl split has millions of rows."""
+    cols = list(ds.column_names)
+    if {"prompt", "chosen", "rejected"} <= set(cols):
+        out = ds.select_columns(["prompt", "chosen", "rejected"])
+    elif {"question", "response_j", "response_k"} <= set(cols):
+        def to_pairs(b):
+            return {"prompt": ["Question: " + q + "\n\nAnswer: " for q in b["question"]],
+                    "chosen": b["response_j"], "rejected": b["response_k"]}
+
+        out = ds.map(to_pairs, batched=True, num_proc=num_proc, remove_columns=cols)
+    else:
+        raise KeyError("a DPO row needs prompt/chosen/rejected or question/response_j/response_k, "
+                       f"got columns {sorted(cols)}")
+    return out.filter(lambda r: _pair_length_ok(r, max_length), num_proc=num_proc)
+
+
 def stack_exchange_pairs(rows):
     """DPO rows in trl's prompt / chosen / rejected form.  Rows of the
     stack-exchange-paired layout are mapped like the reference

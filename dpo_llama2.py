@@ -47,8 +47,9 @@ from distributed_lion_pytorch_amd.models.registry import build_model, load_confi
 from distributed_lion_pytorch_amd.trainer.async_trainer import (LionArguments, apply_lion_args,  # noqa: E402
                                                                 build_lion, warn_unsynced)
 from distributed_lion_pytorch_amd.trainer.dpo import AsyncDPOTrainer, DPOTrainer  # noqa: E402
-from distributed_lion_pytorch_amd.utils.data import (DatasetUnavailable, load_named_rows,  # noqa: E402
-                                                     load_tokenizer, stack_exchange_pairs, synthetic_paired)
+from distributed_lion_pytorch_amd.utils.data import (DatasetUnavailable, _pair_length_ok,  # noqa: E402
+                                                     load_named_rows, load_tokenizer, stack_exchange_pairs,
+                                                     stack_exchange_pairs_dataset, synthetic_paired)
 from distributed_lion_pytorch_amd.utils.metrics import JsonlMetricsCallback  # noqa: E402
 
 logger = logging.getLogger(__name__)
@@ -115,30 +116,38 @@ class ScriptArguments:
 
 def _length_filter(rows, max_length):
     """dpo_llama2.py:157-161 / :165-168 (characters, like the reference)."""
-    return [r for r in rows if len(r["prompt"]) + len(r["chosen"]) <= max_length
-            and len(r["prompt"]) + len(r["rejected"]) <= max_length]
+    return [r for r in rows if _pair_length_ok(r, max_length)]
+
+
+def _is_dataset(rows) -> bool:
+    return hasattr(rows, "select") and hasattr(rows, "map") and hasattr(rows, "__len__")
 
 
 def load_pairs(args, data_dir=None, sanity_check=None):
     """prompt / chosen / rejected rows of ``data_dir`` (default ``--subset``)
     in ``--dataset_name``, mapped and length-filtered like the reference
-    (dpo_llama2.py:84-125, :157-161); synthetic triples with
-    ``--synthetic_data``.  ``sanity_check`` keeps the first 1000 rows."""
+    (dpo_llama2.py:84-125, :157-161): a ``datasets.Dataset`` stays one (batched
+    map + filter, ``--num_workers`` processes), a lazily read json-lines file
+    becomes a list; synthetic triples with ``--synthetic_data``.
+    ``sanity_check`` keeps the first 1000 rows (before the length filter, as
+    the reference's ``select(range(1000))``)."""
     import itertools
 
     sanity_check = args.sanity_check if sanity_check is None else sanity_check
+    ddir = args.subset if data_dir is None else data_dir
     if args.synthetic_data:
         rows = synthetic_paired(args.synthetic_samples, seed=args.seed, target_chars=args.synthetic_chars)
+        return _length_filter(rows[:1000] if sanity_check else rows, args.max_length)
+    src = load_named_rows(args.dataset_name, data_dir=ddir, split=args.split, num_workers=args.num_workers)
+    if _is_dataset(src):
+        if sanity_check:
+            src = src.select(range(min(len(src), 1000)))
+        rows = stack_exchange_pairs_dataset(src, args.max_length, num_proc=args.num_workers)
     else:
-        src = load_named_rows(args.dataset_name, data_dir=args.subset if data_dir is None else data_dir,
-                              split=args.split, num_workers=args.num_workers)
-        rows = itertools.islice(iter(src), 1000) if sanity_check else src
-        rows = stack_exchange_pairs(rows)
-        logger.info("DPO rows from %s (data_dir=%s): %d", args.dataset_name,
-                    args.subset if data_dir is None else data_dir, len(rows))
-    if sanity_check:
-        rows = rows[:1000]
-    return _length_filter(rows, args.max_length)
+        rows = _length_filter(stack_exchange_pairs(itertools.islice(iter(src), 1000) if sanity_check else src),
+                              args.max_length)
+    logger.info("DPO rows from %s (data_dir=%s): %d", args.dataset_name, ddir, len(rows))
+    return rows
 
 
 def train_eval_pairs(args):
@@ -154,6 +163,8 @@ def train_eval_pairs(args):
         except DatasetUnavailable as e:
             logger.warning("no evaluation subset (%s); holding out the front of the training rows", e)
     n_eval = max(1, min(len(rows) // 20, 1000))
+    if _is_dataset(rows):
+        return rows.select(range(n_eval, len(rows))), rows.select(range(n_eval))
     return rows[n_eval:], rows[:n_eval]
 
 

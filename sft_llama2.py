@@ -144,7 +144,11 @@ def create_datasets(tokenizer, script_args, seed):
         valid_rows = list(RowSlice(rows, 0, n_valid))
         train_rows = ShuffledRows(RowSlice(rows, n_valid), script_args.shuffle_buffer, seed)
     else:
-        train_rows, valid_rows = random_split(rows, 0.005, seed)
+        if hasattr(rows, "train_test_split"):  # a datasets.Dataset: split in Arrow, seeded (sft_llama2.py:114)
+            split = rows.train_test_split(test_size=0.005, seed=seed)
+            train_rows, valid_rows = split["train"], split["test"]
+        else:
+            train_rows, valid_rows = random_split(rows, 0.005, seed)
         logger.info(f"Size of the train set: {len(train_rows)}. Size of the validation set: {len(valid_rows)}")
     ratio = chars_token_ratio(train_rows, tokenizer)
     logger.info(f"The character to token ratio of the dataset is: {ratio:.2f}")
