@@ -882,28 +882,20 @@ attn_bwd_dkv_kernel(AttnArgs a) {
   // with dropout, wave 1 writes the 32 per-row hash keys into ls_[buf][2]
   // (head in the group, query tile) of the next step to stage: advanced by
   // counters, not i / nq and i % nq (a runtime division is ~40 SALU per step)
-  // The stage pointers run with the steps (block-uniform, SGPRs): the next
-  // step's Q / dO tile and lse / delta row advance by one query tile, and move
-  // to the next head of the GQA group when the tile index wraps -- adds, not
-  // the 64-bit (head, row) x stride products per step (~40 SALU).  The LDS
-  // destinations are byte addresses computed once.
-  int sq = first;
-  const int64_t qstep = 32 * a.q_st, ostep = 32 * a.o_st;
-  const __bf16* qh = a.q + b * a.q_sb + static_cast<int64_t>(hk * group) * a.q_sh + first * qstep;
-  const __bf16* oh = a.dout + b * a.o_sb + static_cast<int64_t>(hk * group) * a.o_sh + first * ostep;
-  const __bf16* qn = qh;
-  const __bf16* on = oh;
-  int bh_n = b * a.H + hk * group;  // the staged step's (batch, head) row of lse / delta
-  const float* ld_src = (lane < 32 ? a.lse : a.delta) + static_cast<int64_t>(bh_n) * a.T;
-  const uint32_t qs_lds = lds_addr(&qs_[0]), ds_lds = lds_addr(&ds_[0]), ls_lds = lds_addr(&ls_[0][0][0]);
-  constexpr uint32_t kTileB = sizeof(LdsTile<D>), kLsB = sizeof(ls_[0]);
+  // (The forward and dQ kernels advance running stage pointers; here the
+  // per-step (head, row) address products stay: running pointers, row steps
+  // and LDS byte addresses pushed the D = 128 variants, already at ~100 of
+  // their ~106 SGPRs, into SGPR spills.)
+  int sg = 0, sq = first;
   auto stage_next = [&](int buf) {
-    const int bh = bh_n;
+    const int h = hk * group + sg, bh = b * a.H + h;
     const int qrow = __builtin_amdgcn_readfirstlane(sq * 32);
-    qd.issue_at(qn, qs_lds + buf * kTileB, a.T - qrow);
-    dd.issue_at(on, ds_lds + buf * kTileB, a.T - qrow);
+    qd.issue(a.q + b * a.q_sb + h * a.q_sh + static_cast<int64_t>(qrow) * a.q_st, qs_[buf], a.T - qrow);
+    dd.issue(a.dout + b * a.o_sb + h * a.o_sh + static_cast<int64_t>(qrow) * a.o_st, ds_[buf], a.T - qrow);
     if (w == 0) {
-      glds4_a(ld_src + min(qrow + (lane & 31), a.T - 1), ls_lds + buf * kLsB);
+      const float* src = (lane < 32 ? a.lse : a.delta) + static_cast<int64_t>(bh) * a.T +
+                         min(qrow + (lane & 31), a.T - 1);
+      glds4(src, &ls_[buf][0][0]);
     } else if (DROP && w == 1) {
       // the hash bases of the 32 rows for the block's 4 key tiles (lane: row
       // lane & 31, tiles 2 (lane >> 5) + {0, 1}); rows 4i..4i+3 stored as
@@ -919,15 +911,7 @@ attn_bwd_dkv_kernel(AttnArgs a) {
     }
     if (++sq > qhi) {
       sq = first;
-      ++bh_n;
-      qh += a.q_sh;
-      oh += a.o_sh;
-      qn = qh;
-      on = oh;
-      ld_src += a.T;
-    } else {
-      qn += qstep;
-      on += ostep;
+      ++sg;
     }
   };
   for (int j = 0; j < NB - 1 && j < total; ++j) stage_next(j);
