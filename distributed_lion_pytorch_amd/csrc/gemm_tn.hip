@@ -257,8 +257,13 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // wave-group stagger (gemm.hip)
 
+  // Branch-free body: the last pair also stages (its "next" pointers still
+  // point at the current pair -- valid memory, buffers past their last read,
+  // the same restage order as every other pair), so the wait counts never
+  // change and hipcc emits one straight-line block instead of ~15 blocks of
+  // scalar branches on a runtime `more` (SALU per pair 116 -> 90); the extra
+  // 64 KiB of DMA per block is drained before the epilogue.
   for (int it = 0; it < nit; ++it) {
-    const bool more = it + 1 < nit;
     // P1
     read_b(0);
     read_a(0, 0);
@@ -271,41 +276,31 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
     DLION_TN_PHASE_MATH(1)
     // P3
     read_a(0, 2);
-    if (more) stage(1, 0, 0, nQ);
+    stage(1, 0, 0, nQ);
     DLION_TN_PHASE_MATH(2)
     // P4
     read_a(0, 3);
-    if (more) {
-      stage(1, 1, 0, nQ);
-      tn_wait6();  // T(kt+1).{B0,B1,A0}
-    } else {
-      tn_wait2();
-    }
+    stage(1, 1, 0, nQ);
+    tn_wait6();  // T(kt+1).{B0,B1,A0}
     DLION_TN_PHASE_MATH(3)
     // P5
     read_b(1);
     read_a(1, 0);
-    if (more) stage(0, 0, 0, nP);
+    stage(0, 0, 0, nP);
     DLION_TN_PHASE_MATH(0)
     // P6
     read_a(1, 1);
-    if (more) {
-      stage(0, 1, 0, nP);
-      tn_wait8();  // T(kt+1).A1
-    } else {
-      tn_wait0();
-    }
+    stage(0, 1, 0, nP);
+    tn_wait8();  // T(kt+1).A1
     DLION_TN_PHASE_MATH(1)
     // P7
     read_a(1, 2);
-    if (more) stage(1, 0, 1, nQ + kstepQ);
+    stage(1, 0, 1, nQ + kstepQ);
     DLION_TN_PHASE_MATH(2)
     // P8
     read_a(1, 3);
-    if (more) {
-      stage(1, 1, 1, nQ + kstepQ);
-      tn_wait6();  // T(kt+2).{B0,B1,A0}
-    }
+    stage(1, 1, 1, nQ + kstepQ);
+    tn_wait6();  // T(kt+2).{B0,B1,A0}
     DLION_TN_PHASE_MATH(3)
     cP = nP;
     cQ = nQ;
@@ -313,6 +308,7 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
   }
 #undef DLION_TN_PHASE_MATH
 #undef DLION_TN_MFMA
+  tn_wait0();  // the last pair's (unused) stages have landed: no DMA outlives the block
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the wave groups
 
   // ---- epilogue: acc[mt][nt][j] = C[wr*128 + 16mt + (lane&15)][wc*64 + 16nt + 4(lane>>4) + j]
