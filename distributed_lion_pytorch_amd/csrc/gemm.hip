@@ -79,7 +79,10 @@ __device__ __forceinline__ void vm_wait8() { asm volatile("s_waitcnt vmcnt(8)" :
 __device__ __forceinline__ void vm_wait2() { asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
 __device__ __forceinline__ void vm_wait0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-__device__ __forceinline__ void glds16(const uint16_t* src, uint8_t* dst) {
+// scalar operand base + 32-bit lane byte offset: the saddr form of the load
+// (no per-load 64-bit address add); dst is wave-uniform (m0)
+__device__ __forceinline__ void glds16(const uint16_t* base, uint32_t boff, uint8_t* dst) {
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(base) + boff;
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
@@ -116,7 +119,7 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
 // base, k = 0) of the 2 pieces this wave fills in each of the 4 half-tiles
 // {A0, A1, B0, B1}.  Piece q of a half-tile = LDS rows 8q..8q+7 (1 KiB).
 struct Stage {
-  int off[2][2][2];  // [ab][half][piece]
+  uint32_t off[2][2][2];  // [ab][half][piece], bytes
 };
 
 // Diagnostic stamps (STAMP builds only, tools/gemm_stamps.py): s_memtime at
@@ -142,7 +145,8 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
 
   const int tid = threadIdx.x;
-  const int w = tid >> 6, lane = tid & 63;
+  // wave index as a scalar: the LDS-DMA destinations (m0) need no readfirstlane
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int wr = w >> 2, wc = w & 3;
 
   // ---- XCD-aware tile order (bijective for any grid size)
@@ -175,10 +179,10 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
       for (int h = 0; h < 2; ++h) {
         // A half h: LDS row lr -> tile row (lr/64)*128 + 64h + lr%64
         const int ra = min(m0 + (lr >> 6) * 128 + 64 * h + (lr & 63), g.M - 1);
-        st.off[0][h][pi] = ra * g.lda + c * 8;
+        st.off[0][h][pi] = static_cast<uint32_t>(ra * g.lda + c * 8) * 2u;
         // B half h: LDS row lr -> tile col 128h + lr
         const int rb = min(n0 + 128 * h + lr, g.N - 1);
-        st.off[1][h][pi] = rb * g.ldb + c * 8;
+        st.off[1][h][pi] = static_cast<uint32_t>(rb * g.ldb + c * 8) * 2u;
       }
     }
   }
@@ -187,9 +191,13 @@ __global__ void __launch_bounds__(512, 1) gemm_nt_kernel(const GemmArgs g) {
 
   auto stage = [&](int ab, int half, int dbuf, int kt) {
     const uint16_t* base = (ab == 0 ? Ag : Bg) + kt * kBK;
+    asm volatile("" : "+s"(base));  // a scalar base, not re-associated into the lane offsets
     uint8_t* dst = lds + slot(dbuf, ab, half) + (2 * w) * 1024;
-    glds16(base + st.off[ab][half][0], dst);
-    glds16(base + st.off[ab][half][1], dst + 1024);
+    // opaque in-place "update": the offsets stay 32-bit lane registers next to
+    // the loads (hoisted, they became 64-bit pairs and a v_lshl_add_u64 per load)
+    asm volatile("" : "+v"(st.off[ab][half][0]), "+v"(st.off[ab][half][1]));
+    glds16(base, st.off[ab][half][0], dst);
+    glds16(base, st.off[ab][half][1], dst + 1024);
   };
 
   // ---- fragment read offsets (bytes within a half-tile)

@@ -66,7 +66,10 @@ __device__ __forceinline__ void tn_wait8() { asm volatile("s_waitcnt vmcnt(8)" :
 __device__ __forceinline__ void tn_wait2() { asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
 __device__ __forceinline__ void tn_wait0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-__device__ __forceinline__ void tn_glds16(const uint16_t* src, uint8_t* dst) {
+// scalar operand base + 32-bit lane byte offset: the saddr form of the load
+// (no per-load 64-bit address add); dst is wave-uniform (m0)
+__device__ __forceinline__ void tn_glds16(const uint16_t* base, uint32_t boff, uint8_t* dst) {
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(base) + boff;
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
@@ -81,15 +84,21 @@ __device__ __forceinline__ tn_f32x4 tn_mfma(const tn_bf16x8& a, const tn_bf16x8&
 // "s_waitcnt vmcnt(0)" in front of every read phase, draining the staging
 // pipeline (the kernel ran at 58 % of the NT kernel's per-CU rate).  The asm
 // reads are covered by the explicit lgkmcnt(0) each phase issues before its
-// MFMAs (DLION_TN_PHASE_MATH); the results are consumed only there.
+// MFMAs (DLION_TN_PHASE_MATH); the results are consumed only there.  The
+// constant part of the address (the second read's 4 rows, the second k-step's
+// 32 rows) rides in the instruction's offset field: as a register operand
+// hipcc materialised it with a v_add / v_or per read (57 VALU per pair).
+template <int OFF>
 __device__ __forceinline__ tn_v4i16 tn_tr_read(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field is 16 bits");
   tn_v4i16 r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF) : "memory");
   return r;
 }
+template <int OFF>
 __device__ __forceinline__ tn_bf16x8 tn_frag(uint32_t addr) {
-  const tn_v4i16 lo = tn_tr_read(addr);
-  const tn_v4i16 hi = tn_tr_read(addr + 4 * 256);
+  const tn_v4i16 lo = tn_tr_read<OFF>(addr);
+  const tn_v4i16 hi = tn_tr_read<OFF + 4 * 256>(addr);
   // a concatenation, not a copy: lets the register allocator place both reads
   // in the fragment's 4 VGPRs
   return __builtin_bit_cast(tn_bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
@@ -99,7 +108,8 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kTLds];
 
   const int tid = threadIdx.x;
-  const int w = tid >> 6, lane = tid & 63;
+  // wave index as a scalar: the LDS-DMA destinations (m0) need no readfirstlane
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int wr = w >> 2, wc = w & 3;
 
   // ---- XCD-aware order over (split, tile); tiles grouped 8 M-tiles deep
@@ -128,7 +138,7 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
   // LDS row lr = 4q + lane/16 of half-tile piece q, physical chunk pc = lane%16,
   // logical chunk c = pc ^ swz(lr).  Columns past the edge are clamped (loaded,
   // never stored).
-  int off[2][2][2];  // [ab][half][piece]
+  uint32_t off[2][2][2];  // [ab][half][piece], bytes
   {
     const int pc = lane & 15;
 #pragma unroll
@@ -141,10 +151,10 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
       for (int h = 0; h < 2; ++h) {
         // P half h: column col -> tile m (col/64)*128 + 64h + col%64
         const int ma = min(m0 + (col >> 6) * 128 + 64 * h + (col & 63), g.M - 8);
-        off[0][h][pi] = lr * g.ldp + ma;
+        off[0][h][pi] = static_cast<uint32_t>(lr * g.ldp + ma) * 2u;
         // Q half h: column col -> tile n 128h + col
         const int nb = min(n0 + 128 * h + col, g.N - 8);
-        off[1][h][pi] = lr * g.ldq + nb;
+        off[1][h][pi] = static_cast<uint32_t>(lr * g.ldq + nb) * 2u;
       }
     }
   }
@@ -177,8 +187,11 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
   // stage half `half` of operand ab (0 = P, 1 = Q) of the K-tile at `base` into buffer dbuf
   auto stage = [&](int ab, int half, int dbuf, const uint16_t* base) {
     uint8_t* dst = lds + tslot(dbuf, ab, half) + (2 * w) * 1024;
-    tn_glds16(base + off[ab][half][0], dst);
-    tn_glds16(base + off[ab][half][1], dst + 1024);
+    // opaque in-place "update": the offsets stay 32-bit lane registers next to
+    // the loads (hoisted, they became 64-bit pairs and a v_lshl_add_u64 per load)
+    asm volatile("" : "+v"(off[ab][half][0]), "+v"(off[ab][half][1]));
+    tn_glds16(base, off[ab][half][0], dst);
+    tn_glds16(base, off[ab][half][1], dst + 1024);
   };
 
   // ---- fragment read offsets.  Group gq = lane/16, in-group lane 4q+p: rows
@@ -214,8 +227,8 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
     const uint32_t base = lds32 + tslot(dbuf, 1, wc >> 1);
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      bfr[nt][0] = tn_frag(base + fb[nt]);
-      bfr[nt][1] = tn_frag(base + fb[nt] + 32 * 256);
+      bfr[nt][0] = tn_frag<0>(base + fb[nt]);
+      bfr[nt][1] = tn_frag<32 * 256>(base + fb[nt]);
     }
   };
   // A (P): block p (0..3) = m-tiles 2p, 2p+1: half p >> 1, column block 4wr + 2(p & 1) + mt
@@ -223,8 +236,8 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(const TnArgs g) {
     const uint32_t base = lds32 + tslot(dbuf, 0, p >> 1);
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      afr[mt][0] = tn_frag(base + fa[2 * (p & 1) + mt]);
-      afr[mt][1] = tn_frag(base + fa[2 * (p & 1) + mt] + 32 * 256);
+      afr[mt][0] = tn_frag<0>(base + fa[2 * (p & 1) + mt]);
+      afr[mt][1] = tn_frag<32 * 256>(base + fa[2 * (p & 1) + mt]);
     }
   };
 
