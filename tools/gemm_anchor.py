@@ -106,10 +106,15 @@ def tn_rows():
         dy, x = rand(T, R), rand(T, Cc)
         out = torch.empty(R, Cc, dtype=torch.bfloat16, device="cuda")
         s = linear.tn_split_factor(T, R, Cc, max_split=min(32, T // 128))
-        cands = {f"own TN ({s} splits, partials)": lambda dy=dy, x=x, s=s: ops.gemm_tn([dy], [x], s),
-                 "hipblaslt TN": lambda dy=dy, x=x, out=out: ops.lt_gemm_tn(dy, x, out, False)}
+        # the window passes its micro-batches as segments (one operand buffer per
+        # micro-batch, as the step does); one segment must stay below 2^31 elements
+        seg = 20480 if T > 20480 else T
+        dys, xs = list(dy.split(seg)), list(x.split(seg))
+        cands = {f"own TN ({s} splits, partials)": lambda dys=dys, xs=xs, s=s: ops.gemm_tn(dys, xs, s)}
+        if T == seg:  # hipBLASLt takes one operand pair
+            cands["hipblaslt TN"] = lambda dy=dy, x=x, out=out: ops.lt_gemm_tn(dy, x, out, False)
         run_row(role, T, R, Cc, cands, rounds=3, reps=2)
-        del dy, x, out
+        del dy, x, out, dys, xs
         torch.cuda.empty_cache()
 
 
