@@ -80,6 +80,26 @@ def apply_lion_args(training_args, lion_args: LionArguments):
 
 
 @dataclass
+class LegacyTrainingArguments:
+    """TrainingArguments fields that the reference's command lines pass and the
+    installed transformers dropped (``--group_by_length``, gone in transformers
+    5; /root/reference/README.md's SFT command and sft_llama2.py:53 use it):
+    accepted so those command lines still parse."""
+
+    group_by_length: bool = field(default=False, metadata={"help": "TrainingArguments flag of transformers < 5"})
+
+
+def legacy_training_arguments() -> tuple:
+    """``(LegacyTrainingArguments,)`` when the installed TrainingArguments lacks
+    one of its fields (add it to the HfArgumentParser), else ``()``."""
+    import dataclasses
+
+    names = {f.name for f in dataclasses.fields(TrainingArguments)}
+    missing = [f.name for f in dataclasses.fields(LegacyTrainingArguments) if f.name not in names]
+    return (LegacyTrainingArguments,) if missing else ()
+
+
+@dataclass
 class AsyncTrainingArguments(TrainingArguments, LionArguments):
     """HF TrainingArguments + the reference's flags (run_clm.py:73-86) + Lion knobs."""
 

@@ -45,7 +45,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from distributed_lion_pytorch_amd.models.lora import (LoraConfig, load_adapter, merge_and_unload,  # noqa: E402
                                                       print_trainable_parameters, save_adapter)
 from distributed_lion_pytorch_amd.models.registry import build_model, load_config  # noqa: E402
-from distributed_lion_pytorch_amd.trainer.async_trainer import (LionArguments, apply_lion_args,  # noqa: E402
+from distributed_lion_pytorch_amd.trainer.async_trainer import (LionArguments, apply_lion_args, legacy_training_arguments,  # noqa: E402
                                                                 build_lion, warn_unsynced)
 from distributed_lion_pytorch_amd.trainer.sft import AsyncSFTTrainer, SFTTrainer  # noqa: E402
 from distributed_lion_pytorch_amd.utils.data import (ConstantLengthDataset, PackedStream, RowSlice,  # noqa: E402
@@ -159,10 +159,13 @@ def create_datasets(tokenizer, script_args, seed):
 
 
 def main(argv=None):
-    parser = HfArgumentParser((ScriptArguments, LionArguments, TrainingArguments))
-    script_args, lion_args, training_args = parser.parse_args_into_dataclasses(args=argv)
+    legacy = legacy_training_arguments()  # --group_by_length on transformers >= 5
+    parser = HfArgumentParser((ScriptArguments, LionArguments, TrainingArguments) + legacy)
+    parsed = parser.parse_args_into_dataclasses(args=argv)
+    script_args, lion_args, training_args = parsed[:3]
     logging.basicConfig(level=logging.INFO, handlers=[logging.StreamHandler(sys.stdout)])
-    if getattr(training_args, "group_by_length", False) and script_args.packing:
+    group_by_length = parsed[3].group_by_length if legacy else getattr(training_args, "group_by_length", False)
+    if group_by_length and script_args.packing:
         raise ValueError("Cannot use both packing and group by length")
     # packing + gradient checkpointing is allowed here (the reference forbids
     # checkpointing because of a peft/trl issue, sft_llama2.py:58-59)

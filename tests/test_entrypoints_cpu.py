@@ -178,3 +178,45 @@ def test_dpo_reward_stats_keep_train_and_eval_apart(tmp_path):
     assert evals and trains
     assert all("eval_rewards/accuracies" in h and "rewards/accuracies" not in h for h in evals), evals
     assert all("rewards/accuracies" in h and "eval_rewards/accuracies" not in h for h in trains), trains
+
+
+def test_reference_readme_command_lines(tmp_path):
+    """The three launch commands of /root/reference/README.md:16-66 parse
+    unchanged (wandb reporting aside), including ``--group_by_length``, which
+    transformers 5 dropped from TrainingArguments; the SFT one also trains
+    two steps on a tiny model, and group_by_length + packing is refused as in
+    /root/reference/sft_llama2.py:53."""
+    from transformers import HfArgumentParser
+
+    import dpo_llama2
+    import run_clm
+    import sft_llama2
+    from distributed_lion_pytorch_amd.trainer.async_trainer import AsyncTrainingArguments
+
+    clm = ["--config_name", "gpt2", "--tokenizer_name", "gpt2", "--dataset_name", "openwebtext",
+           "--per_device_train_batch_size", "20", "--per_device_eval_batch_size", "24", "--do_train", "--do_eval",
+           "--output_dir", str(tmp_path / "gpt2_lion_wd_0.1"), "--report_to", "none", "--torch_dtype", "bfloat16",
+           "--gradient_accumulation_steps", "8", "--max_steps", "100000", "--warmup_steps", "2000", "--lion",
+           "--save_total_limit", "2", "--learning_rate", "0.0001", "--weight_decay", "0.1", "--async_grad"]
+    m, d, t = HfArgumentParser((run_clm.ModelArguments, run_clm.DataTrainingArguments, AsyncTrainingArguments)) \
+        .parse_args_into_dataclasses(args=clm)
+    assert t.lion and t.async_grad and t.gradient_accumulation_steps == 8 and d.dataset_name == "openwebtext"
+
+    sft = ["--output_dir", str(tmp_path / "sft"), "--max_steps", "2", "--logging_steps", "10", "--save_steps", "10",
+           "--per_device_train_batch_size", "4", "--per_device_eval_batch_size", "1",
+           "--gradient_accumulation_steps", "2", "--gradient_checkpointing", "False", "--group_by_length", "False",
+           "--learning_rate", "1e-4", "--lr_scheduler_type", "cosine", "--warmup_steps", "100",
+           "--weight_decay", "0.05", "--optim", "paged_adamw_32bit", "--bf16", "True",
+           "--remove_unused_columns", "False", "--run_name", "sft_llama2", "--report_to", "none", "--lion",
+           "--async_grad"]
+    tiny = ["--model_name", "llama-tiny", "--synthetic_data", "--synthetic_samples", "100", "--seq_length", "64",
+            "--use_cpu"]
+    sft_llama2.main(sft + tiny)
+    assert os.path.isfile(os.path.join(tmp_path, "sft", "final_checkpoint", "adapter_model.safetensors"))
+    with pytest.raises(ValueError, match="packing"):
+        sft_llama2.main([a if a != "False" or sft[i - 1] != "--group_by_length" else "True"
+                         for i, a in enumerate(sft)] + tiny)
+
+    dpo = ["--model_name_or_path", "sft/final_checkpoint", "--output_dir", "dpo", "--lion", "--async_grad"]
+    s, lion = HfArgumentParser((dpo_llama2.ScriptArguments, dpo_llama2.LionArguments)).parse_args_into_dataclasses(args=dpo)
+    assert s.lion and s.async_grad and s.model_name_or_path == "sft/final_checkpoint"
