@@ -147,8 +147,6 @@ def main():
             "tokens_per_s_before": sum(pre) / max(1, len(pre)), "tokens_per_s_after": sum(post) / max(1, len(post)),
             "final_loss": log[-1]["loss"], "steps": log}), flush=True)
     dist.destroy_process_group()
-    if os.environ.get("DLION_DEBUG_EXIT"):
-        print(f"rank {el.me} destroyed", file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":

@@ -31,7 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PRELUDE = textwrap.dedent("""
     import json, os, sys
     import torch, torch.distributed as dist
-    sys.path.insert(0, os.environ["DLION_ROOT"])
+    sys.path.insert(0, sys.argv[1])
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
@@ -48,10 +48,10 @@ EPILOGUE = textwrap.dedent("""
 def _run(body: str, timeout: int = 150) -> dict:
     from dist_utils import free_port
 
-    env = dict(os.environ, DLION_ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()),
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()),
                RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     code = PRELUDE + textwrap.dedent(body) + EPILOGUE
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout, env=env,
+    r = subprocess.run([sys.executable, "-c", code, ROOT], capture_output=True, text=True, timeout=timeout, env=env,
                        cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")]

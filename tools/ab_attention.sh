@@ -13,9 +13,9 @@ for r in $(seq 1 $R); do
     label=${lv%%=*}; lib=${lv#*=}
     d=$O/${label}_r$r
     if [ "$lib" == "default" ]; then
-      DLION_BENCH_OURS_ONLY=1 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o prof -- python3 tools/bench_attention.py "$@" > $d.log 2>&1 || { tail -5 $d.log; exit 1; }
+      timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o prof -- python3 tools/bench_attention.py --ours-only "$@" > $d.log 2>&1 || { tail -5 $d.log; exit 1; }
     else
-      DLION_LIB=$lib DLION_BENCH_OURS_ONLY=1 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o prof -- python3 tools/bench_attention.py "$@" > $d.log 2>&1 || { tail -5 $d.log; exit 1; }
+      DLION_LIB=$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o prof -- python3 tools/bench_attention.py --ours-only "$@" > $d.log 2>&1 || { tail -5 $d.log; exit 1; }
     fi
     f=$(find $d -name "*kernel_stats.csv" | head -1)
     python3 tools/attn_kernel_times.py "${label}_r$r=$f" | tee -a $O/summary.txt

@@ -25,8 +25,9 @@ def timeit(fn, reps=10):
 
 
 def main():
-    B, T, H, D = [int(x) for x in (sys.argv[1:5] if len(sys.argv) > 4 else (20, 1024, 12, 64))]
-    p = float(sys.argv[5]) if len(sys.argv) > 5 else 0.1
+    argv = [x for x in sys.argv[1:] if x != "--ours-only"]
+    B, T, H, D = [int(x) for x in (argv[0:4] if len(argv) > 3 else (20, 1024, 12, 64))]
+    p = float(argv[4]) if len(argv) > 4 else 0.1
     dev = "cuda"
     qkv = torch.randn(B, T, 3, H, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
     dout = torch.randn(B, T, H * D, device=dev, dtype=torch.bfloat16)
@@ -52,7 +53,7 @@ def main():
         with torch.no_grad():
             sdpa(False)
 
-    only_ours = os.environ.get("DLION_BENCH_OURS_ONLY") == "1"  # PMC passes: our kernels only
+    only_ours = "--ours-only" in sys.argv  # PMC passes: our kernels only
     for _ in range(5):
         res["ours_fwd"].append(timeit(ours_fwd))
         res["ours_fb"].append(timeit(ours_fb))

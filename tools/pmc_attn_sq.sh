@@ -1,12 +1,11 @@
 # SQ counters of the attention kernels at the GPT-2 shape (one 8-counter pass + one instruction-mix pass)
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp
 OUT=gpurun_out/pmc_attn_sq; rm -rf $OUT; mkdir -p $OUT
-export DLION_BENCH_OURS_ONLY=1
 i=0
 for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU" \
            "SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_WAVES SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_SCA"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d $OUT -o pmc$i --pmc $grp -- python3 tools/bench_attention.py "$@" > $OUT/log$i.txt 2>&1 || exit 1
+  timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv -d $OUT -o pmc$i --pmc $grp -- python3 tools/bench_attention.py --ours-only "$@" > $OUT/log$i.txt 2>&1 || exit 1
 done
 python3 - "$OUT" > $OUT/summary.txt <<'PY'
 import csv, glob, collections, sys
